@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident CRC32C over 4 KiB pages (Curve chunk-integrity path).
+
+Workload (BASELINE.json configs[1]): per GPU, 1024 chunk files resident in HBM
+(16 MiB data + 4 KiB metapage each, synthetic uniform-random bytes).  One
+*step* is one pass of the scan hasher over that batch:
+    page CRCs of every 4 KiB data page      (the hot kernel)
+  + metapage CRCs, 4 MiB slice CRCs (ScanMap.crc), chunk data/file CRCs
+  + per-copyset digest partials (XOR of shifted file CRCs)
+  + at N>1: all_gather of the per-copyset partials over RCCL (the only exchange)
+Multi-GPU: one process per GPU (torchrun), chunk ranges sharded by rank
+(weak scaling: every rank holds its own 1024 chunks).
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+GiB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+ALG_BYTES_PER_PAGE = 4100  # 4096 read + 4 written
+N_COPYSETS = 64
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--chunks", type=int, default=1024, help="chunks per GPU")
+    p.add_argument("--page-bytes", type=int, default=4096)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (rank 0, N=1)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--e2e-gib", type=float, default=1.0, help="pinned host buffer for the e2e leg")
+    p.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/traffic_*.json)")
+    return p.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print("[bench]", *a, flush=True)
+
+
+def cpu_baseline(pool, args, rank):
+    """Reference CPU path restated (oracle, single-stream SSE4.2 crc32q as butil
+    builds it) timed on this host over a bounded sample of the same workload:
+    whole chunks copied from HBM, hashed page by page with CRC32(page, 4096)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    sample_chunks = min(16, pool.n)
+    host = pool.data[:sample_chunks].cpu().numpy()
+    dev_crcs = pool.page_crcs[: sample_chunks * (pool.chunk_size // args.page_bytes)].cpu().numpy().view(np.uint32)
+    want = O.page_crcs(host, args.page_bytes)
+    parity = bool((want == dev_crcs).all())
+    res = {}
+    for threads, budget in ((1, args.cpu_seconds), (16, max(1.0, args.cpu_seconds / 4))):
+        nbytes, t0 = 0, time.perf_counter()
+        while True:
+            O.page_crcs(host, args.page_bytes, threads=threads)
+            nbytes += host.nbytes
+            el = time.perf_counter() - t0
+            if el >= budget:
+                break
+        res[threads] = (nbytes / GiB / el, nbytes, el)
+    v1, nb1, el1 = res[1]
+    v16, _, _ = res[16]
+    return {
+        "value": round(v1, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+        "sample": f"{sample_chunks} x 16 MiB chunks copied from HBM, CRC32(page, {args.page_bytes}) per page, "
+                  f"{nb1 / GiB:.1f} GiB hashed in {el1:.1f} s (oracle/crc32c_oracle.c oc_crc32c_sse42, "
+                  f"single-stream crc32q as butil builds it)",
+        "value_16_threads": round(v16, 3),
+        "parity_vs_device": parity,
+    }
+
+
+def e2e_leg(args, dev):
+    """Host-resident input (pinned, as chunk files pread into pinned buffers):
+    cc_page_crc_host = pinned H2D + kernel + D2H of CRCs, 2-slot overlap."""
+    from curve_amd import crc as C
+    nb = int(args.e2e_gib * GiB) // args.page_bytes * args.page_bytes
+    h = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+    h.random_(0, 256)
+    a = h.numpy()
+    C.page_crc_host(a, args.page_bytes)  # warm (staging alloc)
+    t0, reps = time.perf_counter(), 0
+    while time.perf_counter() - t0 < 2.0:
+        C.page_crc_host(a, args.page_bytes)
+        reps += 1
+    el = time.perf_counter() - t0
+    return round(reps * nb / GiB / el, 2)
+
+
+def load_traffic(args):
+    path = args.traffic_json
+    if path is None:
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_*.json")))
+        path = cands[-1] if cands else None
+    if not path or not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        t = json.load(f)
+    return t.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from curve_amd import crc as C
+    from curve_amd.scan import DevicePool, chunk_file_name, copyset_after_bytes
+
+    pb = args.page_bytes
+    chunk, meta_sz = C.CHUNK_SIZE, C.META_PAGE_SIZE
+    n = args.chunks
+    log(rank, f"world={world} chunks/gpu={n} ({n * chunk / GiB:.1f} GiB data per GPU)")
+    data = torch.empty((n, chunk), dtype=torch.uint8, device=dev)
+    data.random_(0, 256)
+    meta = torch.zeros((n, meta_sz), dtype=torch.uint8, device=dev)
+    meta[:, 0] = 2  # FORMAT_VERSION_V2 in the metapage's first byte
+    meta[:, 1:9].random_(0, 256)
+    first_id = rank * n
+    ids = list(range(first_id, first_id + n))
+    pool = DevicePool(data, meta, ids, page_bytes=pb)
+
+    # copyset geometry over the WHOLE pool (all ranks): chunk id -> copyset id % 64
+    total = n * world
+    names_all = [chunk_file_name(i) for i in range(total)]
+    group_all = [i % N_COPYSETS for i in range(total)]
+    file_size = chunk + meta_sz
+    after_all = [0] * total
+    for g in range(N_COPYSETS):
+        members = [i for i in range(total) if group_all[i] == g]
+        aft = copyset_after_bytes([names_all[i] for i in members], [file_size] * len(members))
+        for i, a in zip(members, aft):
+            after_all[i] = a
+    after = torch.tensor(after_all[first_id:first_id + n], dtype=torch.int64, device=dev)
+    group = torch.tensor(group_all[first_id:first_id + n], dtype=torch.int32, device=dev)
+    digest = torch.zeros(N_COPYSETS, dtype=torch.int32, device=dev)
+    gathered = torch.zeros(world * N_COPYSETS, dtype=torch.int32, device=dev) if world > 1 else None
+
+    stream = torch.cuda.current_stream()
+    ev = []
+
+    def step(timed):
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        pool.hash_pages()
+        if timed:
+            e1.record(stream)
+            ev.append((e0, e1))
+        C.page_crc(pool.meta, meta_sz, out=pool.meta_crcs[:n])
+        C.fold(pool.page_crcs, C.SCAN_SIZE // pb, pb, out=pool.slice_crcs)
+        C.fold(pool.slice_crcs, chunk // C.SCAN_SIZE, C.SCAN_SIZE, out=pool.data_crcs)
+        C.combine_dev(pool.meta_crcs[:n], pool.data_crcs, chunk, out=pool.file_crcs)
+        digest.zero_()
+        C.digest_dev(pool.file_crcs, after, group, N_COPYSETS, out=digest)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, digest)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    # verify pass (after the timed region): every page must match
+    cnt = torch.tensor([0, -1], dtype=torch.int64, device=dev)
+    ve0, ve1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ve0.record(stream)
+    C.page_verify(pool.data, pool.page_crcs, pb, counters=cnt)
+    ve1.record(stream)
+    torch.cuda.synchronize()
+    verify_ms = ve0.elapsed_time(ve1)
+    bad = int(cnt[0].item())
+
+    n_pages = n * chunk // pb
+    per_step_bytes = n * chunk * world
+    value = per_step_bytes * args.steps / GiB / el
+    achieved = n_pages * ALG_BYTES_PER_PAGE / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(args)
+
+    out = {
+        "metric": "GiB/s CRC32C over 4KiB pages (device-resident) + % HBM roofline, 1/2/4/8 GPU",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (uniform random bytes generated in HBM)",
+        "config": {"workload": f"{n} x 16 MiB chunk files per GPU (+4 KiB metapages), 4 KiB pages: "
+                               "page CRC + 4 MiB slice fold + file CRC + per-copyset digest"
+                               + (" + RCCL all_gather of digests" if world > 1 else ""),
+                   "chunks_per_gpu": n, "page_bytes": pb, "copysets": N_COPYSETS,
+                   "parallelism": f"chunk-range shard x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "page_crc_kernel<16,0>", "kernel_ms_avg": round(kern_ms, 4),
+                     "alg_bytes_per_launch": n_pages * ALG_BYTES_PER_PAGE,
+                     "traffic_source": traffic_src},
+        "verify": {"GiBps": round(n * chunk / GiB / (verify_ms * 1e-3), 2), "bad_pages": bad},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(pool, args, rank)
+    if rank == 0 and world == 1 and not args.no_e2e:
+        out["e2e_pinned_GiBps"] = e2e_leg(args, dev)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

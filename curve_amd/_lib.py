@@ -1,0 +1,87 @@
+"""ctypes binding of libcurvecrc.so (include/curve_crc.h).
+
+The library is built in-tree (curve_amd/libcurvecrc.so, `make -C curve_amd/csrc`)
+and loaded from there; if it is missing, importing any device entry point raises
+-- there is deliberately no CPU fallback for the device path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcurvecrc.so")
+CSRC = os.path.join(_HERE, "csrc")
+
+CC_OK = 0
+CC_EINVAL = -22
+CC_ENODEV = -19
+CC_ENOMEM = -12
+CC_EHIP = -5
+CC_ECORRUPT = -74
+
+# every symbol include/curve_crc.h declares: (name, restype, argtypes)
+_u32, _u64, _sz, _vp, _int = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int
+
+
+class CcOpts(ctypes.Structure):
+    _fields_ = [("page_bytes", _u32), ("slice_bytes", _u32), ("staging_bytes", _u64)]
+
+
+SIGNATURES = {
+    "crc32c_value": (_u32, [_vp, _sz]),
+    "crc32c_extend": (_u32, [_u32, _vp, _sz]),
+    "crc32c_combine": (_u32, [_u32, _u32, _u64]),
+    "crc32c_shift": (_u32, [_u32, _u64]),
+    "crc32c_zeros": (_u32, [_u64]),
+    "cc_fold_host": (_u32, [_vp, _u64, _u64]),
+    "cc_engine_init": (_int, [ctypes.POINTER(CcOpts)]),
+    "cc_engine_fini": (_int, []),
+    "cc_device_count": (_int, []),
+    "cc_strerror": (ctypes.c_char_p, [_int]),
+    "cc_version": (ctypes.c_char_p, []),
+    "cc_page_crc_dev": (_int, [_vp, _u64, _u32, _vp, _vp]),
+    "cc_page_verify_dev": (_int, [_vp, _u64, _u32, _vp, _vp, _vp, _vp]),
+    "cc_fold_dev": (_int, [_vp, _u64, _u32, _u64, _vp, _vp]),
+    "cc_shift_dev": (_int, [_vp, _vp, _u64, _vp, _vp]),
+    "cc_combine_dev": (_int, [_vp, _vp, _u64, _u64, _vp, _vp]),
+    "cc_digest_dev": (_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
+    "cc_page_crc_host": (_int, [_vp, _u64, _u32, _vp]),
+    "cc_lds_image": (_int, [_vp, _sz]),
+}
+
+_lib = None
+
+
+class CurveCrcError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = _lib.cc_strerror(code).decode() if _lib is not None else str(code)
+        super().__init__(f"{what}: {msg} ({code})" if what else f"{msg} ({code})")
+
+
+def build(arch: str = "gfx950") -> str:
+    subprocess.run(["make", "-s", "-C", CSRC, f"ARCH={arch}"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    """The loaded libcurvecrc; raises OSError (loudly) if it was never built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} missing: build it with `make -C {CSRC}` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != CC_OK:
+        raise CurveCrcError(rc, what)

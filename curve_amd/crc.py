@@ -1,0 +1,228 @@
+"""Host-side mirror of the reference's CRC32C surface.
+
+`CRC32` mirrors curve::common::CRC32 (src/common/crc32.h:40-55): the two
+overloads become one function with an optional leading `crc`.  Device batch
+operations work on torch CUDA tensors (device memory + the current stream are
+plumbing; the compute is libcurvecrc's HIP kernels) and raise `CurveCrcError`
+on any failure -- there is no CPU fallback for them.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Union
+
+from . import _lib
+from ._lib import CurveCrcError, check, lib
+
+PAGE_SIZE = 4096                # conf/chunkserver.conf:22 (blocksize / page)
+CHUNK_SIZE = 16 * 1024 * 1024   # conf/chunkserver.conf:13
+META_PAGE_SIZE = 4096           # conf/chunkserver.conf:16
+SCAN_SIZE = 4 * 1024 * 1024     # conf/chunkserver.conf:114
+
+
+def _host_buf(data):
+    if isinstance(data, (bytes, bytearray)):
+        b = bytes(data)
+        return ctypes.c_char_p(b), len(b), b
+    if isinstance(data, memoryview):
+        b = data.tobytes()
+        return ctypes.c_char_p(b), len(b), b
+    try:  # numpy array
+        import numpy as np
+        if isinstance(data, np.ndarray):
+            a = np.ascontiguousarray(data)
+            return ctypes.c_void_p(a.ctypes.data), a.nbytes, a
+    except ImportError:  # pragma: no cover
+        pass
+    if isinstance(data, str):
+        b = data.encode()
+        return ctypes.c_char_p(b), len(b), b
+    raise TypeError(f"unsupported buffer type {type(data)!r}")
+
+
+def CRC32(*args) -> int:
+    """CRC32(data) == curve::common::CRC32(pData, iLen)           (crc32.h:40-42)
+       CRC32(crc, data) == curve::common::CRC32(crc, pData, iLen)  (crc32.h:53-55)
+    CPU primitive for small buffers (metapage headers, conf-epoch, ...)."""
+    if len(args) == 1:
+        crc, data = 0, args[0]
+    elif len(args) == 2:
+        crc, data = args
+    else:
+        raise TypeError("CRC32(data) or CRC32(crc, data)")
+    p, n, _keep = _host_buf(data)
+    return int(lib().crc32c_extend(int(crc) & 0xFFFFFFFF, p, n))
+
+
+def combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    return int(lib().crc32c_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, int(len_b)))
+
+
+def shift(crc: int, nbytes: int) -> int:
+    return int(lib().crc32c_shift(crc & 0xFFFFFFFF, int(nbytes)))
+
+
+def zeros(nbytes: int) -> int:
+    return int(lib().crc32c_zeros(int(nbytes)))
+
+
+def fold_host(page_crcs, page_bytes: int) -> int:
+    import numpy as np
+    a = np.ascontiguousarray(page_crcs, dtype=np.uint32)
+    return int(lib().cc_fold_host(ctypes.c_void_p(a.ctypes.data), a.size, int(page_bytes)))
+
+
+def device_count() -> int:
+    return int(lib().cc_device_count())
+
+
+def engine_init(page_bytes: int = 0, slice_bytes: int = 0, staging_bytes: int = 0) -> None:
+    o = _lib.CcOpts(page_bytes, slice_bytes, staging_bytes)
+    check(lib().cc_engine_init(ctypes.byref(o)), "cc_engine_init")
+
+
+def engine_fini() -> None:
+    check(lib().cc_engine_fini(), "cc_engine_fini")
+
+
+# ---------------------------------------------------------------------------
+# device batch operations (torch tensors as device-memory handles)
+# ---------------------------------------------------------------------------
+def _torch():
+    import torch
+    return torch
+
+
+def _stream_handle(stream) -> Optional[int]:
+    torch = _torch()
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _dev_ptr(t, what: str):
+    if not t.is_cuda:
+        raise CurveCrcError(_lib.CC_EINVAL, f"{what} must be a device tensor")
+    if not t.is_contiguous():
+        raise CurveCrcError(_lib.CC_EINVAL, f"{what} must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _nbytes(t) -> int:
+    return t.numel() * t.element_size()
+
+
+def page_crc(pages, page_bytes: int = PAGE_SIZE, out=None, stream=None):
+    """CRC32C of every `page_bytes` page of the device tensor `pages` (any dtype,
+    contiguous, size a multiple of page_bytes) -> int32 tensor of CRC bits
+    (uint32 values viewed as int32; `.view(torch.uint32)` / `& 0xFFFFFFFF` to read)."""
+    torch = _torch()
+    nb = _nbytes(pages)
+    if nb % page_bytes:
+        raise CurveCrcError(_lib.CC_EINVAL, "pages size is not a multiple of page_bytes")
+    n = nb // page_bytes
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=pages.device)
+    elif out.numel() < n or out.element_size() != 4:
+        raise CurveCrcError(_lib.CC_EINVAL, "out too small or not 32-bit")
+    with torch.cuda.device(pages.device):
+        check(lib().cc_page_crc_dev(_dev_ptr(pages, "pages"), n, page_bytes, _dev_ptr(out, "out"),
+                                    _stream_handle(stream)), "cc_page_crc_dev")
+    return out
+
+
+def page_verify(pages, expected, page_bytes: int = PAGE_SIZE, stream=None, counters=None):
+    """Recompute and compare.  Returns a 2-element int64 device tensor
+    [bad_count, first_bad] (first_bad = 2^64-1 -> -1 when clean); no host sync."""
+    torch = _torch()
+    nb = _nbytes(pages)
+    if nb % page_bytes:
+        raise CurveCrcError(_lib.CC_EINVAL, "pages size is not a multiple of page_bytes")
+    n = nb // page_bytes
+    if expected.numel() < n or expected.element_size() != 4:
+        raise CurveCrcError(_lib.CC_EINVAL, "expected must hold one 32-bit CRC per page")
+    if counters is None:
+        counters = torch.tensor([0, -1], dtype=torch.int64, device=pages.device)
+    base = counters.data_ptr()
+    with torch.cuda.device(pages.device):
+        check(lib().cc_page_verify_dev(_dev_ptr(pages, "pages"), n, page_bytes, _dev_ptr(expected, "expected"),
+                                       ctypes.c_void_p(base), ctypes.c_void_p(base + 8),
+                                       _stream_handle(stream)), "cc_page_verify_dev")
+    return counters
+
+
+def fold(crcs, per_group: int, unit_bytes: int, out=None, stream=None):
+    """Group fold on device: out[g] = CRC of the concatenation of `per_group`
+    consecutive units (each `unit_bytes`) given their CRCs."""
+    torch = _torch()
+    n = crcs.numel()
+    if per_group <= 0 or n % per_group:
+        raise CurveCrcError(_lib.CC_EINVAL, "crcs count is not a multiple of per_group")
+    g = n // per_group
+    if out is None:
+        out = torch.empty(g, dtype=torch.int32, device=crcs.device)
+    with torch.cuda.device(crcs.device):
+        check(lib().cc_fold_dev(_dev_ptr(crcs, "crcs"), g, per_group, int(unit_bytes), _dev_ptr(out, "out"),
+                                _stream_handle(stream)), "cc_fold_dev")
+    return out
+
+
+def shift_dev(crcs, shift_bytes, out=None, stream=None):
+    """out[i] = shift(crcs[i], shift_bytes[i]) on device (int64 shift counts)."""
+    torch = _torch()
+    n = crcs.numel()
+    if shift_bytes.numel() != n or shift_bytes.element_size() != 8:
+        raise CurveCrcError(_lib.CC_EINVAL, "shift_bytes must be int64, one per crc")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=crcs.device)
+    with torch.cuda.device(crcs.device):
+        check(lib().cc_shift_dev(_dev_ptr(crcs, "crcs"), _dev_ptr(shift_bytes, "shift_bytes"), n,
+                                 _dev_ptr(out, "out"), _stream_handle(stream)), "cc_shift_dev")
+    return out
+
+
+def combine_dev(a, b, len_b: int, out=None, stream=None):
+    """out[i] = combine(a[i], b[i], len_b) on device."""
+    torch = _torch()
+    n = a.numel()
+    if b.numel() != n:
+        raise CurveCrcError(_lib.CC_EINVAL, "a / b length mismatch")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=a.device)
+    with torch.cuda.device(a.device):
+        check(lib().cc_combine_dev(_dev_ptr(a, "a"), _dev_ptr(b, "b"), int(len_b), n, _dev_ptr(out, "out"),
+                                   _stream_handle(stream)), "cc_combine_dev")
+    return out
+
+
+def digest_dev(file_crcs, after_bytes, group, n_groups: int, out=None, stream=None):
+    """Per-copyset digest partials: out[group[i]] ^= shift(file_crcs[i], after_bytes[i])."""
+    torch = _torch()
+    n = file_crcs.numel()
+    if after_bytes.numel() != n or group.numel() != n:
+        raise CurveCrcError(_lib.CC_EINVAL, "file_crcs / after_bytes / group length mismatch")
+    if out is None:
+        out = torch.zeros(n_groups, dtype=torch.int32, device=file_crcs.device)
+    with torch.cuda.device(file_crcs.device):
+        check(lib().cc_digest_dev(_dev_ptr(file_crcs, "file_crcs"), _dev_ptr(after_bytes, "after_bytes"),
+                                  _dev_ptr(group, "group"), n, _dev_ptr(out, "out"), _stream_handle(stream)),
+              "cc_digest_dev")
+    return out
+
+
+def page_crc_host(data, page_bytes: int = PAGE_SIZE):
+    """Host in / host out (blocking): numpy uint8 buffer -> numpy uint32 CRCs."""
+    import numpy as np
+    a = np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    if a.nbytes % page_bytes:
+        raise CurveCrcError(_lib.CC_EINVAL, "size is not a multiple of page_bytes")
+    n = a.nbytes // page_bytes
+    out = np.empty(n, dtype=np.uint32)
+    check(lib().cc_page_crc_host(ctypes.c_void_p(a.ctypes.data), n, page_bytes,
+                                 ctypes.c_void_p(out.ctypes.data)), "cc_page_crc_host")
+    return out
+
+
+def as_u32(t) -> "list[int]":
+    """Device/host int32 CRC tensor -> python ints in [0, 2^32)."""
+    return [int(x) & 0xFFFFFFFF for x in t.detach().cpu().tolist()]

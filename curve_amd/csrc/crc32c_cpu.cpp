@@ -1,0 +1,113 @@
+// curve_amd/csrc/crc32c_cpu.cpp -- the CPU side of the C ABI: the CRC32C
+// primitive that replaces curve::common::CRC32 (src/common/crc32.h:40-55) for
+// small, latency-bound buffers (metapage header CRC, chunkserver_chunkfile.cpp:86;
+// conf-epoch CRC, conf_epoch_file.cpp:148-164; ...) plus the GF(2) combine
+// algebra.  Bulk page data goes to the GPU (engine.cpp); this file is not a
+// fallback for it.
+//
+// Large buffers run three independent crc32q streams (the x86 crc32 instruction
+// has 3-cycle latency, 1/cycle throughput) and merge them with x^(8n) mod P
+// multiplications; results are bit-identical to butil's single stream.
+#include <nmmintrin.h>
+#include <string.h>
+
+#include "../../include/curve_crc.h"
+#include "gf2.h"
+
+namespace {
+
+constexpr size_t kBlock = 4096;  // bytes per stream per round in the 3-way loop
+
+// x^(8*kBlock) and x^(16*kBlock) as 4x256 byte tables: shift-by-constant
+// in 4 lookups instead of a 32-step multiply.
+struct ShiftTables {
+    uint32_t t1[4][256];  // register * x^(8*kBlock)
+    uint32_t t2[4][256];  // register * x^(16*kBlock)
+    ShiftTables() {
+        const uint32_t m1 = cc::xpow(8ull * kBlock);
+        const uint32_t m2 = cc::xpow(16ull * kBlock);
+        for (int k = 0; k < 4; k++)
+            for (uint32_t b = 0; b < 256; b++) {
+                t1[k][b] = cc::mulmod(m1, b << (8 * k));
+                t2[k][b] = cc::mulmod(m2, b << (8 * k));
+            }
+    }
+    static inline uint32_t apply(const uint32_t (&t)[4][256], uint32_t r) {
+        return t[0][r & 0xFF] ^ t[1][(r >> 8) & 0xFF] ^ t[2][(r >> 16) & 0xFF] ^ t[3][r >> 24];
+    }
+};
+const ShiftTables& shift_tables() {
+    static const ShiftTables s;
+    return s;
+}
+
+inline uint64_t load64(const unsigned char* p) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    return v;
+}
+
+// raw register update over [p, p+n)
+uint32_t raw_update(uint32_t reg, const unsigned char* p, size_t n) {
+    uint64_t l = reg;
+    while (n && (reinterpret_cast<uintptr_t>(p) & 7u)) {
+        l = _mm_crc32_u8(static_cast<uint32_t>(l), *p++);
+        n--;
+    }
+    if (n >= 3 * kBlock) {
+        const ShiftTables& st = shift_tables();
+        while (n >= 3 * kBlock) {
+            uint64_t a = l, b = 0, c = 0;
+            const unsigned char* pa = p;
+            const unsigned char* pb = p + kBlock;
+            const unsigned char* pc = p + 2 * kBlock;
+            for (size_t i = 0; i < kBlock; i += 8) {
+                a = _mm_crc32_u64(a, load64(pa + i));
+                b = _mm_crc32_u64(b, load64(pb + i));
+                c = _mm_crc32_u64(c, load64(pc + i));
+            }
+            l = ShiftTables::apply(st.t2, static_cast<uint32_t>(a)) ^
+                ShiftTables::apply(st.t1, static_cast<uint32_t>(b)) ^ static_cast<uint32_t>(c);
+            p += 3 * kBlock;
+            n -= 3 * kBlock;
+        }
+    }
+    while (n >= 8) {
+        l = _mm_crc32_u64(l, load64(p));
+        p += 8;
+        n -= 8;
+    }
+    while (n--) l = _mm_crc32_u8(static_cast<uint32_t>(l), *p++);
+    return static_cast<uint32_t>(l);
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t crc32c_extend(uint32_t crc, const void* p, size_t n) {
+    return ~raw_update(~crc, static_cast<const unsigned char*>(p), n);
+}
+
+uint32_t crc32c_value(const void* p, size_t n) { return crc32c_extend(0, p, n); }
+
+uint32_t crc32c_shift(uint32_t crc, uint64_t nbytes) { return cc::shift_bytes(crc, nbytes); }
+
+uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
+    return cc::shift_bytes(crc_a, len_b) ^ crc_b;
+}
+
+uint32_t crc32c_zeros(uint64_t nbytes) {
+    // V(0^n) = ~shift(~0, n)
+    return ~cc::shift_bytes(0xFFFFFFFFu, nbytes);
+}
+
+uint32_t cc_fold_host(const uint32_t* page_crcs, uint64_t n, uint64_t page_bytes) {
+    if (n == 0) return 0;
+    const uint32_t m = cc::xpow(page_bytes << 3);
+    uint32_t acc = page_crcs[0];
+    for (uint64_t i = 1; i < n; i++) acc = cc::mulmod(m, acc) ^ page_crcs[i];
+    return acc;
+}
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+// curve_amd/csrc/kernels.h -- internal launcher interface between engine.hip
+// (C ABI, device contexts) and kernels.hip (gfx950 kernels).  Not exported.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cc {
+
+// LDS image geometry of the page kernel (see DESIGN.md "LDS image").
+constexpr uint32_t kLdsBytes = 163840;  // all 160 KiB of a CU's LDS
+constexpr uint32_t kFinBase = 131072;   // per-lane final-shift nibble tables
+constexpr uint32_t kWordsPerWaveStep = 64;  // one dword per lane per step
+constexpr uint32_t kWaveBytes = 256;        // bytes consumed per wave step
+constexpr int kWavesPerBlock = 16;
+constexpr int kBlockThreads = 64 * kWavesPerBlock;
+
+// Host builder of the 160 KiB LDS image (engine.hip).
+void build_lds_image(uint32_t* image /* kLdsBytes/4 words */);
+
+struct PageLaunch {
+    const uint32_t* pages;
+    uint64_t n_pages;
+    uint32_t words_per_lane;  // page_bytes / 256
+    const void* image;        // device copy of the LDS image
+    uint32_t kconst;          // V-domain correction for this page size
+    uint32_t* out;            // compute: CRC per page
+    const uint32_t* expected; // verify: expected CRC per page
+    unsigned long long* bad_count;
+    unsigned long long* first_bad;
+    int blocks;
+};
+
+hipError_t launch_page_crc(const PageLaunch& a, hipStream_t s);
+hipError_t launch_page_verify(const PageLaunch& a, hipStream_t s);
+
+struct FoldLaunch {
+    const uint32_t* crcs;
+    uint64_t n_groups;
+    uint32_t per_group;
+    uint32_t m_unit;      // x^(8*unit_bytes) mod P
+    uint32_t m_tree[7];   // x^(8*unit_bytes*q*2^t), t=0..5 (fast path, q = per_group/64)
+    uint32_t* out;
+};
+hipError_t launch_fold(const FoldLaunch& a, hipStream_t s);
+
+// x^(2^k) mod P table for the shift kernel, uploaded once per device.
+hipError_t upload_x2k(const uint32_t* t64);
+
+hipError_t launch_shift(const uint32_t* crcs, const uint64_t* shift_bytes, uint64_t n,
+                        uint32_t* out, hipStream_t s);
+
+hipError_t launch_combine(const uint32_t* a, const uint32_t* b, uint32_t m_len_b, uint64_t n, uint32_t* out,
+                          hipStream_t s);
+
+hipError_t launch_digest(const uint32_t* crcs, const uint64_t* after_bytes, const uint32_t* group, uint64_t n,
+                         uint32_t* digest, hipStream_t s);
+
+}  // namespace cc

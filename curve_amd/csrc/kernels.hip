@@ -1,0 +1,332 @@
+// curve_amd/csrc/kernels.hip -- hand-written gfx950 (CDNA4) kernels for the
+// per-page CRC32C hot path.  Bandwidth-bound integer GF(2) work: no MFMA.
+//
+// Page kernel (one wavefront per page, grid-stride over pages)
+// ------------------------------------------------------------
+// A page of P = 256*M bytes is M steps of one coalesced 256-byte wave load:
+// lane l holds dwords w[l + 64 j], j = 0..M-1.  In the raw (zero-init) CRC
+// domain the page register is XOR_i F^(n-i)(w_i), F = "multiply by x^32 mod P"
+// (feeding one dword).  Lane l runs a Horner chain with the 256-byte jump
+// G = F^64:   s = w[l]; s = G(s) ^ w[l + 64 j]   (j = 1..M-1)
+// which leaves s = XOR_j F^(64(M-1-j)) w_j, so lane l's share of the page
+// register is F^(64-l)(s) -- independent of M.  The wave XOR-reduces the 64
+// shares and adds the length constant K(P) = ~shift(~0, P) to get V(page).
+//
+// G is applied with 4 byte lookups per dword from LDS tables replicated 32x
+// so that lane l always reads bank (l mod 32): every ds_read_b32 is
+// conflict-free (2 LDS cycles per wave instruction).  The address of a lookup
+// is ONE v_perm_b32 that splices {lane slot, state byte k, region} into a
+// dword.  F^(64-l) is lane-specific: 8 nibble lookups into per-lane tables
+// (bank = lane mod 32 again).  Layout: DESIGN.md "LDS image".
+//
+// Reference being replaced: the CRC32(buf, size) loop of the scan hasher
+// (src/chunkserver/op_request.cpp:794, :847) and of the chunk/copyset hashers
+// (src/chunkserver/datastore/chunkserver_chunkfile.cpp:805,
+// src/chunkserver/copyset_node.cpp:964), all of which call
+// curve::common::CRC32 (src/common/crc32.h:40-55).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace cc {
+namespace {
+
+constexpr uint32_t kPolyDev = 0x82F63B78u;
+
+__device__ __forceinline__ uint32_t lds_u32(const uint32_t* tab, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + byte_addr);
+}
+
+// One application of G = x^(32*64) mod P to the 32-bit state s.
+// c0 = lane slot (region 0), c1 = lane slot | region 1 (bit 16).
+__device__ __forceinline__ uint32_t apply_g(const uint32_t* tab, uint32_t s, uint32_t c0, uint32_t c1) {
+    // v_perm_b32 selector bytes: [0] = c.byte0 (lane*4), [1] = s.byte_k,
+    // [2] = c.byte2 (region), [3] = 0x00.
+    const uint32_t a0 = __builtin_amdgcn_perm(c0, s, 0x0C060004u);
+    const uint32_t a1 = __builtin_amdgcn_perm(c0, s, 0x0C060104u);
+    const uint32_t a2 = __builtin_amdgcn_perm(c1, s, 0x0C060204u);
+    const uint32_t a3 = __builtin_amdgcn_perm(c1, s, 0x0C060304u);
+    const uint32_t t0 = lds_u32(tab, a0);
+    const uint32_t t1 = lds_u32(tab, a1 + 128u);
+    const uint32_t t2 = lds_u32(tab, a2);
+    const uint32_t t3 = lds_u32(tab, a3 + 128u);
+    return t0 ^ t1 ^ t2 ^ t3;
+}
+
+// Lane-specific final shift F^(64-l) via 8 nibble lookups.  cf = kFinBase + 4*lane.
+__device__ __forceinline__ uint32_t apply_fin(const uint32_t* tab, uint32_t s, uint32_t cf) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int n = 0; n < 8; n++) {
+        const uint32_t v = (s >> (4 * n)) & 15u;
+        r ^= lds_u32(tab, ((v << 8) | cf) + 4096u * n);
+    }
+    return r;
+}
+
+// XOR over the 64 lanes, result wave-uniform (SGPR).
+__device__ __forceinline__ uint32_t wave_xor(uint32_t r) {
+    r ^= __builtin_amdgcn_mov_dpp(r, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    r ^= __builtin_amdgcn_mov_dpp(r, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    r ^= __builtin_amdgcn_mov_dpp(r, 0x124, 0xF, 0xF, false);  // row_ror:4
+    r ^= __builtin_amdgcn_mov_dpp(r, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return __builtin_amdgcn_readlane(r, 0) ^ __builtin_amdgcn_readlane(r, 16) ^
+           __builtin_amdgcn_readlane(r, 32) ^ __builtin_amdgcn_readlane(r, 48);
+}
+
+__device__ __forceinline__ void fill_lds(uint32_t* tab, const uint4* __restrict__ image) {
+    uint4* t4 = reinterpret_cast<uint4*>(tab);
+#pragma unroll 2
+    for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kBlockThreads) t4[i] = image[i];
+    __syncthreads();
+}
+
+template <int M>
+__device__ __forceinline__ void load_page(uint32_t (&w)[M], const uint32_t* __restrict__ p) {
+#pragma unroll
+    for (int j = 0; j < M; j++) w[j] = __builtin_nontemporal_load(p + 64 * j);
+    // keep the whole page's loads ahead of the chain that follows (the
+    // machine scheduler otherwise sinks them into it, shrinking the prefetch)
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int M>
+__device__ __forceinline__ uint32_t chain(const uint32_t* tab, const uint32_t (&w)[M], uint32_t c0, uint32_t c1) {
+    uint32_t s = w[0];
+#pragma unroll
+    for (int j = 1; j < M; j++) s = apply_g(tab, s, c0, c1) ^ w[j];
+    return s;
+}
+
+template <int MODE>
+__device__ __forceinline__ void emit(uint32_t crc, uint64_t page, uint32_t lane, uint32_t* __restrict__ out,
+                                     const uint32_t* __restrict__ expected,
+                                     unsigned long long* __restrict__ bad_count,
+                                     unsigned long long* __restrict__ first_bad) {
+    if (MODE == 0) {
+        if (lane == 0) out[page] = crc;
+    } else {
+        const uint32_t want = expected[page];
+        if (crc != want && lane == 0) {
+            atomicAdd(bad_count, 1ull);
+            atomicMin(first_bad, (unsigned long long)page);
+        }
+    }
+}
+
+// MODE 0: compute CRCs into out[]; MODE 1: verify against expected[].
+// Two register buffers ping-pong so the next page's 16 loads are in flight
+// while the current page is hashed; loads are unconditional (the index is
+// clamped to the last page) so hipcc can count vmcnt exactly.
+template <int M, int MODE>
+__global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
+    const uint32_t* __restrict__ pages, uint64_t n_pages, const uint4* __restrict__ image,
+    uint32_t kconst, uint32_t* __restrict__ out, const uint32_t* __restrict__ expected,
+    unsigned long long* __restrict__ bad_count, unsigned long long* __restrict__ first_bad) {
+    __shared__ uint32_t tab[kLdsBytes / 4];
+    fill_lds(tab, image);
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+    uint64_t page = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+    if (page >= n_pages) return;
+    const uint64_t last = n_pages - 1;
+    const uint32_t c0 = lane << 2 & 0x7Cu;
+    const uint32_t c1 = c0 | 0x10000u;
+    const uint32_t cf = kFinBase + (lane << 2);
+    const uint32_t* base = pages + lane;
+
+    uint32_t A[M], B[M];
+    load_page<M>(A, base + page * (64u * M));
+    for (;;) {
+        const uint64_t p1 = page + stride;
+        load_page<M>(B, base + (p1 < last ? p1 : last) * (64u * M));
+        emit<MODE>(wave_xor(apply_fin(tab, chain<M>(tab, A, c0, c1), cf)) ^ kconst, page, lane, out, expected,
+                   bad_count, first_bad);
+        if (p1 >= n_pages) break;
+        const uint64_t p2 = p1 + stride;
+        load_page<M>(A, base + (p2 < last ? p2 : last) * (64u * M));
+        emit<MODE>(wave_xor(apply_fin(tab, chain<M>(tab, B, c0, c1), cf)) ^ kconst, p1, lane, out, expected,
+                   bad_count, first_bad);
+        if (p2 >= n_pages) break;
+        page = p2;
+    }
+}
+
+// Any M (page_bytes = 256*M): no register prefetch, dynamic chain length.
+template <int MODE>
+__global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
+    const uint32_t* __restrict__ pages, uint64_t n_pages, uint32_t M, const uint4* __restrict__ image,
+    uint32_t kconst, uint32_t* __restrict__ out, const uint32_t* __restrict__ expected,
+    unsigned long long* __restrict__ bad_count, unsigned long long* __restrict__ first_bad) {
+    __shared__ uint32_t tab[kLdsBytes / 4];
+    fill_lds(tab, image);
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint32_t c0 = lane << 2 & 0x7Cu;
+    const uint32_t c1 = c0 | 0x10000u;
+    const uint32_t cf = kFinBase + (lane << 2);
+    for (uint64_t page = (uint64_t)blockIdx.x * kWavesPerBlock + wave; page < n_pages; page += stride) {
+        const uint32_t* p = pages + page * (64ull * M) + lane;
+        uint32_t s = p[0];
+        for (uint32_t j = 1; j < M; j++) s = apply_g(tab, s, c0, c1) ^ p[64ull * j];
+        emit<MODE>(wave_xor(apply_fin(tab, s, cf)) ^ kconst, page, lane, out, expected, bad_count, first_bad);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// GF(2) helpers for the fold / shift kernels (tiny volume: 4 B per page).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mulmod_dev(uint32_t a, uint32_t b) {
+    uint32_t prod = 0;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        prod ^= b & (0u - ((a >> (31 - i)) & 1u));
+        b = (b >> 1) ^ (kPolyDev & (0u - (b & 1u)));
+    }
+    return prod;
+}
+
+struct X2k {
+    uint32_t t[64];
+};
+__constant__ X2k c_x2k;  // x^(2^k) mod P, uploaded once per device by engine.hip
+
+__device__ __forceinline__ uint32_t xpow_dev(uint64_t n) {
+    uint32_t r = 0x80000000u;
+    for (int k = 0; n; k++, n >>= 1)
+        if (n & 1u) r = mulmod_dev(r, c_x2k.t[k]);
+    return r;
+}
+
+// Fast path: per_group = 64*q.  One wave per group; lane l folds units
+// [l*q, (l+1)*q) by Horner, then a 6-level shuffle tree merges lanes.
+__global__ __launch_bounds__(256) void fold_kernel_wave(const uint32_t* __restrict__ crcs, uint64_t n_groups,
+                                                        uint32_t per_group, FoldLaunch a,
+                                                        uint32_t* __restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= n_groups) return;
+    const uint32_t q = per_group >> 6;
+    const uint32_t* p = crcs + g * per_group + (uint64_t)lane * q;
+    uint32_t s = p[0];
+    for (uint32_t i = 1; i < q; i++) s = mulmod_dev(a.m_unit, s) ^ p[i];
+#pragma unroll
+    for (int t = 0; t < 6; t++) {
+        const uint32_t other = __shfl_down(s, 1u << t, 64);
+        if ((lane & ((2u << t) - 1u)) == 0) s = mulmod_dev(a.m_tree[t], s) ^ other;
+    }
+    if (lane == 0) out[g] = s;
+}
+
+// Generic path: one thread per group, serial combine.
+__global__ void fold_kernel_serial(const uint32_t* __restrict__ crcs, uint64_t n_groups, uint32_t per_group,
+                                   uint32_t m_unit, uint32_t* __restrict__ out) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_groups) return;
+    const uint32_t* p = crcs + g * per_group;
+    uint32_t s = per_group ? p[0] : 0u;
+    for (uint32_t i = 1; i < per_group; i++) s = mulmod_dev(m_unit, s) ^ p[i];
+    out[g] = s;
+}
+
+__global__ void shift_kernel(const uint32_t* __restrict__ crcs, const uint64_t* __restrict__ nbytes, uint64_t n,
+                             uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = crcs[i];
+    const uint64_t nb = nbytes[i];
+    out[i] = (c == 0u || nb == 0u) ? c : mulmod_dev(xpow_dev(nb << 3), c);
+}
+
+__global__ void combine_kernel(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t m,
+                               uint64_t n, uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = mulmod_dev(m, a[i]) ^ b[i];
+}
+
+__global__ void digest_kernel(const uint32_t* __restrict__ crcs, const uint64_t* __restrict__ after,
+                              const uint32_t* __restrict__ group, uint64_t n, uint32_t* __restrict__ digest) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = crcs[i];
+    const uint64_t nb = after[i];
+    const uint32_t v = (c == 0u || nb == 0u) ? c : mulmod_dev(xpow_dev(nb << 3), c);
+    atomicXor(digest + group[i], v);
+}
+
+template <int MODE>
+hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
+    const dim3 grid(a.blocks), block(kBlockThreads);
+    const uint4* img = static_cast<const uint4*>(a.image);
+#define CC_CASE(MM)                                                                                     \
+    case MM:                                                                                            \
+        hipLaunchKernelGGL((page_crc_kernel<MM, MODE>), grid, block, 0, s, a.pages, a.n_pages, img,    \
+                           a.kconst, a.out, a.expected, a.bad_count, a.first_bad);                      \
+        break;
+    switch (a.words_per_lane) {
+        CC_CASE(1)
+        CC_CASE(2)
+        CC_CASE(4)
+        CC_CASE(8)
+        CC_CASE(16)
+        CC_CASE(32)
+        default:
+            hipLaunchKernelGGL((page_crc_kernel_dyn<MODE>), grid, block, 0, s, a.pages, a.n_pages,
+                               a.words_per_lane, img, a.kconst, a.out, a.expected, a.bad_count, a.first_bad);
+    }
+#undef CC_CASE
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_page_crc(const PageLaunch& a, hipStream_t s) { return launch_page<0>(a, s); }
+hipError_t launch_page_verify(const PageLaunch& a, hipStream_t s) { return launch_page<1>(a, s); }
+
+hipError_t launch_fold(const FoldLaunch& a, hipStream_t s) {
+    if (a.n_groups == 0) return hipSuccess;
+    if (a.per_group >= 64 && a.per_group % 64 == 0) {
+        const uint64_t blocks = (a.n_groups + 3) / 4;
+        hipLaunchKernelGGL(fold_kernel_wave, dim3((uint32_t)blocks), dim3(256), 0, s, a.crcs, a.n_groups,
+                           a.per_group, a, a.out);
+    } else {
+        const uint64_t blocks = (a.n_groups + 255) / 256;
+        hipLaunchKernelGGL(fold_kernel_serial, dim3((uint32_t)blocks), dim3(256), 0, s, a.crcs, a.n_groups,
+                           a.per_group, a.m_unit, a.out);
+    }
+    return hipGetLastError();
+}
+
+hipError_t upload_x2k(const uint32_t* t64) { return hipMemcpyToSymbol(HIP_SYMBOL(c_x2k), t64, sizeof(X2k)); }
+
+hipError_t launch_shift(const uint32_t* crcs, const uint64_t* shift_bytes, uint64_t n, uint32_t* out,
+                        hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(shift_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, crcs, shift_bytes, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_combine(const uint32_t* a, const uint32_t* b, uint32_t m_len_b, uint64_t n, uint32_t* out,
+                          hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(combine_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a, b, m_len_b, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_digest(const uint32_t* crcs, const uint64_t* after_bytes, const uint32_t* group, uint64_t n,
+                         uint32_t* digest, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(digest_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, crcs, after_bytes, group, n, digest);
+    return hipGetLastError();
+}
+
+}  // namespace cc

@@ -1,0 +1,153 @@
+"""Scan-service / hash surfaces of the chunkserver, on the device engine.
+
+Mirrors, with the reference's names and semantics:
+  ScanMap                        proto/scan.proto:23-31
+  ScanChunkRequest::OnApply      src/chunkserver/op_request.cpp:769-820 (slice CRC -> ScanMap)
+  ScanManager slice schedule     src/chunkserver/scan_manager.cpp:250-283 (metapage op + data slices)
+  CSChunkFile::GetHash           src/chunkserver/datastore/chunkserver_chunkfile.cpp:785-811
+  CopysetNode::GetHash           src/chunkserver/copyset_node.cpp:925-975
+Data lives in HBM as a `DevicePool`: one [n_chunks, chunk_size] data tensor and
+one [n_chunks, meta_page_size] metapage tensor (a chunk file is
+metapage || data, chunkserver_chunkfile.cpp:497-536).  All arithmetic is in
+libcurvecrc's kernels; torch only owns the memory and the stream.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+from . import crc as C
+
+CHUNK_SIZE = C.CHUNK_SIZE
+META_PAGE_SIZE = C.META_PAGE_SIZE
+SCAN_SIZE = C.SCAN_SIZE
+PAGE_SIZE = C.PAGE_SIZE
+
+
+@dataclass(frozen=True)
+class ScanMap:
+    """proto/scan.proto:23-31 (all fields required)."""
+    logicalPoolId: int
+    copysetId: int
+    chunkId: int
+    index: int
+    crc: int
+    offset: int
+    len: int
+
+
+def chunk_file_name(chunk_id: int, snap_sn: Optional[int] = None) -> str:
+    """FileNameOperator (src/chunkserver/datastore/filename_operator.h:55-62)."""
+    return f"chunk_{chunk_id}" if snap_sn is None else f"chunk_{chunk_id}_snap_{snap_sn}"
+
+
+def copyset_after_bytes(names: Sequence[str], sizes: Sequence[int]) -> List[int]:
+    """For each file (in the caller's order): bytes of the copyset's files that
+    sort after it.  CopysetNode::GetHash uses std::sort on the names
+    (lexicographic: chunk_10 < chunk_2, copyset_node.cpp:938)."""
+    order = sorted(range(len(names)), key=lambda i: names[i])
+    after = [0] * len(names)
+    acc = 0
+    for i in reversed(order):
+        after[i] = acc
+        acc += sizes[i]
+    return after
+
+
+def scan_schedule(chunk_size: int = CHUNK_SIZE, scan_size: int = SCAN_SIZE, meta_page_size: int = META_PAGE_SIZE):
+    """(readMetaPage, offset, len) for each scan op of one chunk, in ScanJobProcess
+    order; Init requires scanSize <= chunkSize and chunkSize % scanSize == 0
+    (scan_manager.cpp:43-48)."""
+    if scan_size > chunk_size or chunk_size % scan_size:
+        raise ValueError("scanSize must divide chunkSize")
+    ops = [(True, 0, meta_page_size)]
+    ops += [(False, off, scan_size) for off in range(0, chunk_size, scan_size)]
+    return ops
+
+
+class DevicePool:
+    """A device-resident set of chunk files (one copyset-agnostic batch)."""
+
+    def __init__(self, data, meta, chunk_ids: Sequence[int], page_bytes: int = PAGE_SIZE,
+                 scan_size: int = SCAN_SIZE):
+        import torch
+        self.torch = torch
+        self.data = data          # [n, chunk_size] uint8, device
+        self.meta = meta          # [n, meta_page_size] uint8, device
+        self.n = data.shape[0]
+        self.chunk_size = data.shape[1]
+        self.meta_size = meta.shape[1]
+        self.page_bytes = page_bytes
+        self.scan_size = scan_size
+        self.chunk_ids = list(chunk_ids)
+        assert len(self.chunk_ids) == self.n == meta.shape[0]
+        assert self.chunk_size % scan_size == 0 and scan_size % page_bytes == 0
+        dev = data.device
+        self.page_crcs = torch.empty(self.n * self.chunk_size // page_bytes, dtype=torch.int32, device=dev)
+        self.meta_crcs = torch.empty(self.n * max(1, self.meta_size // page_bytes), dtype=torch.int32, device=dev)
+        self.slice_crcs = torch.empty(self.n * self.chunk_size // scan_size, dtype=torch.int32, device=dev)
+        self.data_crcs = torch.empty(self.n, dtype=torch.int32, device=dev)
+        self.file_crcs = torch.empty(self.n, dtype=torch.int32, device=dev)
+
+    # -- the hot path ------------------------------------------------------
+    def hash_pages(self, stream=None):
+        C.page_crc(self.data, self.page_bytes, out=self.page_crcs, stream=stream)
+        return self.page_crcs
+
+    def scan(self, stream=None):
+        """Page CRCs -> 4 MiB slice CRCs (ScanMap.crc), metapage CRCs, chunk-data
+        and chunk-file CRCs; everything stays on the device."""
+        self.hash_pages(stream)
+        C.page_crc(self.meta, self.meta_size, out=self.meta_crcs[: self.n], stream=stream)
+        per_slice = self.scan_size // self.page_bytes
+        C.fold(self.page_crcs, per_slice, self.page_bytes, out=self.slice_crcs, stream=stream)
+        C.fold(self.slice_crcs, self.chunk_size // self.scan_size, self.scan_size, out=self.data_crcs, stream=stream)
+        C.combine_dev(self.meta_crcs[: self.n], self.data_crcs, self.chunk_size, out=self.file_crcs, stream=stream)
+        return self.slice_crcs
+
+    def verify(self, expected_page_crcs, stream=None):
+        return C.page_verify(self.data, expected_page_crcs, self.page_bytes, stream=stream)
+
+    # -- reference surfaces built on the device results ----------------------
+    def scan_maps(self, logical_pool_id: int, copyset_id: int, first_index: int = 0) -> List[ScanMap]:
+        """ScanMaps as ScanChunkRequest::OnApply builds them (op_request.cpp:795-803),
+        one per scan op in ScanJobProcess order; `index` is the raft log index,
+        here a running counter from first_index."""
+        slices = C.as_u32(self.slice_crcs)
+        metas = C.as_u32(self.meta_crcs[: self.n])
+        per_chunk = self.chunk_size // self.scan_size
+        out, idx = [], first_index
+        for c, cid in enumerate(self.chunk_ids):
+            out.append(ScanMap(logical_pool_id, copyset_id, cid, idx, metas[c], 0, self.meta_size))
+            idx += 1
+            for k in range(per_chunk):
+                out.append(ScanMap(logical_pool_id, copyset_id, cid, idx, slices[c * per_chunk + k],
+                                   k * self.scan_size, self.scan_size))
+                idx += 1
+        return out
+
+    def chunk_hash(self, c: int, offset: int = 0, length: Optional[int] = None) -> str:
+        """CSChunkFile::GetHash(offset, length) over the raw FILE (metapage at file
+        offset 0), for page-aligned ranges; decimal string like std::to_string."""
+        if length is None:
+            length = self.chunk_size
+        pb = self.page_bytes
+        if offset % pb or length % pb:
+            raise ValueError("device chunk hash needs page-aligned offset/length")
+        file_pages = [("m", 0)] + [("d", i) for i in range(self.chunk_size // pb)]
+        sel = file_pages[offset // pb:(offset + length) // pb]
+        pcs = C.as_u32(self.page_crcs[c * (self.chunk_size // pb):(c + 1) * (self.chunk_size // pb)])
+        meta = C.as_u32(self.meta_crcs[c:c + 1])[0]
+        crcs = [meta if k == "m" else pcs[i] for k, i in sel]
+        import numpy as np
+        return str(C.fold_host(np.array(crcs, dtype=np.uint32), pb)) if crcs else "0"
+
+    def copyset_digest_partial(self, names: Sequence[str], after_bytes: Sequence[int], group: Sequence[int],
+                               n_groups: int, stream=None):
+        """XOR partials of the per-copyset chained hash for the files this pool
+        holds; XOR over all holders == CopysetNode::GetHash."""
+        torch = self.torch
+        dev = self.data.device
+        after = torch.tensor(list(after_bytes), dtype=torch.int64, device=dev)
+        grp = torch.tensor(list(group), dtype=torch.int32, device=dev)
+        return C.digest_dev(self.file_crcs, after, grp, n_groups, stream=stream)

@@ -1,0 +1,143 @@
+/*
+ * include/curve_crc.h -- C ABI of libcurvecrc, the MI355X-native chunk-checksum
+ * engine for Curve's per-page CRC32C integrity path.
+ *
+ * Plain C: no C++ or torch types cross this boundary; pointers + sizes only.
+ * Every entry point cites the reference interface it replaces (paths relative
+ * to the opencurve/curve tree).
+ *
+ * Conventions
+ *   - CRC values are CRC-32C (Castagnoli, reflected poly 0x82F63B78) with
+ *     butil semantics: crc32c_extend(c, A||B) == crc32c_extend(crc32c_extend(c, A), B),
+ *     crc32c_value(p, n) == crc32c_extend(0, p, n), value of the empty buffer = 0.
+ *   - Functions returning `int` return CC_OK (0) or a negative CC_E* code.
+ *   - `*_dev` calls take caller-owned device memory on the calling thread's
+ *     current HIP device, enqueue on `stream` (a hipStream_t, NULL = default
+ *     stream) and return without synchronising.  They never fall back to the
+ *     CPU: with no usable GPU they return CC_ENODEV.
+ */
+#ifndef CURVE_CRC_H_
+#define CURVE_CRC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CC_OK 0
+#define CC_EINVAL (-22)   /* bad argument (size, alignment, null pointer) */
+#define CC_ENODEV (-19)   /* no HIP device / device code unavailable */
+#define CC_ENOMEM (-12)   /* device or pinned-host allocation failed */
+#define CC_EHIP (-5)      /* a HIP runtime call failed */
+#define CC_ECORRUPT (-74) /* verify found mismatching pages (host verify) */
+
+/* ------------------------------------------------------------------------
+ * CPU primitive -- drop-in for the inline header src/common/crc32.h
+ * ------------------------------------------------------------------------ */
+
+/* Replaces curve::common::CRC32(const char*, size_t)  (src/common/crc32.h:40-42)
+ * = butil::crc32c::Value.  Also nebd::common::CRC32 (nebd/src/common/crc32.h). */
+uint32_t crc32c_value(const void* p, size_t n);
+
+/* Replaces curve::common::CRC32(uint32_t, const char*, size_t) (src/common/crc32.h:53-55)
+ * = butil::crc32c::Extend.  Pure, reentrant, any length/alignment. */
+uint32_t crc32c_extend(uint32_t crc, const void* p, size_t n);
+
+/* GF(2) algebra (new; needed to derive the reference digests from page CRCs).
+ * crc32c_combine(V(A), V(B), |B|) == V(A||B)  (zlib crc32_combine identity).
+ * crc32c_shift(c, n) multiplies the 32-bit register by x^(8n) mod P. */
+uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+uint32_t crc32c_shift(uint32_t crc, uint64_t nbytes);
+/* V(n zero bytes); e.g. crc32c_zeros(4096) == 0x98F94189, the CRC of every page
+ * of a freshly formatted pool chunk (src/tools/curve_format_main.cpp:132). */
+uint32_t crc32c_zeros(uint64_t nbytes);
+
+/* Fold n page CRCs (each over page_bytes) into the CRC of their concatenation. */
+uint32_t cc_fold_host(const uint32_t* page_crcs, uint64_t n, uint64_t page_bytes);
+
+/* ------------------------------------------------------------------------
+ * Engine lifetime -- created next to ScanManager::Init and torn down at
+ * ChunkServer::Fini (src/chunkserver/chunkserver.cpp:298-303, :455).
+ * Optional: device calls initialise per-device state lazily.
+ * ------------------------------------------------------------------------ */
+typedef struct cc_opts {
+    uint32_t page_bytes;     /* default 4096 (conf/chunkserver.conf:22 blocksize) */
+    uint32_t slice_bytes;    /* default 4 MiB (copyset.scan_size_byte, conf/chunkserver.conf:114) */
+    uint64_t staging_bytes;  /* pinned host staging per device for *_host calls, default 256 MiB */
+} cc_opts;
+
+int cc_engine_init(const cc_opts* opts);  /* NULL = defaults */
+int cc_engine_fini(void);
+int cc_device_count(void);
+const char* cc_strerror(int code);
+const char* cc_version(void);
+
+/* ------------------------------------------------------------------------
+ * Device batch calls -- the hot path (replace the CRC32() loops of the scan
+ * hasher, op_request.cpp:794/:847, and of the chunk/copyset hashers,
+ * chunkserver_chunkfile.cpp:805, copyset_node.cpp:964).
+ * ------------------------------------------------------------------------ */
+
+/* d_out[i] = crc32c_value(d_pages + i*page_bytes, page_bytes).
+ * page_bytes: multiple of 256, 256..1 MiB.  d_pages 4-byte aligned. */
+int cc_page_crc_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes,
+                    uint32_t* d_out, void* stream);
+
+/* Recompute and compare against d_expected.  *d_bad_count += mismatches;
+ * *d_first_bad = min(*d_first_bad, first mismatching page index).  The caller
+ * zeroes d_bad_count and sets d_first_bad to UINT64_MAX before the call. */
+int cc_page_verify_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes,
+                       const uint32_t* d_expected, uint64_t* d_bad_count,
+                       uint64_t* d_first_bad, void* stream);
+
+/* Group fold: d_out[g] = CRC of the concatenation of units g*per_group ..
+ * g*per_group+per_group-1, each unit_bytes long, from their CRCs d_crcs.
+ * E.g. 1024 page CRCs -> one 4 MiB ScanMap.crc (proto/scan.proto:28). */
+int cc_fold_dev(const uint32_t* d_crcs, uint64_t n_groups, uint32_t per_group,
+                uint64_t unit_bytes, uint32_t* d_out, void* stream);
+
+/* Linear-domain digest contributions (per-copyset digest):
+ * d_out[i] = crc32c_shift(d_crcs[i], d_shift_bytes[i]).  XOR of contributions
+ * plus a length-only constant reproduces CopysetNode::GetHash's chain. */
+int cc_shift_dev(const uint32_t* d_crcs, const uint64_t* d_shift_bytes, uint64_t n,
+                 uint32_t* d_out, void* stream);
+
+/* d_out[i] = crc32c_combine(d_a[i], d_b[i], len_b): e.g. a chunk FILE's CRC from
+ * its metapage CRC and its 16 MiB data CRC (the file is metapage || data,
+ * chunkserver_chunkfile.cpp:497-536 reads data at offset + metaPageSize). */
+int cc_combine_dev(const uint32_t* d_a, const uint32_t* d_b, uint64_t len_b, uint64_t n,
+                   uint32_t* d_out, void* stream);
+
+/* Per-copyset digest partials: for each file i,
+ *   d_digest[d_group[i]] ^= crc32c_shift(d_file_crcs[i], d_after_bytes[i])
+ * where d_after_bytes[i] = bytes of the copyset's files that sort after file i
+ * (CopysetNode::GetHash chains files in std::sort name order, copyset_node.cpp:938).
+ * The XOR is order-free, so ranks holding disjoint file sets produce partials
+ * whose XOR is exactly the reference's chained copyset hash.  d_digest is
+ * caller-zeroed. */
+int cc_digest_dev(const uint32_t* d_file_crcs, const uint64_t* d_after_bytes,
+                  const uint32_t* d_group, uint64_t n_files, uint32_t* d_digest,
+                  void* stream);
+
+/* ------------------------------------------------------------------------
+ * Host-in / host-out convenience (blocking; thread-safe: one internal
+ * submission lock + pinned staging ring per device).  Starts and ends in host
+ * memory like the reference's datastore read path (chunkserver_chunkfile.cpp:497-536).
+ * ------------------------------------------------------------------------ */
+int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
+                     uint32_t* h_out);
+
+/* ------------------------------------------------------------------------
+ * Diagnostics (new; no reference counterpart)
+ * ------------------------------------------------------------------------ */
+/* Copy the 163840-byte LDS image the page kernel loads into every CU (G tables
+ * + per-lane final maps, DESIGN.md "LDS image") so host tests can replay the
+ * kernel's arithmetic on the CPU.  Needs no GPU. */
+int cc_lds_image(void* out, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CURVE_CRC_H_ */

@@ -1,0 +1,118 @@
+"""Generate tests/golden/*.json fixtures (committed; rerun to regenerate).
+
+Two kinds of vectors:
+  * known answers copied (as data) from the reference's own tests -- these PIN
+    the oracle: RFC 3720 B.4 (test/common/crc32_test.cpp:49-84), Extend identity
+    (:90-93), copyset hash 1355371765 (test/chunkserver/copyset_node_test.cpp:811-835),
+    conf-epoch CRC 599727352 (test/chunkserver/conf_epoch_file_test.cpp:103-106);
+  * vectors computed by the oracle AFTER it reproduces the pinned ones, cross-
+    checked by an independent pure-Python bitwise CRC where small enough.
+
+Usage:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import json
+import os
+import struct
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+from oracle import oracle as O  # noqa: E402
+
+RFC_PDU = [0x01, 0xc0, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00,
+           0x14, 0x00, 0x00, 0x00, 0x00, 0x00, 0x04, 0x00, 0x00, 0x00, 0x00, 0x14, 0x00, 0x00, 0x00, 0x18,
+           0x28, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x02, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00]
+
+COPYSET_FILES = {  # copyset_node_test.cpp:811-835 (echo adds '\n'; dd bs=512 count=15)
+    "test-1.txt": "wwwww\n",
+    "test-2.txt": "abcddddddddd333\n",
+    "test-3.txt": None,  # 7680 zero bytes
+    "test-4.txt": "mmmmmmmm\n",
+    "test-5.txt": "eeeeeeeeeee\n",
+}
+
+
+def copyset_bytes():
+    return {k: (bytes(7680) if v is None else v.encode()) for k, v in COPYSET_FILES.items()}
+
+
+def metapage_v2(sn: int = 1, corrected_sn: int = 0, page_size: int = 4096) -> bytes:
+    """ChunkFileMetaPage::encode for a non-clone chunk (chunkserver_chunkfile.cpp:64-88):
+    version(u8)=2 sn(u64) correctedSn(u64) loc_size(size_t=0), CRC32 of those 25 B at byte 25."""
+    hdr = struct.pack("<BQQQ", 2, sn, corrected_sn, 0)
+    assert len(hdr) == 25
+    crc = O.crc32c(hdr)
+    page = bytearray(page_size)
+    page[:25] = hdr
+    page[25:29] = struct.pack("<I", crc)
+    return bytes(page)
+
+
+def synthetic_chunk(seed: int):
+    data = O.splitmix64_bytes(seed, O.CHUNK_SIZE)
+    return metapage_v2(), data
+
+
+def main():
+    g = {}
+    # ---- pinned known answers (reference test data) ----
+    g["rfc3720"] = [
+        {"input": "zeros32", "crc": 0x8a9136aa},
+        {"input": "ff32", "crc": 0x62a8ab43},
+        {"input": "inc32", "crc": 0x46dd794e},
+        {"input": "dec32", "crc": 0x113fdb5c},
+        {"input_hex": bytes(RFC_PDU).hex(), "crc": 0xd9963a56},
+    ]
+    g["extend"] = {"a": "hello ", "b": "world"}
+    g["copyset_hash"] = {"files": COPYSET_FILES, "zero_file_bytes": 7680, "hash": "1355371765"}
+    g["conf_epoch"] = {"logicPoolId": 123, "copysetId": 1345, "epoch": 0,
+                       "magic": 0x6225929368674119, "crc": 599727352}
+    # verify the oracle reproduces them before deriving anything else
+    assert O.copyset_hash(copyset_bytes()) == g["copyset_hash"]["hash"]
+    assert O.conf_epoch_crc(123, 1345, 0) == 599727352
+    assert O.crc32c(bytes(32)) == 0x8a9136aa
+
+    # ---- derived vectors ----
+    g["zero_page"] = {"bytes": 4096, "crc": O.crc32c(bytes(4096))}
+    assert g["zero_page"]["crc"] == O.crc32c_py(bytes(4096)) == 0x98F94189
+
+    pages = O.splitmix64_bytes(0x5EED, 64 * 4096)
+    crcs = O.page_crcs(pages, 4096)
+    g["seeded_pages"] = {"generator": "splitmix64", "seed": 0x5EED, "page_bytes": 4096, "n_pages": 64,
+                         "crcs": [int(c) for c in crcs]}
+    for i in (0, 17, 63):
+        assert O.crc32c_py(pages[i * 4096:(i + 1) * 4096].tobytes()) == crcs[i]
+
+    # 512-B pages (blocksize 512 is allowed, conf/chunkserver.conf:17-22)
+    p512 = O.splitmix64_bytes(0x512, 64 * 512)
+    g["seeded_pages_512"] = {"generator": "splitmix64", "seed": 0x512, "page_bytes": 512, "n_pages": 64,
+                             "crcs": [int(c) for c in O.page_crcs(p512, 512)]}
+
+    # one synthetic 16 MiB chunk: slices, metapage, chunk hash, page CRCs
+    meta, data = synthetic_chunk(0xC0FFEE)
+    raw = meta + data.tobytes()
+    slices = O.scan_slices(meta, data.tobytes())
+    pc = O.page_crcs(data, 4096)
+    pc.astype("<u4").tofile(os.path.join(HERE, "chunk_c0ffee_pages.u32"))
+    g["chunk_c0ffee"] = {
+        "generator": "splitmix64", "seed": 0xC0FFEE, "chunk_bytes": O.CHUNK_SIZE,
+        "metapage": {"version": 2, "sn": 1, "correctedSn": 0, "crc": O.crc32c(meta)},
+        "scan_slices": [{"offset": o, "len": n, "crc": c} for (o, n, c) in slices],
+        "chunk_hash_0_chunksize": O.chunk_hash(raw, 0, O.CHUNK_SIZE),
+        "chunk_hash_4096_8192": O.chunk_hash(raw, 4096, 8192),
+        "whole_file_crc": O.crc32c(raw),
+        "page_crcs_file": "chunk_c0ffee_pages.u32",
+        "page_crcs_crc": O.crc32c(pc.astype("<u4").tobytes()),
+    }
+
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(g, f, indent=1)
+    print("wrote", os.path.join(HERE, "golden.json"))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,89 @@
+"""CPU replay of the page kernel's arithmetic (curve_amd/csrc/kernels.hip).
+
+Uses the exact LDS image the library uploads (cc_lds_image), forms every LDS
+address the way the kernel does (v_perm_b32 byte splice, immediate offsets),
+runs the per-lane Horner chain, the lane-specific nibble final map and the
+wave XOR-reduce.  Lets the CPU suite pin the table math and the address
+layout; only instruction semantics remain for the GPU tests.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+K_LDS_BYTES = 163840
+K_FIN_BASE = 131072
+
+
+def lds_image() -> np.ndarray:
+    from curve_amd import _lib
+    img = np.zeros(K_LDS_BYTES // 4, dtype=np.uint32)
+    rc = _lib.lib().cc_lds_image(ctypes.c_void_p(img.ctypes.data), K_LDS_BYTES)
+    assert rc == 0
+    return img
+
+
+def v_perm_b32(s0: np.ndarray, s1: np.ndarray, sel: int) -> np.ndarray:
+    """V_PERM_B32: D.byte[i] = byte sel.byte[i] of the 64-bit {S0:S1}
+    (0-3 -> S1 bytes, 4-7 -> S0 bytes, 12 -> 0x00); only selectors the kernel uses."""
+    s0 = s0.astype(np.uint64)
+    s1 = s1.astype(np.uint64)
+    out = np.zeros(np.broadcast(s0, s1).shape, dtype=np.uint64)
+    for i in range(4):
+        b = (sel >> (8 * i)) & 0xFF
+        if b < 4:
+            v = (s1 >> np.uint64(8 * b)) & np.uint64(0xFF)
+        elif b < 8:
+            v = (s0 >> np.uint64(8 * (b - 4))) & np.uint64(0xFF)
+        elif b == 12:
+            v = np.zeros_like(out)
+        else:
+            raise NotImplementedError(hex(b))
+        out |= v << np.uint64(8 * i)
+    return out.astype(np.uint32)
+
+
+def lds_read(img: np.ndarray, byte_addr: np.ndarray) -> np.ndarray:
+    a = byte_addr.astype(np.int64)
+    assert (a % 4 == 0).all() and (a >= 0).all() and (a < K_LDS_BYTES).all()
+    return img[a // 4]
+
+
+def page_crcs_model(pages: np.ndarray, page_bytes: int, img: np.ndarray | None = None) -> np.ndarray:
+    """Replay the kernel over `pages` (uint8, n*page_bytes) -> uint32 CRCs."""
+    from curve_amd import crc as C
+    if img is None:
+        img = lds_image()
+    M = page_bytes // 256
+    words = np.ascontiguousarray(pages).view(np.uint32).reshape(-1, M, 64)  # [page, j, lane]
+    lane = np.arange(64, dtype=np.uint32)
+    c0 = (lane << 2) & np.uint32(0x7C)
+    c1 = c0 | np.uint32(0x10000)
+    cf = np.uint32(K_FIN_BASE) + (lane << 2)
+    s = words[:, 0, :].copy()
+    for j in range(1, M):
+        t0 = lds_read(img, v_perm_b32(c0, s, 0x0C060004))
+        t1 = lds_read(img, v_perm_b32(c0, s, 0x0C060104) + 128)
+        t2 = lds_read(img, v_perm_b32(c1, s, 0x0C060204))
+        t3 = lds_read(img, v_perm_b32(c1, s, 0x0C060304) + 128)
+        s = t0 ^ t1 ^ t2 ^ t3 ^ words[:, j, :]
+    r = np.zeros_like(s)
+    for n in range(8):
+        v = (s >> np.uint32(4 * n)) & np.uint32(15)
+        r ^= lds_read(img, ((v << np.uint32(8)) | cf) + np.uint32(4096 * n))
+    red = np.bitwise_xor.reduce(r, axis=1)
+    return red ^ np.uint32(C.zeros(page_bytes))
+
+
+def bank_conflicts(byte_addrs: np.ndarray) -> int:
+    """Extra LDS cycles of one ds_read_b32 wave instruction (64 lane addresses),
+    per the gfx950 rule: lane groups {0-31},{32-63}, bank = (a/4) mod 32,
+    identical addresses broadcast."""
+    extra = 0
+    for g in (byte_addrs[:32], byte_addrs[32:]):
+        banks = {}
+        for a in g.tolist():
+            banks.setdefault((a // 4) % 32, set()).add(a)
+        extra += max(len(v) for v in banks.values()) - 1
+    return extra

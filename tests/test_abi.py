@@ -1,0 +1,65 @@
+"""The C-ABI library loads and exports every symbol include/*.h declares
+(no compute calls that need a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def declared_symbols():
+    names = set()
+    inc = os.path.join(ROOT, "include")
+    for fn in os.listdir(inc):
+        if not fn.endswith(".h"):
+            continue
+        txt = open(os.path.join(inc, fn)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b([a-z_][a-z0-9_]*)\s*\(", txt, re.M):
+            if m.group(1) not in ("if", "sizeof"):
+                names.add(m.group(1))
+    return names
+
+
+def test_header_parses():
+    names = declared_symbols()
+    for must in ("crc32c_value", "crc32c_extend", "cc_page_crc_dev", "cc_page_verify_dev",
+                 "cc_fold_dev", "cc_page_crc_host", "cc_engine_init", "cc_engine_fini"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from curve_amd import _lib
+    L = _lib.lib()
+    missing = [n for n in sorted(declared_symbols()) if not hasattr(L, n)]
+    assert not missing, missing
+    # and the python binding describes every one of them
+    assert declared_symbols() <= set(_lib.SIGNATURES)
+
+
+def test_no_gpu_fails_loudly_here():
+    """Without a device the device entry points return CC_ENODEV (never a CPU fallback)."""
+    from curve_amd import _lib
+    L = _lib.lib()
+    if L.cc_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    buf = ctypes.create_string_buffer(4096)
+    out = ctypes.create_string_buffer(4)
+    assert L.cc_page_crc_dev(buf, 1, 4096, out, None) == _lib.CC_ENODEV
+    assert L.cc_page_crc_host(buf, 1, 4096, out) == _lib.CC_ENODEV
+    assert L.cc_engine_init(None) == _lib.CC_ENODEV
+
+
+def test_argument_checks_need_no_gpu():
+    from curve_amd import _lib
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(4096)
+    out = ctypes.create_string_buffer(4)
+    assert L.cc_page_crc_dev(buf, 1, 100, out, None) == _lib.CC_EINVAL   # not a multiple of 256
+    assert L.cc_page_crc_dev(buf, 1, 0, out, None) == _lib.CC_EINVAL
+    assert L.cc_page_crc_dev(None, 1, 4096, out, None) == _lib.CC_EINVAL
+    assert L.cc_page_crc_dev(buf, 0, 4096, out, None) == _lib.CC_OK       # empty batch is a no-op
+    assert L.cc_lds_image(None, 0) == _lib.CC_EINVAL
+    assert L.cc_strerror(_lib.CC_ENODEV) == b"no usable HIP device"

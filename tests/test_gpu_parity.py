@@ -1,0 +1,245 @@
+"""GPU parity tests: libcurvecrc's HIP path vs the oracle, bit-exact.
+
+Small/medium cases compare every CRC with the oracle; full-size cases use
+size-independent properties (fold of page CRCs == CRC of the whole buffer,
+verify of a clean pool == 0 mismatches, corruptions found exactly).
+All calls go through the C ABI (ctypes) -- never through the oracle.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from curve_amd import crc as C
+    C.engine_init()
+    return torch.device("cuda", 0)
+
+
+def u32(t):
+    return t.detach().cpu().numpy().view(np.uint32)
+
+
+def to_dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+@pytest.mark.parametrize("page_bytes", [4096, 512, 256, 768, 1024, 2048, 8192, 16384, 65536])
+@pytest.mark.parametrize("n_pages", [1, 15, 16, 17, 4097])
+def test_page_crc_random(dev, oracle, page_bytes, n_pages):
+    from curve_amd import crc as C
+    rng = np.random.default_rng(page_bytes * 131 + n_pages)
+    pages = rng.integers(0, 256, page_bytes * n_pages, dtype=np.uint8)
+    got = u32(C.page_crc(to_dev(pages, dev), page_bytes))
+    assert (got == oracle.page_crcs(pages, page_bytes)).all()
+
+
+def test_golden_seeded_pages(dev, oracle, golden):
+    from curve_amd import crc as C
+    for key in ("seeded_pages", "seeded_pages_512"):
+        s = golden[key]
+        pages = oracle.splitmix64_bytes(s["seed"], s["n_pages"] * s["page_bytes"])
+        assert [int(x) for x in u32(C.page_crc(to_dev(pages, dev), s["page_bytes"]))] == s["crcs"]
+
+
+def test_golden_chunk(dev, oracle, golden):
+    """The committed 16 MiB chunk fixture: all 4096 page CRCs, the 4 ScanMap
+    slice CRCs, metapage CRC and chunk hash, derived on the device."""
+    from golden.make_golden import synthetic_chunk
+    from curve_amd.scan import DevicePool
+    g = golden["chunk_c0ffee"]
+    meta, data = synthetic_chunk(g["seed"])
+    pool = DevicePool(to_dev(data.reshape(1, -1), dev),
+                      to_dev(np.frombuffer(meta, dtype=np.uint8).reshape(1, -1), dev), [1])
+    pool.scan()
+    pc = np.fromfile(os.path.join(os.path.dirname(__file__), "golden", g["page_crcs_file"]), dtype="<u4")
+    assert (u32(pool.page_crcs) == pc).all()
+    maps = pool.scan_maps(logical_pool_id=1, copyset_id=2)
+    assert [(m.offset, m.len, m.crc) for m in maps] == \
+        [(s["offset"], s["len"], s["crc"]) for s in g["scan_slices"]]
+    assert pool.chunk_hash(0, 0, 16 << 20) == g["chunk_hash_0_chunksize"]
+    assert pool.chunk_hash(0, 4096, 8192) == g["chunk_hash_4096_8192"]
+    assert (int(u32(pool.file_crcs)[0])) == g["whole_file_crc"]
+
+
+def test_zero_pages(dev):
+    from curve_amd import crc as C
+    z = torch.zeros(4096 * 1000, dtype=torch.uint8, device=dev)
+    assert (u32(C.page_crc(z, 4096)) == 0x98F94189).all()
+
+
+def test_unaligned_view_rejected_or_exact(dev, oracle):
+    """A 4-byte-aligned offset view works; a non-4-byte-aligned one is refused."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(5)
+    buf = rng.integers(0, 256, 4096 * 9 + 8, dtype=np.uint8)
+    d = to_dev(buf, dev)
+    got = u32(C.page_crc(d[4:4 + 4096 * 9], 4096))
+    assert (got == oracle.page_crcs(buf[4:4 + 4096 * 9], 4096)).all()
+    with pytest.raises(C.CurveCrcError):
+        C.page_crc(d[1:1 + 4096 * 9], 4096)
+
+
+def test_verify_clean_and_corrupt(dev, oracle):
+    from curve_amd import crc as C
+    rng = np.random.default_rng(11)
+    n = 3000
+    pages = rng.integers(0, 256, 4096 * n, dtype=np.uint8)
+    want = oracle.page_crcs(pages, 4096)
+    d = to_dev(pages, dev)
+    exp = to_dev(want.view(np.int32), dev)
+    cnt = C.page_verify(d, exp, 4096)
+    torch.cuda.synchronize()
+    assert int(cnt[0]) == 0 and int(cnt[1]) == -1
+    bad = [7, 1234, 2999]
+    for p in bad:
+        d[p * 4096 + 100] ^= 0x40
+    cnt = C.page_verify(d, exp, 4096)
+    torch.cuda.synchronize()
+    assert int(cnt[0]) == len(bad) and int(cnt[1]) == min(bad)
+
+
+@pytest.mark.parametrize("per_group,unit", [(1024, 4096), (64, 4096), (128, 512), (4, 4 << 20), (3, 4096), (100, 4096), (1, 4096)])
+def test_fold(dev, oracle, per_group, unit):
+    from curve_amd import crc as C
+    rng = np.random.default_rng(per_group + unit)
+    groups = 9
+    crcs = rng.integers(0, 2**32, per_group * groups, dtype=np.uint64).astype(np.uint32)
+    got = u32(C.fold(to_dev(crcs.view(np.int32), dev), per_group, unit))
+    from curve_amd.crc import fold_host
+    want = [fold_host(crcs[g * per_group:(g + 1) * per_group], unit) for g in range(groups)]
+    assert [int(x) for x in got] == want
+    # and the fold is the CRC of the concatenation (cross-check with the oracle on real data)
+    if unit == 4096 and per_group <= 128:
+        data = rng.integers(0, 256, unit * per_group, dtype=np.uint8)
+        pc = C.page_crc(to_dev(data, dev), unit)
+        assert int(u32(C.fold(pc, per_group, unit))[0]) == oracle.crc32c(data.tobytes())
+
+
+def test_shift_combine_digest(dev, oracle):
+    from curve_amd import crc as C
+    rng = np.random.default_rng(2)
+    n = 500
+    crcs = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    sh = rng.integers(0, 1 << 40, n, dtype=np.int64)
+    sh[:5] = [0, 1, 4096, 16 << 20, (16 << 20) + 4096]
+    got = u32(C.shift_dev(to_dev(crcs.view(np.int32), dev), to_dev(sh, dev)))
+    assert [int(x) for x in got] == [oracle.raw_shift(int(c), int(s)) for c, s in zip(crcs, sh)]
+    b = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    got = u32(C.combine_dev(to_dev(crcs.view(np.int32), dev), to_dev(b.view(np.int32), dev), 16 << 20))
+    assert [int(x) for x in got] == [oracle.combine(int(x), int(y), 16 << 20) for x, y in zip(crcs, b)]
+
+
+def test_copyset_digest_matches_reference_chain(dev, oracle, golden):
+    """The 5-file fixture of copyset_node_test.cpp:811-835 through the device
+    path: page CRCs (files zero-padded into 256-B pages is NOT allowed, so the
+    file CRCs come from the CPU primitive) -> digest partials split over two
+    'ranks' -> XOR == 1355371765."""
+    from conftest import copyset_files
+    from curve_amd import crc as C
+    from curve_amd.scan import copyset_after_bytes
+    files = copyset_files(golden)
+    names = list(files)
+    sizes = [len(files[k]) for k in names]
+    after = copyset_after_bytes(names, sizes)
+    fcrc = np.array([C.CRC32(files[k]) for k in names], dtype=np.uint32)
+    parts = []
+    for sel in ([0, 2, 4], [1, 3]):
+        out = C.digest_dev(to_dev(fcrc[sel].view(np.int32), dev), to_dev(np.array(after, dtype=np.int64)[sel], dev),
+                           to_dev(np.zeros(len(sel), dtype=np.int32), dev), 1)
+        parts.append(int(u32(out)[0]))
+    assert str(parts[0] ^ parts[1]) == "1355371765"
+
+
+def test_pool_digest_equals_chained_copyset_hash(dev, oracle):
+    """A small pool of real chunk files (metapage + data): the device digest
+    equals CopysetNode::GetHash's sorted-name chain computed by the oracle."""
+    from curve_amd import crc as C
+    from curve_amd.scan import DevicePool, chunk_file_name, copyset_after_bytes
+    chunk = 1 << 20  # 1 MiB chunks keep the oracle chain fast
+    n = 12
+    rng = np.random.default_rng(9)
+    data = rng.integers(0, 256, (n, chunk), dtype=np.uint8)
+    meta = rng.integers(0, 256, (n, 4096), dtype=np.uint8)
+    ids = [1, 2, 3, 10, 11, 20, 100, 5, 7, 9, 12, 21]
+    pool = DevicePool(to_dev(data, dev), to_dev(meta, dev), ids, scan_size=256 << 10)
+    pool.scan()
+    names = [chunk_file_name(i) for i in ids]
+    groups = [i % 2 for i in range(n)]
+    after = [0] * n
+    for g in (0, 1):
+        mem = [i for i in range(n) if groups[i] == g]
+        for i, a in zip(mem, copyset_after_bytes([names[i] for i in mem], [chunk + 4096] * len(mem))):
+            after[i] = a
+    dig = u32(pool.copyset_digest_partial(names, after, groups, 2))
+    for g in (0, 1):
+        files = {names[i]: meta[i].tobytes() + data[i].tobytes() for i in range(n) if groups[i] == g}
+        assert str(int(dig[g])) == oracle.copyset_hash(files)
+    # ScanMaps of every chunk vs the oracle's slice schedule
+    maps = pool.scan_maps(1, 1)
+    k = 0
+    for c in range(n):
+        ref = oracle.scan_slices(meta[c].tobytes(), data[c].tobytes(), 256 << 10)
+        for off, ln, crc in ref:
+            m = maps[k]
+            assert (m.chunkId, m.offset, m.len, m.crc) == (ids[c], off, ln, crc)
+            k += 1
+
+
+def test_host_path_pageable_and_pinned(dev, oracle):
+    from curve_amd import crc as C
+    rng = np.random.default_rng(4)
+    n = 70000  # > one staging slot (128 MiB / 4 KiB = 32768 pages) -> exercises the 2-slot ring
+    pages = rng.integers(0, 256, 4096 * n, dtype=np.uint8)
+    want = oracle.page_crcs(pages, 4096, threads=8)
+    assert (C.page_crc_host(pages, 4096) == want).all()
+    pinned = torch.from_numpy(pages).pin_memory()
+    assert (C.page_crc_host(pinned.numpy(), 4096) == want).all()
+
+
+def test_large_pool_properties(dev, oracle):
+    """Full-size-ish (2 GiB = 128 chunks): every page CRC equals the oracle's
+    (multithreaded) and the fold of all page CRCs equals the CRC of the whole buffer."""
+    from curve_amd import crc as C
+    n_chunks = 128
+    d = torch.empty((n_chunks, 16 << 20), dtype=torch.uint8, device=dev)
+    d.random_(0, 256)
+    pc = C.page_crc(d, 4096)
+    host = d.cpu().numpy()
+    assert (u32(pc) == oracle.page_crcs(host, 4096, threads=16)).all()
+    whole = C.fold(pc, pc.numel(), 4096)
+    assert int(u32(whole)[0]) == oracle.crc32c(host)
+    cnt = C.page_verify(d, pc, 4096)
+    torch.cuda.synchronize()
+    assert int(cnt[0]) == 0
+
+
+def test_streams_and_multithread_callers(dev, oracle):
+    """Device calls on side streams from several Python threads (apply-thread shape)."""
+    import threading
+    from curve_amd import crc as C
+    rng = np.random.default_rng(8)
+    bufs = [rng.integers(0, 256, 4096 * 513, dtype=np.uint8) for _ in range(4)]
+    results = [None] * 4
+
+    def work(i):
+        s = torch.cuda.Stream(device=dev)
+        with torch.cuda.stream(s):
+            d = to_dev(bufs[i], dev)
+            out = C.page_crc(d, 4096, stream=s)
+            s.synchronize()
+            results[i] = u32(out)
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    for i in range(4):
+        assert (results[i] == oracle.page_crcs(bufs[i], 4096)).all()

@@ -1,0 +1,45 @@
+"""Host-logic tests of the page kernel: replay its arithmetic on the CPU with
+the library's own LDS image and check it bit-exact against the oracle, and
+check the LDS layout is bank-conflict-free for every lookup the kernel makes."""
+import numpy as np
+import pytest
+
+import kernel_model as km
+
+
+@pytest.fixture(scope="module")
+def img():
+    return km.lds_image()
+
+
+@pytest.mark.parametrize("page_bytes", [256, 512, 1024, 4096, 8192, 3 * 256, 16384])
+def test_model_matches_oracle(oracle, img, page_bytes):
+    rng = np.random.default_rng(page_bytes)
+    pages = rng.integers(0, 256, page_bytes * 19, dtype=np.uint8)
+    assert (km.page_crcs_model(pages, page_bytes, img) == oracle.page_crcs(pages, page_bytes)).all()
+
+
+def test_model_golden_pages(oracle, golden, img):
+    s = golden["seeded_pages"]
+    pages = oracle.splitmix64_bytes(s["seed"], s["n_pages"] * s["page_bytes"])
+    assert [int(c) for c in km.page_crcs_model(pages, 4096, img)] == s["crcs"]
+
+
+def test_zero_and_ones_pages(img):
+    z = np.zeros(4096 * 3, dtype=np.uint8)
+    assert (km.page_crcs_model(z, 4096, img) == 0x98F94189).all()
+
+
+def test_lookups_bank_conflict_free():
+    lane = np.arange(64, dtype=np.uint32)
+    c0 = (lane << 2) & np.uint32(0x7C)
+    c1 = c0 | np.uint32(0x10000)
+    rng = np.random.default_rng(0)
+    for _ in range(50):
+        s = rng.integers(0, 2**32, 64, dtype=np.uint64).astype(np.uint32)
+        for c, sel, off in ((c0, 0x0C060004, 0), (c0, 0x0C060104, 128), (c1, 0x0C060204, 0), (c1, 0x0C060304, 128)):
+            assert km.bank_conflicts(km.v_perm_b32(c, s, sel) + off) == 0
+        cf = np.uint32(km.K_FIN_BASE) + (lane << 2)
+        for n in range(8):
+            v = (s >> np.uint32(4 * n)) & np.uint32(15)
+            assert km.bank_conflicts(((v << np.uint32(8)) | cf) + 4096 * n) == 0

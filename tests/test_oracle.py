@@ -1,0 +1,81 @@
+"""The oracle is pinned by the reference's own known answers before anything
+else trusts it."""
+import numpy as np
+import pytest
+
+from conftest import copyset_files, rfc_input
+
+
+@pytest.mark.parametrize("impl", ["sse42", "table", "bitwise"])
+def test_rfc3720_vectors(oracle, golden, impl):
+    # test/common/crc32_test.cpp:49-84
+    for e in golden["rfc3720"]:
+        assert oracle.crc32c(rfc_input(e), impl=impl) == e["crc"]
+
+
+def test_rfc3720_pure_python(oracle, golden):
+    for e in golden["rfc3720"]:
+        assert oracle.crc32c_py(rfc_input(e)) == e["crc"]
+
+
+def test_extend_identity(oracle, golden):
+    # test/common/crc32_test.cpp:90-93
+    a, b = golden["extend"]["a"].encode(), golden["extend"]["b"].encode()
+    assert oracle.crc32c(a + b) == oracle.crc32c(b, oracle.crc32c(a))
+
+
+def test_basic_inequalities(oracle):
+    # test/common/crc32_test.cpp:30-45
+    z10, o10, z20 = bytes(10), b"\x01" * 10, bytes(20)
+    assert oracle.crc32c(z10) == oracle.crc32c(bytes(10))
+    assert oracle.crc32c(z10) != oracle.crc32c(o10)
+    assert oracle.crc32c(z10) != oracle.crc32c(z20)
+    assert oracle.crc32c(b"a") != oracle.crc32c(b"foo")
+    assert oracle.crc32c(b"") == 0
+
+
+def test_copyset_hash_golden(oracle, golden):
+    # test/chunkserver/copyset_node_test.cpp:811-835 -> "1355371765", independent of creation order
+    files = copyset_files(golden)
+    assert oracle.copyset_hash(files) == golden["copyset_hash"]["hash"] == "1355371765"
+    rev = dict(reversed(list(files.items())))
+    assert oracle.copyset_hash(rev) == "1355371765"
+
+
+def test_conf_epoch_golden(oracle, golden):
+    # test/chunkserver/conf_epoch_file_test.cpp:103-106
+    c = golden["conf_epoch"]
+    assert oracle.conf_epoch_crc(c["logicPoolId"], c["copysetId"], c["epoch"], c["magic"]) == 599727352
+
+
+def test_combine_matrix_vs_concat(oracle):
+    rng = np.random.default_rng(7)
+    for la, lb in [(0, 5), (5, 0), (1, 1), (13, 4096), (4096, 4096 * 3 + 7)]:
+        a = rng.integers(0, 256, la, dtype=np.uint8).tobytes()
+        b = rng.integers(0, 256, lb, dtype=np.uint8).tobytes()
+        assert oracle.combine(oracle.crc32c(a), oracle.crc32c(b), lb) == oracle.crc32c(a + b)
+
+
+def test_seeded_pages_fixture(oracle, golden):
+    for key in ("seeded_pages", "seeded_pages_512"):
+        s = golden[key]
+        pages = oracle.splitmix64_bytes(s["seed"], s["n_pages"] * s["page_bytes"])
+        assert [int(c) for c in oracle.page_crcs(pages, s["page_bytes"])] == s["crcs"]
+        # multithreaded baseline path agrees
+        assert [int(c) for c in oracle.page_crcs(pages, s["page_bytes"], threads=4)] == s["crcs"]
+
+
+def test_synthetic_chunk_fixture(oracle, golden):
+    import os
+    from golden.make_golden import synthetic_chunk
+    g = golden["chunk_c0ffee"]
+    meta, data = synthetic_chunk(g["seed"])
+    assert oracle.crc32c(meta) == g["metapage"]["crc"]
+    assert [list(x) for x in oracle.scan_slices(meta, data.tobytes())] == \
+        [[s["offset"], s["len"], s["crc"]] for s in g["scan_slices"]]
+    # 5 scan ops per 16 MiB chunk at scanSize 4 MiB (scan_manager_test.cpp:107-142)
+    assert len(g["scan_slices"]) == 5
+    pc = np.fromfile(os.path.join(os.path.dirname(__file__), "golden", g["page_crcs_file"]), dtype="<u4")
+    assert (oracle.page_crcs(data, 4096) == pc).all()
+    raw = meta + data.tobytes()
+    assert oracle.chunk_hash(raw, 0, oracle.CHUNK_SIZE) == g["chunk_hash_0_chunksize"]
