@@ -112,10 +112,18 @@ inline bool page_size_ok(uint32_t page_bytes) {
 // V(page) = raw(page) ^ K(P),  K(P) = ~shift(~0, P)  == crc32c_zeros(P).
 inline uint32_t kconst_for(uint32_t page_bytes) { return ~shift_bytes(0xFFFFFFFFu, page_bytes); }
 
-int blocks_for(const DevCtx* c, uint64_t n_pages) {
-    const uint64_t need = (n_pages + kWavesPerBlock - 1) / kWavesPerBlock;
-    // exactly one 160 KiB-LDS workgroup fits per CU: launch one per CU (or fewer)
-    return (int)(need < (uint64_t)c->cus ? (need ? need : 1) : (uint64_t)c->cus);
+// Grid + tile size.  Exactly one 160 KiB-LDS workgroup fits per CU, so the
+// grid is one block per CU (or fewer for tiny batches).  Each wave owns tiles
+// of 2^ts consecutive pages (one coalesced CRC store per tile); the tile is the
+// largest power of two <= 64 that still gives every wave of the grid a tile.
+void geometry_for(const DevCtx* c, uint64_t n_pages, PageLaunch* a) {
+    const uint64_t waves = (uint64_t)c->cus * kWavesPerBlock;
+    uint32_t ts = 6;
+    while (ts > 0 && (n_pages >> ts) < waves) ts--;
+    const uint64_t tiles = (n_pages + (1ull << ts) - 1) >> ts;
+    const uint64_t need = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    a->blocks = (int)(need < (uint64_t)c->cus ? (need ? need : 1) : (uint64_t)c->cus);
+    a->tile_shift = ts;
 }
 
 int staging_init(DevCtx* c) {
@@ -239,7 +247,7 @@ int cc_page_crc_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes, 
     a.image = c->image;
     a.kconst = kconst_for(page_bytes);
     a.out = d_out;
-    a.blocks = blocks_for(c, n_pages);
+    geometry_for(c, n_pages, &a);
     return map_err(launch_page_crc(a, static_cast<hipStream_t>(stream)));
 }
 
@@ -260,7 +268,7 @@ int cc_page_verify_dev(const void* d_pages, uint64_t n_pages, uint32_t page_byte
     a.expected = d_expected;
     a.bad_count = reinterpret_cast<unsigned long long*>(d_bad_count);
     a.first_bad = reinterpret_cast<unsigned long long*>(d_first_bad);
-    a.blocks = blocks_for(c, n_pages);
+    geometry_for(c, n_pages, &a);
     return map_err(launch_page_verify(a, static_cast<hipStream_t>(stream)));
 }
 
@@ -356,7 +364,7 @@ int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
         a.image = c->image;
         a.kconst = kconst_for(page_bytes);
         a.out = st.dcrc[slot];
-        a.blocks = blocks_for(c, n);
+        geometry_for(c, n, &a);
         if ((e = launch_page_crc(a, st.stream[slot])) != hipSuccess) return map_err(e);
         if ((e = hipMemcpyAsync(st.hcrc[slot], st.dcrc[slot], n * 4, hipMemcpyDeviceToHost, st.stream[slot])) !=
             hipSuccess)

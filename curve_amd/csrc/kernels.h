@@ -28,6 +28,7 @@ struct PageLaunch {
     unsigned long long* bad_count;
     unsigned long long* first_bad;
     int blocks;
+    uint32_t tile_shift;      // 2^tile_shift consecutive pages per wave tile (0..6)
 };
 
 hipError_t launch_page_crc(const PageLaunch& a, hipStream_t s);

@@ -115,23 +115,48 @@ __device__ __forceinline__ void emit(uint32_t crc, uint64_t page, uint32_t lane,
     }
 }
 
+// Tile of 64 consecutive pages per wave: the page CRCs are gathered into one
+// register (lane k <- page k of the tile) and leave as ONE coalesced 256-byte
+// store (compute) or are compared against ONE 256-byte load of expected CRCs
+// with a ballot (verify).  Sparse 4-byte single-lane stores cost ~10 % of HBM
+// efficiency in the first version.
+template <int MODE>
+__device__ __forceinline__ void flush_tile(uint32_t acc, uint64_t tile_first, uint32_t cnt, uint32_t lane,
+                                           uint32_t* __restrict__ out, const uint32_t* __restrict__ expected,
+                                           unsigned long long* __restrict__ bad_count,
+                                           unsigned long long* __restrict__ first_bad) {
+    if (MODE == 0) {
+        if (lane < cnt) out[tile_first + lane] = acc;
+    } else {
+        const uint32_t want = lane < cnt ? expected[tile_first + lane] : acc;
+        const uint64_t bad = __ballot(want != acc);
+        if (bad && lane == 0) {
+            atomicAdd(bad_count, (unsigned long long)__popcll(bad));
+            atomicMin(first_bad, (unsigned long long)(tile_first + __ffsll((long long)bad) - 1));
+        }
+    }
+}
+
 // MODE 0: compute CRCs into out[]; MODE 1: verify against expected[].
-// Two register buffers ping-pong so the next page's 16 loads are in flight
-// while the current page is hashed; loads are unconditional (the index is
-// clamped to the last page) so hipcc can count vmcnt exactly.
+// Wave w walks tiles w, w+W, w+2W, ... (W = waves in the grid), 64 pages each;
+// its k-th page is (w + (k>>6) W)*64 + (k&63), increasing in k.  Two register
+// buffers ping-pong so the next page's loads are in flight while the current
+// page is hashed; loads are unconditional (index clamped to the last page) so
+// hipcc can count vmcnt exactly.
 template <int M, int MODE>
 __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
     const uint32_t* __restrict__ pages, uint64_t n_pages, const uint4* __restrict__ image,
     uint32_t kconst, uint32_t* __restrict__ out, const uint32_t* __restrict__ expected,
-    unsigned long long* __restrict__ bad_count, unsigned long long* __restrict__ first_bad) {
+    unsigned long long* __restrict__ bad_count, unsigned long long* __restrict__ first_bad, uint32_t tshift) {
     __shared__ uint32_t tab[kLdsBytes / 4];
     fill_lds(tab, image);
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerBlock;
-    uint64_t page = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
-    if (page >= n_pages) return;
+    const uint32_t tmask = (1u << tshift) - 1u;  // tile = 2^tshift pages (<= 64)
+    const uint64_t wstride = ((uint64_t)gridDim.x * kWavesPerBlock) << tshift;  // pages between a wave's tiles
+    const uint64_t wfirst = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) << tshift;
+    if (wfirst >= n_pages) return;
     const uint64_t last = n_pages - 1;
     const uint32_t c0 = lane << 2 & 0x7Cu;
     const uint32_t c1 = c0 | 0x10000u;
@@ -139,18 +164,31 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
     const uint32_t* base = pages + lane;
 
     uint32_t A[M], B[M];
+    uint32_t acc = 0;
+    uint64_t k = 0, page = wfirst;
     load_page<M>(A, base + page * (64u * M));
     for (;;) {
-        const uint64_t p1 = page + stride;
+        // ---- page k in A ----
+        uint64_t k1 = k + 1;
+        uint64_t p1 = wfirst + (k1 >> tshift) * wstride + (k1 & tmask);
         load_page<M>(B, base + (p1 < last ? p1 : last) * (64u * M));
-        emit<MODE>(wave_xor(apply_fin(tab, chain<M>(tab, A, c0, c1), cf)) ^ kconst, page, lane, out, expected,
-                   bad_count, first_bad);
+        uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, A, c0, c1), cf)) ^ kconst;
+        acc = lane == (uint32_t)(k & tmask) ? crc : acc;
+        if ((k & tmask) == tmask || p1 >= n_pages)
+            flush_tile<MODE>(acc, page - (k & tmask), (uint32_t)(k & tmask) + 1u, lane, out, expected, bad_count,
+                             first_bad);
         if (p1 >= n_pages) break;
-        const uint64_t p2 = p1 + stride;
+        // ---- page k1 in B ----
+        const uint64_t k2 = k1 + 1;
+        const uint64_t p2 = wfirst + (k2 >> tshift) * wstride + (k2 & tmask);
         load_page<M>(A, base + (p2 < last ? p2 : last) * (64u * M));
-        emit<MODE>(wave_xor(apply_fin(tab, chain<M>(tab, B, c0, c1), cf)) ^ kconst, p1, lane, out, expected,
-                   bad_count, first_bad);
+        crc = wave_xor(apply_fin(tab, chain<M>(tab, B, c0, c1), cf)) ^ kconst;
+        acc = lane == (uint32_t)(k1 & tmask) ? crc : acc;
+        if ((k1 & tmask) == tmask || p2 >= n_pages)
+            flush_tile<MODE>(acc, p1 - (k1 & tmask), (uint32_t)(k1 & tmask) + 1u, lane, out, expected, bad_count,
+                             first_bad);
         if (p2 >= n_pages) break;
+        k = k2;
         page = p2;
     }
 }
@@ -267,7 +305,7 @@ hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
 #define CC_CASE(MM)                                                                                     \
     case MM:                                                                                            \
         hipLaunchKernelGGL((page_crc_kernel<MM, MODE>), grid, block, 0, s, a.pages, a.n_pages, img,    \
-                           a.kconst, a.out, a.expected, a.bad_count, a.first_bad);                      \
+                           a.kconst, a.out, a.expected, a.bad_count, a.first_bad, a.tile_shift);        \
         break;
     switch (a.words_per_lane) {
         CC_CASE(1)

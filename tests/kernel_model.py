@@ -87,3 +87,38 @@ def bank_conflicts(byte_addrs: np.ndarray) -> int:
             banks.setdefault((a // 4) % 32, set()).add(a)
         extra += max(len(v) for v in banks.values()) - 1
     return extra
+
+
+def geometry(n_pages: int, cus: int = 256, waves_per_block: int = 16):
+    """engine.hip geometry_for(): (blocks, tile_shift)."""
+    waves = cus * waves_per_block
+    ts = 6
+    while ts > 0 and (n_pages >> ts) < waves:
+        ts -= 1
+    tiles = (n_pages + (1 << ts) - 1) >> ts
+    need = (tiles + waves_per_block - 1) // waves_per_block
+    blocks = need if need < cus else cus
+    return max(blocks, 1), ts
+
+
+def tile_walk(n_pages: int, blocks: int, ts: int, waves_per_block: int = 16):
+    """Replay page_crc_kernel's per-wave page sequence and flushes.
+    Returns (pages hashed in order, [(tile_first, cnt)] flushes)."""
+    hashed, flushes = [], []
+    tmask = (1 << ts) - 1
+    wstride = (blocks * waves_per_block) << ts
+    for w in range(blocks * waves_per_block):
+        wfirst = w << ts
+        if wfirst >= n_pages:
+            continue
+        k, page = 0, wfirst
+        while True:
+            hashed.append(page)
+            k1 = k + 1
+            p1 = wfirst + (k1 >> ts) * wstride + (k1 & tmask)
+            if (k & tmask) == tmask or p1 >= n_pages:
+                flushes.append((page - (k & tmask), (k & tmask) + 1))
+            if p1 >= n_pages:
+                break
+            k, page = k1, p1
+    return hashed, flushes

@@ -243,3 +243,22 @@ def test_streams_and_multithread_callers(dev, oracle):
     [t.join() for t in ts]
     for i in range(4):
         assert (results[i] == oracle.page_crcs(bufs[i], 4096)).all()
+
+
+@pytest.mark.parametrize("n_pages", [8192 + 5, 20000, 65536 + 3, 262144 + 77])
+def test_tiled_geometries(dev, oracle, n_pages):
+    """Batches large enough for 2..64-page wave tiles (coalesced CRC stores and
+    ballot verify), with a partial last tile; corruptions found exactly."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(n_pages)
+    pages = rng.integers(0, 256, 256 * n_pages, dtype=np.uint8)
+    d = to_dev(pages, dev)
+    want = oracle.page_crcs(pages, 256)
+    got = C.page_crc(d, 256)
+    assert (u32(got) == want).all()
+    bad = sorted({3, n_pages // 2, n_pages - 1, int(rng.integers(0, n_pages))})
+    for p in bad:
+        d[p * 256 + 17] ^= 1
+    cnt = C.page_verify(d, got, 256)
+    torch.cuda.synchronize()
+    assert int(cnt[0]) == len(bad) and int(cnt[1]) == bad[0]

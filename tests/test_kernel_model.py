@@ -43,3 +43,21 @@ def test_lookups_bank_conflict_free():
         for n in range(8):
             v = (s >> np.uint32(4 * n)) & np.uint32(15)
             assert km.bank_conflicts(((v << np.uint32(8)) | cf) + 4096 * n) == 0
+
+
+@pytest.mark.parametrize("n_pages", [1, 2, 63, 64, 65, 4095, 4096, 4097, 8192, 8197, 20000, 262143, 262144,
+                                     262144 + 77, 4194304 + 13])
+@pytest.mark.parametrize("cus", [256, 255, 80])
+def test_tile_walk_covers_every_page_once(n_pages, cus):
+    blocks, ts = km.geometry(n_pages, cus)
+    assert 0 <= ts <= 6 and 1 <= blocks <= cus
+    if n_pages > 300000:  # the full walk is slow in Python: check the geometry only
+        assert (n_pages >> ts) >= cus * 16 or ts == 0
+        return
+    hashed, flushes = km.tile_walk(n_pages, blocks, ts)
+    assert sorted(hashed) == list(range(n_pages))
+    covered = []
+    for first, cnt in flushes:
+        assert 1 <= cnt <= (1 << ts) and first % (1 << ts) == 0
+        covered += range(first, first + cnt)
+    assert sorted(covered) == list(range(n_pages))
