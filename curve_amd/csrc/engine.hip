@@ -118,7 +118,10 @@ inline uint32_t kconst_for(uint32_t page_bytes) { return ~shift_bytes(0xFFFFFFFF
 // largest power of two <= 64 that still gives every wave of the grid a tile.
 void geometry_for(const DevCtx* c, uint64_t n_pages, PageLaunch* a) {
     const uint64_t waves = (uint64_t)c->cus * kWavesPerBlock;
-    uint32_t ts = 6;
+#ifndef CC_MAX_TSHIFT
+#define CC_MAX_TSHIFT 6
+#endif
+    uint32_t ts = CC_MAX_TSHIFT;
     while (ts > 0 && (n_pages >> ts) < waves) ts--;
     const uint64_t tiles = (n_pages + (1ull << ts) - 1) >> ts;
     const uint64_t need = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;

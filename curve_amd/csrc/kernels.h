@@ -11,7 +11,10 @@ constexpr uint32_t kLdsBytes = 163840;  // all 160 KiB of a CU's LDS
 constexpr uint32_t kFinBase = 131072;   // per-lane final-shift nibble tables
 constexpr uint32_t kWordsPerWaveStep = 64;  // one dword per lane per step
 constexpr uint32_t kWaveBytes = 256;        // bytes consumed per wave step
-constexpr int kWavesPerBlock = 16;
+#ifndef CC_WAVES
+#define CC_WAVES 8  // waves per CU (one workgroup per CU: the LDS image fills it); 8 beat 16 by 4-5 %
+#endif
+constexpr int kWavesPerBlock = CC_WAVES;
 constexpr int kBlockThreads = 64 * kWavesPerBlock;
 
 // Host builder of the 160 KiB LDS image (engine.hip).

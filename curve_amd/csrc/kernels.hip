@@ -34,8 +34,17 @@ namespace {
 
 constexpr uint32_t kPolyDev = 0x82F63B78u;
 
+#ifndef CC_NT_LOADS
+#define CC_NT_LOADS 1
+#endif
+
 __device__ __forceinline__ uint32_t lds_u32(const uint32_t* tab, uint32_t byte_addr) {
+#if CC_LDS_B64  // diagnostic: 8-byte lookups (half unused), tests instruction- vs byte-bound LDS
+    const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(tab) + (byte_addr & ~7u));
+    return (byte_addr & 4u) ? v.y : v.x;
+#else
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + byte_addr);
+#endif
 }
 
 // One application of G = x^(32*64) mod P to the 32-bit state s.
@@ -56,6 +65,9 @@ __device__ __forceinline__ uint32_t apply_g(const uint32_t* tab, uint32_t s, uin
 
 // Lane-specific final shift F^(64-l) via 8 nibble lookups.  cf = kFinBase + 4*lane.
 __device__ __forceinline__ uint32_t apply_fin(const uint32_t* tab, uint32_t s, uint32_t cf) {
+#if CC_ABLATE == 2
+    return s ^ cf;
+#endif
     uint32_t r = 0;
 #pragma unroll
     for (int n = 0; n < 8; n++) {
@@ -85,17 +97,37 @@ __device__ __forceinline__ void fill_lds(uint32_t* tab, const uint4* __restrict_
 template <int M>
 __device__ __forceinline__ void load_page(uint32_t (&w)[M], const uint32_t* __restrict__ p) {
 #pragma unroll
-    for (int j = 0; j < M; j++) w[j] = __builtin_nontemporal_load(p + 64 * j);
+    for (int j = 0; j < M; j++) {
+#if CC_ABLATE == 3
+        w[j] = (uint32_t)(uintptr_t)(p + 64 * j) * 0x9E3779B1u;  // no memory traffic: compute ceiling
+        continue;
+#endif
+#if CC_NT_LOADS
+        w[j] = __builtin_nontemporal_load(p + 64 * j);  // read-once stream: nt (probe: +12 % read BW)
+#else
+        w[j] = p[64 * j];
+#endif
+    }
     // keep the whole page's loads ahead of the chain that follows (the
     // machine scheduler otherwise sinks them into it, shrinking the prefetch)
     __builtin_amdgcn_sched_barrier(0);
 }
 
+#ifndef CC_ABLATE
+#define CC_ABLATE 0  // diagnostic builds only: 1 = no G lookups, 2 = no final map (wrong CRCs)
+#endif
+
 template <int M>
 __device__ __forceinline__ uint32_t chain(const uint32_t* tab, const uint32_t (&w)[M], uint32_t c0, uint32_t c1) {
     uint32_t s = w[0];
 #pragma unroll
-    for (int j = 1; j < M; j++) s = apply_g(tab, s, c0, c1) ^ w[j];
+    for (int j = 1; j < M; j++) {
+#if CC_ABLATE == 1
+        s = ((s << 1) | (s >> 31)) ^ w[j];
+#else
+        s = apply_g(tab, s, c0, c1) ^ w[j];
+#endif
+    }
     return s;
 }
 
@@ -137,12 +169,68 @@ __device__ __forceinline__ void flush_tile(uint32_t acc, uint64_t tile_first, ui
     }
 }
 
+#ifndef CC_PREFETCH
+#define CC_PREFETCH 2  // wave steps in flight ahead of the one being hashed (2..4 measured equal)
+#endif
+#ifndef CC_MAX_TSHIFT
+#define CC_MAX_TSHIFT 6
+#endif
+
+// Page sequence of one wave: its k-th page is wfirst + (k >> ts) * wstride + (k & tmask),
+// strictly increasing in k.
+struct Walk {
+    uint64_t wfirst, wstride;
+    uint32_t tshift, tmask;
+    __device__ __forceinline__ uint64_t page(uint64_t k) const {
+        return wfirst + (k >> tshift) * wstride + (k & tmask);
+    }
+};
+
+#ifndef CC_PAIR
+#define CC_PAIR 1  // pages hashed together per wave step (independent chains interleave)
+#endif
+
+template <int M, int P>
+__device__ __forceinline__ void load_pages(uint32_t (&w)[P][M], const uint32_t* __restrict__ base, const Walk& W,
+                                           uint64_t k, uint64_t last) {
+#if CC_PRIO_LOADS
+    __builtin_amdgcn_s_setprio(2);
+#endif
+#pragma unroll
+    for (int q = 0; q < P; q++) {
+        const uint64_t pg = W.page(k + q);
+        load_page<M>(w[q], base + (pg < last ? pg : last) * (64u * M));
+    }
+#if CC_PRIO_LOADS
+    __builtin_amdgcn_s_setprio(0);
+#endif
+}
+
+// P independent Horner chains, interleaved step by step so each wave keeps
+// 4*P LDS lookups in flight instead of 4.
+template <int M, int P>
+__device__ __forceinline__ void chains(const uint32_t* tab, const uint32_t (&w)[P][M], uint32_t c0, uint32_t c1,
+                                       uint32_t (&s)[P]) {
+#pragma unroll
+    for (int q = 0; q < P; q++) s[q] = w[q][0];
+#pragma unroll
+    for (int j = 1; j < M; j++) {
+#pragma unroll
+        for (int q = 0; q < P; q++) {
+#if CC_ABLATE == 1
+            s[q] = ((s[q] << 1) | (s[q] >> 31)) ^ w[q][j];
+#else
+            s[q] = apply_g(tab, s[q], c0, c1) ^ w[q][j];
+#endif
+        }
+    }
+}
+
 // MODE 0: compute CRCs into out[]; MODE 1: verify against expected[].
-// Wave w walks tiles w, w+W, w+2W, ... (W = waves in the grid), 64 pages each;
-// its k-th page is (w + (k>>6) W)*64 + (k&63), increasing in k.  Two register
-// buffers ping-pong so the next page's loads are in flight while the current
-// page is hashed; loads are unconditional (index clamped to the last page) so
-// hipcc can count vmcnt exactly.
+// Wave w walks tiles w, w+W, w+2W, ... (W = waves in the grid) of 2^ts pages,
+// P pages per step.  CC_PREFETCH+1 register buffers rotate so CC_PREFETCH
+// steps' loads are in flight while the current step is hashed.  Loads are
+// unconditional (index clamped to the last page) so hipcc counts vmcnt exactly.
 template <int M, int MODE>
 __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
     const uint32_t* __restrict__ pages, uint64_t n_pages, const uint4* __restrict__ image,
@@ -153,43 +241,52 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t tmask = (1u << tshift) - 1u;  // tile = 2^tshift pages (<= 64)
-    const uint64_t wstride = ((uint64_t)gridDim.x * kWavesPerBlock) << tshift;  // pages between a wave's tiles
-    const uint64_t wfirst = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) << tshift;
-    if (wfirst >= n_pages) return;
+    Walk W;
+    W.tshift = tshift;
+    W.tmask = (1u << tshift) - 1u;
+    W.wstride = ((uint64_t)gridDim.x * kWavesPerBlock) << tshift;
+    W.wfirst = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) << tshift;
+    if (W.wfirst >= n_pages) return;
     const uint64_t last = n_pages - 1;
     const uint32_t c0 = lane << 2 & 0x7Cu;
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
     const uint32_t* base = pages + lane;
-
-    uint32_t A[M], B[M];
+    constexpr int D = CC_PREFETCH;
+    constexpr int P = (M <= 16) ? CC_PAIR : 1;  // register budget: P*(D+1)*M data VGPRs
     uint32_t acc = 0;
-    uint64_t k = 0, page = wfirst;
-    load_page<M>(A, base + page * (64u * M));
-    for (;;) {
-        // ---- page k in A ----
-        uint64_t k1 = k + 1;
-        uint64_t p1 = wfirst + (k1 >> tshift) * wstride + (k1 & tmask);
-        load_page<M>(B, base + (p1 < last ? p1 : last) * (64u * M));
-        uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, A, c0, c1), cf)) ^ kconst;
-        acc = lane == (uint32_t)(k & tmask) ? crc : acc;
-        if ((k & tmask) == tmask || p1 >= n_pages)
-            flush_tile<MODE>(acc, page - (k & tmask), (uint32_t)(k & tmask) + 1u, lane, out, expected, bad_count,
-                             first_bad);
-        if (p1 >= n_pages) break;
-        // ---- page k1 in B ----
-        const uint64_t k2 = k1 + 1;
-        const uint64_t p2 = wfirst + (k2 >> tshift) * wstride + (k2 & tmask);
-        load_page<M>(A, base + (p2 < last ? p2 : last) * (64u * M));
-        crc = wave_xor(apply_fin(tab, chain<M>(tab, B, c0, c1), cf)) ^ kconst;
-        acc = lane == (uint32_t)(k1 & tmask) ? crc : acc;
-        if ((k1 & tmask) == tmask || p2 >= n_pages)
-            flush_tile<MODE>(acc, p1 - (k1 & tmask), (uint32_t)(k1 & tmask) + 1u, lane, out, expected, bad_count,
-                             first_bad);
-        if (p2 >= n_pages) break;
-        k = k2;
-        page = p2;
+
+    // ring of D+1 register buffers; after full unrolling every index is a
+    // compile-time constant, so the ring lives in VGPRs (no scratch)
+    uint32_t ring[D + 1][P][M];
+#pragma unroll
+    for (int st = 0; st < D; st++) load_pages<M, P>(ring[st], base, W, (uint64_t)st * P, last);
+    // Every step's loads are unconditional (clamped) and termination is tested
+    // once per ring revolution: path-insensitive waitcnt dataflow then sees the
+    // same D stages outstanding on every edge into a step and keeps each wait
+    // at its exact count (a per-step early exit made hipcc over-wait a stage).
+    for (uint64_t k = 0;; k += (uint64_t)(D + 1) * P) {
+#pragma unroll
+        for (int st = 0; st <= D; st++) {
+            const uint64_t kk = k + (uint64_t)st * P;
+            load_pages<M, P>(ring[(st + D) % (D + 1)], base, W, kk + (uint64_t)D * P, last);
+            uint32_t s[P];
+            chains<M, P>(tab, ring[st], c0, c1, s);
+#pragma unroll
+            for (int q = 0; q < P; q++) {
+                const uint64_t kq = kk + q;
+                const uint64_t pc = W.page(kq);
+                if (pc < n_pages) {
+                    const uint64_t pn = W.page(kq + 1);
+                    const uint32_t crc = wave_xor(apply_fin(tab, s[q], cf)) ^ kconst;
+                    const uint32_t slot = (uint32_t)(kq & W.tmask);
+                    acc = lane == slot ? crc : acc;
+                    if (slot == W.tmask || pn >= n_pages)
+                        flush_tile<MODE>(acc, pc - slot, slot + 1u, lane, out, expected, bad_count, first_bad);
+                }
+            }
+        }
+        if (W.page(k + (uint64_t)(D + 1) * P) >= n_pages) break;
     }
 }
 
