@@ -37,6 +37,9 @@ constexpr uint32_t kPolyDev = 0x82F63B78u;
 #ifndef CC_NT_LOADS
 #define CC_NT_LOADS 1
 #endif
+#ifndef CC_STORE
+#define CC_STORE 2  // 0 plain, 1 none (diagnostic), 2 nontemporal
+#endif
 
 __device__ __forceinline__ uint32_t lds_u32(const uint32_t* tab, uint32_t byte_addr) {
 #if CC_LDS_B64  // diagnostic: 8-byte lookups (half unused), tests instruction- vs byte-bound LDS
@@ -158,9 +161,17 @@ __device__ __forceinline__ void flush_tile(uint32_t acc, uint64_t tile_first, ui
                                            unsigned long long* __restrict__ bad_count,
                                            unsigned long long* __restrict__ first_bad) {
     if (MODE == 0) {
+#if CC_STORE == 1  // diagnostic: no store (wrong output), keeps acc live
+        asm volatile("" ::"v"(acc));
+#elif CC_STORE == 2
+        // nt: the CRC stream must not interleave cached partial-line writes with
+        // the 16 GiB nt read stream (plain stores cost 3 % of HBM throughput)
+        if (lane < cnt) __builtin_nontemporal_store(acc, out + tile_first + lane);
+#else
         if (lane < cnt) out[tile_first + lane] = acc;
+#endif
     } else {
-        const uint32_t want = lane < cnt ? expected[tile_first + lane] : acc;
+        const uint32_t want = lane < cnt ? __builtin_nontemporal_load(expected + tile_first + lane) : acc;
         const uint64_t bad = __ballot(want != acc);
         if (bad && lane == 0) {
             atomicAdd(bad_count, (unsigned long long)__popcll(bad));

@@ -51,6 +51,11 @@ def launch(path):
     assert rc == 0, rc
 
 
+if a.verify:  # expected CRCs from the first variant's compute path
+    L0 = libs[a.libs[0]]
+    for path in a.libs:
+        assert L0.cc_page_crc_dev(ctypes.c_void_p(data.data_ptr()), n, a.page_bytes,
+                                  ctypes.c_void_p(outs[path].data_ptr()), h) == 0
 for path in a.libs:  # warm + results
     launch(path)
 torch.cuda.synchronize()
@@ -65,6 +70,9 @@ for r in range(a.rounds):
         e1.record(s)
         torch.cuda.synchronize()
         times[path].append(e0.elapsed_time(e1) / a.reps)
+if a.verify:
+    torch.cuda.synchronize()
+    assert int(cnt[0]) == 0, "verify flagged clean pages"
 for path in a.libs:
     same = bool(torch.equal(outs[path], ref)) if not a.verify else None
     ms = statistics.median(times[path])
