@@ -43,6 +43,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--e2e-gib", type=float, default=1.0, help="pinned host buffer for the e2e leg")
+    p.add_argument("--stream-chunks", type=int, default=10000, help="config-4 stream leg (0 = skip)")
     p.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/traffic_*.json)")
     return p.parse_args()
 
@@ -103,6 +104,37 @@ def e2e_leg(args, dev):
     return round(reps * nb / GiB / el, 2)
 
 
+def stream_leg(args):
+    """BASELINE config 4: scan-service stream of `--stream-chunks` x 16 MiB chunk
+    files from host memory (pinned, as pread into pinned buffers would leave
+    them), pipelined H2D + hashing (cc_scan_host), ScanMap slice CRCs + file CRCs,
+    then the per-copyset digests (100 chunks per copyset).  A pinned pool of 64
+    distinct chunk files is re-referenced to keep host RAM bounded."""
+    from curve_amd import crc as C
+    from curve_amd.pool import copyset_layout
+    n = args.stream_chunks
+    pool_n = 64
+    data = torch.empty((pool_n, C.CHUNK_SIZE), dtype=torch.uint8, pin_memory=True)
+    data.random_(0, 256)
+    meta = torch.zeros((pool_n, C.META_PAGE_SIZE), dtype=torch.uint8, pin_memory=True)
+    meta[:, 0] = 2
+    dn, mn = data.numpy(), meta.numpy()
+    chunks = [(mn[i % pool_n], dn[i % pool_n]) for i in range(n)]
+    C.scan_host(chunks[:8])  # warm
+    t0 = time.perf_counter()
+    mc, sc, fc = C.scan_host(chunks)
+    el = time.perf_counter() - t0
+    per = 100
+    lay = copyset_layout(list(range(n)), [i // per for i in range(n)], [C.CHUNK_SIZE + C.META_PAGE_SIZE] * n)
+    dig = [0] * lay.n_groups
+    for i in range(n):
+        dig[lay.group[i]] ^= C.shift(int(fc[i]), lay.after_bytes[i])
+    el_all = time.perf_counter() - t0
+    return {"chunks": n, "GiBps_e2e": round(n * (C.CHUNK_SIZE + C.META_PAGE_SIZE) / GiB / el, 2),
+            "seconds": round(el, 3), "with_digest_seconds": round(el_all, 3), "copysets": lay.n_groups,
+            "scan_maps": int(sc.size + mc.size), "source": "pinned host pool of 64 chunk files, re-referenced"}
+
+
 def load_traffic(args):
     path = args.traffic_json
     if path is None:
@@ -120,13 +152,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; BENCH_DIST_BACKEND=gloo + more ranks than GPUs only to
+    # rehearse the multi-rank flow on a 1-GPU box (the driver uses nccl = RCCL)
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from curve_amd import crc as C
-    from curve_amd.scan import DevicePool, chunk_file_name, copyset_after_bytes
+    from curve_amd.pool import copyset_layout, reduce_digests, shard_range
+    from curve_amd.scan import DevicePool
 
     pb = args.page_bytes
     chunk, meta_sz = C.CHUNK_SIZE, C.META_PAGE_SIZE
@@ -141,21 +181,17 @@ def main():
     ids = list(range(first_id, first_id + n))
     pool = DevicePool(data, meta, ids, page_bytes=pb)
 
-    # copyset geometry over the WHOLE pool (all ranks): chunk id -> copyset id % 64
+    # copyset geometry over the WHOLE pool (all ranks): chunk id -> copyset id % 64,
+    # chunk files named chunk_<id>, chained in std::sort name order per copyset
     total = n * world
-    names_all = [chunk_file_name(i) for i in range(total)]
-    group_all = [i % N_COPYSETS for i in range(total)]
-    file_size = chunk + meta_sz
-    after_all = [0] * total
-    for g in range(N_COPYSETS):
-        members = [i for i in range(total) if group_all[i] == g]
-        aft = copyset_after_bytes([names_all[i] for i in members], [file_size] * len(members))
-        for i, a in zip(members, aft):
-            after_all[i] = a
-    after = torch.tensor(after_all[first_id:first_id + n], dtype=torch.int64, device=dev)
-    group = torch.tensor(group_all[first_id:first_id + n], dtype=torch.int32, device=dev)
-    digest = torch.zeros(N_COPYSETS, dtype=torch.int32, device=dev)
-    gathered = torch.zeros(world * N_COPYSETS, dtype=torch.int32, device=dev) if world > 1 else None
+    lay = copyset_layout(list(range(total)), [i % N_COPYSETS for i in range(total)],
+                         [chunk + meta_sz] * total)
+    lo, hi = shard_range(total, rank, world)
+    assert (lo, hi) == (first_id, first_id + n)
+    after = torch.tensor(lay.after_bytes[lo:hi], dtype=torch.int64, device=dev)
+    group = torch.tensor(lay.group[lo:hi], dtype=torch.int32, device=dev)
+    digest = torch.zeros(lay.n_groups, dtype=torch.int32, device=dev)
+    full_digest = [digest]
 
     stream = torch.cuda.current_stream()
     ev = []
@@ -174,9 +210,8 @@ def main():
         C.fold(pool.slice_crcs, chunk // C.SCAN_SIZE, C.SCAN_SIZE, out=pool.data_crcs)
         C.combine_dev(pool.meta_crcs[:n], pool.data_crcs, chunk, out=pool.file_crcs)
         digest.zero_()
-        C.digest_dev(pool.file_crcs, after, group, N_COPYSETS, out=digest)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, digest)
+        C.digest_dev(pool.file_crcs, after, group, lay.n_groups, out=digest)
+        full_digest[0] = reduce_digests(digest, dist) if world > 1 else digest
 
     for _ in range(args.warmup):
         step(False)
@@ -242,6 +277,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(pool, args, rank)
     if rank == 0 and world == 1 and not args.no_e2e:
         out["e2e_pinned_GiBps"] = e2e_leg(args, dev)
+        if args.stream_chunks:
+            out["stream"] = stream_leg(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -29,6 +29,10 @@ class CcOpts(ctypes.Structure):
     _fields_ = [("page_bytes", _u32), ("slice_bytes", _u32), ("staging_bytes", _u64)]
 
 
+class CcChunkSrc(ctypes.Structure):
+    _fields_ = [("meta", _vp), ("data", _vp)]
+
+
 SIGNATURES = {
     "crc32c_value": (_u32, [_vp, _sz]),
     "crc32c_extend": (_u32, [_u32, _vp, _sz]),
@@ -49,6 +53,7 @@ SIGNATURES = {
     "cc_digest_dev": (_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
     "cc_page_crc_host": (_int, [_vp, _u64, _u32, _vp]),
     "cc_lds_image": (_int, [_vp, _sz]),
+    "cc_scan_host": (_int, [ctypes.POINTER(CcChunkSrc), _u64, _u32, _u32, _u32, _u32, _vp, _vp, _vp]),
 }
 
 _lib = None

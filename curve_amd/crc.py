@@ -223,6 +223,33 @@ def page_crc_host(data, page_bytes: int = PAGE_SIZE):
     return out
 
 
+def scan_host(chunks, chunk_bytes: int = CHUNK_SIZE, meta_bytes: int = META_PAGE_SIZE,
+              page_bytes: int = PAGE_SIZE, slice_bytes: int = SCAN_SIZE):
+    """Streaming scan of host-resident chunk files (cc_scan_host).
+    `chunks`: sequence of (meta, data) numpy uint8 arrays (pinned or pageable).
+    Returns (meta_crcs[n], slice_crcs[n, chunk/slice], file_crcs[n]) as uint32 numpy."""
+    import numpy as np
+    n = len(chunks)
+    arr = (_lib.CcChunkSrc * max(n, 1))()
+    keep = []
+    for i, (m, d) in enumerate(chunks):
+        m = np.ascontiguousarray(m)
+        d = np.ascontiguousarray(d)
+        if m.nbytes != meta_bytes or d.nbytes != chunk_bytes:
+            raise CurveCrcError(_lib.CC_EINVAL, f"chunk {i}: wrong metapage/data size")
+        keep += [m, d]
+        arr[i].meta = m.ctypes.data
+        arr[i].data = d.ctypes.data
+    S = chunk_bytes // slice_bytes
+    mc = np.empty(n, dtype=np.uint32)
+    sc = np.empty((n, S), dtype=np.uint32)
+    fc = np.empty(n, dtype=np.uint32)
+    check(lib().cc_scan_host(arr, n, chunk_bytes, meta_bytes, page_bytes, slice_bytes,
+                             ctypes.c_void_p(mc.ctypes.data), ctypes.c_void_p(sc.ctypes.data),
+                             ctypes.c_void_p(fc.ctypes.data)), "cc_scan_host")
+    return mc, sc, fc
+
+
 def as_u32(t) -> "list[int]":
     """Device/host int32 CRC tensor -> python ints in [0, 2^32)."""
     return [int(x) & 0xFFFFFFFF for x in t.detach().cpu().tolist()]

@@ -391,4 +391,131 @@ int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
     return CC_OK;
 }
 
+// Streaming scan.  Each staging slot holds a batch of whole chunks (data and
+// metapages in separate device regions) plus the per-chunk results; a batch is
+// {H2D data+meta, page kernel over data, page kernel over metapages, fold to
+// slices, fold to chunk data CRC, combine to file CRC, D2H results} on the
+// slot's stream, so consecutive batches on the two streams overlap copy and
+// compute.
+int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_bytes, uint32_t meta_bytes,
+                 uint32_t page_bytes, uint32_t slice_bytes, uint32_t* h_meta_crcs, uint32_t* h_slice_crcs,
+                 uint32_t* h_file_crcs) {
+    if (n_chunks == 0) return CC_OK;
+    if (!chunks || !page_size_ok(page_bytes) || !page_size_ok(meta_bytes) || chunk_bytes == 0 ||
+        slice_bytes == 0 || chunk_bytes % slice_bytes || slice_bytes % page_bytes)
+        return CC_EINVAL;
+    DevCtx* c = nullptr;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->submit);
+    if ((rc = staging_init(c))) return rc;
+    Staging& st = c->st;
+    const uint64_t per_chunk_dev = (uint64_t)chunk_bytes + meta_bytes;
+    const uint64_t batch = st.bytes / per_chunk_dev;
+    if (batch == 0) return CC_EINVAL;  // staging smaller than one chunk file
+    const uint32_t slices = chunk_bytes / slice_bytes;
+    const uint64_t pages_per_chunk = chunk_bytes / page_bytes;
+    // per-slot device result region (carved from dcrc, sized per/256*4 bytes):
+    // page CRCs [batch*pages_per_chunk] | meta [batch] | slices [batch*slices] | data [batch] | file [batch]
+    const uint64_t need_words = batch * pages_per_chunk + batch * (3 + (uint64_t)slices);
+    if (need_words * 4 > st.bytes / 256 * 4) return CC_EINVAL;
+    const uint32_t k_page = kconst_for(page_bytes), k_meta = kconst_for(meta_bytes);
+    FoldLaunch f1 = {}, f2 = {};
+    f1.per_group = slice_bytes / page_bytes;
+    f1.m_unit = xpow((uint64_t)page_bytes << 3);
+    for (int t = 0; t < 6; t++) f1.m_tree[t] = xpow(((uint64_t)page_bytes * (f1.per_group / 64) << t) << 3);
+    f2.per_group = slices;
+    f2.m_unit = xpow((uint64_t)slice_bytes << 3);
+    for (int t = 0; t < 6; t++) f2.m_tree[t] = xpow(((uint64_t)slice_bytes * (slices / 64) << t) << 3);
+    const uint32_t m_chunk = xpow((uint64_t)chunk_bytes << 3);
+
+    const bool pinned0 = is_pinned(chunks[0].data) && is_pinned(chunks[0].meta);
+    uint64_t pend_first[2] = {0, 0}, pend_n[2] = {0, 0};
+    hipError_t e = hipSuccess;
+    auto drain = [&](int s) -> int {
+        if (!pend_n[s]) return CC_OK;
+        hipError_t ee = hipEventSynchronize(st.done[s]);
+        if (ee != hipSuccess) return map_err(ee);
+        const uint32_t* r = st.hcrc[s];
+        const uint64_t nb = pend_n[s], f = pend_first[s];
+        const uint32_t* rm = r;
+        const uint32_t* rs = r + nb;
+        const uint32_t* rf = r + nb + nb * slices;
+        if (h_meta_crcs) memcpy(h_meta_crcs + f, rm, nb * 4);
+        if (h_slice_crcs) memcpy(h_slice_crcs + f * slices, rs, nb * slices * 4);
+        if (h_file_crcs) memcpy(h_file_crcs + f, rf, nb * 4);
+        pend_n[s] = 0;
+        return CC_OK;
+    };
+    int slot = 0;
+    for (uint64_t first = 0; first < n_chunks; first += batch) {
+        const uint64_t nb = (n_chunks - first < batch) ? n_chunks - first : batch;
+        if ((rc = drain(slot))) return rc;
+        unsigned char* ddata = static_cast<unsigned char*>(st.dev[slot]);
+        unsigned char* dmeta = ddata + nb * (uint64_t)chunk_bytes;
+        unsigned char* hstage = static_cast<unsigned char*>(st.host[slot]);
+        hipStream_t s = st.stream[slot];
+        for (uint64_t i = 0; i < nb; i++) {
+            const cc_chunk_src& cs = chunks[first + i];
+            if (!cs.data || !cs.meta) return CC_EINVAL;
+            const void* sd = cs.data;
+            const void* sm = cs.meta;
+            if (!pinned0) {
+                memcpy(hstage + i * (uint64_t)chunk_bytes, cs.data, chunk_bytes);
+                memcpy(hstage + nb * (uint64_t)chunk_bytes + i * (uint64_t)meta_bytes, cs.meta, meta_bytes);
+                continue;
+            }
+            if ((e = hipMemcpyAsync(ddata + i * (uint64_t)chunk_bytes, sd, chunk_bytes, hipMemcpyHostToDevice, s)) !=
+                hipSuccess)
+                return map_err(e);
+            if ((e = hipMemcpyAsync(dmeta + i * (uint64_t)meta_bytes, sm, meta_bytes, hipMemcpyHostToDevice, s)) !=
+                hipSuccess)
+                return map_err(e);
+        }
+        if (!pinned0 && (e = hipMemcpyAsync(ddata, hstage, nb * per_chunk_dev, hipMemcpyHostToDevice, s)) != hipSuccess)
+            return map_err(e);
+        uint32_t* res = st.dcrc[slot];
+        uint32_t* d_pages = res + nb * (3 + (uint64_t)slices);
+        uint32_t* d_meta = res;
+        uint32_t* d_slices = res + nb;
+        uint32_t* d_file = res + nb + nb * slices;
+        uint32_t* d_data = d_file + nb;
+        PageLaunch a = {};
+        a.pages = reinterpret_cast<const uint32_t*>(ddata);
+        a.n_pages = nb * pages_per_chunk;
+        a.words_per_lane = page_bytes / kWaveBytes;
+        a.image = c->image;
+        a.kconst = k_page;
+        a.out = d_pages;
+        geometry_for(c, a.n_pages, &a);
+        if ((e = launch_page_crc(a, s)) != hipSuccess) return map_err(e);
+        a.pages = reinterpret_cast<const uint32_t*>(dmeta);
+        a.n_pages = nb;
+        a.words_per_lane = meta_bytes / kWaveBytes;
+        a.kconst = k_meta;
+        a.out = d_meta;
+        geometry_for(c, nb, &a);
+        if ((e = launch_page_crc(a, s)) != hipSuccess) return map_err(e);
+        f1.crcs = d_pages;
+        f1.n_groups = nb * slices;
+        f1.out = d_slices;
+        if ((e = launch_fold(f1, s)) != hipSuccess) return map_err(e);
+        f2.crcs = d_slices;
+        f2.n_groups = nb;
+        f2.out = d_data;
+        if ((e = launch_fold(f2, s)) != hipSuccess) return map_err(e);
+        if ((e = launch_combine(d_meta, d_data, m_chunk, nb, d_file, s)) != hipSuccess) return map_err(e);
+        if ((e = hipMemcpyAsync(st.hcrc[slot], res, nb * (2 + (uint64_t)slices) * 4, hipMemcpyDeviceToHost, s)) !=
+            hipSuccess)
+            return map_err(e);
+        if ((e = hipEventRecord(st.done[slot], s)) != hipSuccess) return map_err(e);
+        pend_first[slot] = first;
+        pend_n[slot] = nb;
+        slot ^= 1;
+    }
+    if ((rc = drain(slot))) return rc;
+    if ((rc = drain(slot ^ 1))) return rc;
+    return CC_OK;
+}
+
 }  // extern "C"

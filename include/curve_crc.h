@@ -129,6 +129,29 @@ int cc_digest_dev(const uint32_t* d_file_crcs, const uint64_t* d_after_bytes,
 int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
                      uint32_t* h_out);
 
+/* One chunk file as the datastore holds it: metapage + data
+ * (file = metapage || data, chunkserver_chunkfile.cpp:497-536). */
+typedef struct cc_chunk_src {
+    const void* meta; /* meta_bytes of host memory */
+    const void* data; /* chunk_bytes of host memory */
+} cc_chunk_src;
+
+/* Streaming scan of host-resident chunk files (BASELINE config 4; the scan
+ * hasher ScanChunkRequest::OnApply, op_request.cpp:769-820, for every scan op
+ * of every chunk in ScanManager::ScanJobProcess order, scan_manager.cpp:250-283).
+ * Per chunk c:
+ *   h_meta_crcs[c]                          = CRC32(metapage)          (the readMetaPage op)
+ *   h_slice_crcs[c*S + k], S = chunk/slice  = CRC32(data[k*slice, +slice))
+ *   h_file_crcs[c]                          = CRC32(metapage || data)  (chunk-file CRC for
+ *                                             the copyset chain, copyset_node.cpp:964)
+ * Pipelined over two pinned staging slots and two HIP streams: the H2D copy of
+ * batch i+1 overlaps the hashing of batch i.  Pinned (hipHostMalloc'ed or
+ * registered) sources are DMA'd directly; pageable ones are staged by memcpy.
+ * Any output pointer may be NULL.  Blocking; thread-safe (per-device lock). */
+int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_bytes,
+                 uint32_t meta_bytes, uint32_t page_bytes, uint32_t slice_bytes,
+                 uint32_t* h_meta_crcs, uint32_t* h_slice_crcs, uint32_t* h_file_crcs);
+
 /* ------------------------------------------------------------------------
  * Diagnostics (new; no reference counterpart)
  * ------------------------------------------------------------------------ */

@@ -262,3 +262,26 @@ def test_tiled_geometries(dev, oracle, n_pages):
     cnt = C.page_verify(d, got, 256)
     torch.cuda.synchronize()
     assert int(cnt[0]) == len(bad) and int(cnt[1]) == bad[0]
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_scan_host_stream(dev, oracle, pinned):
+    """cc_scan_host: host-resident chunk files streamed through the 2-slot pinned
+    pipeline -> metapage / slice / file CRCs == the oracle's ScanJobProcess geometry."""
+    from curve_amd import crc as C
+    chunk, meta, slice_ = 1 << 20, 4096, 256 << 10
+    n = 300  # > 2 staging slots' worth of 1 MiB chunks (128 MiB slots)
+    rng = np.random.default_rng(77 + pinned)
+    pool_d = rng.integers(0, 256, (8, chunk), dtype=np.uint8)
+    pool_m = rng.integers(0, 256, (8, meta), dtype=np.uint8)
+    if pinned:
+        pool_d = torch.from_numpy(pool_d).pin_memory().numpy()
+        pool_m = torch.from_numpy(pool_m).pin_memory().numpy()
+    chunks = [(pool_m[(i * 3) % 8], pool_d[i % 8]) for i in range(n)]
+    mc, sc, fc = C.scan_host(chunks, chunk, meta, 4096, slice_)
+    for i in range(n):
+        m, d = chunks[i]
+        ref = oracle.scan_slices(m.tobytes(), d.tobytes(), slice_)
+        assert mc[i] == ref[0][2]
+        assert [int(x) for x in sc[i]] == [c for (_, _, c) in ref[1:]]
+        assert fc[i] == oracle.crc32c(m.tobytes() + d.tobytes())
