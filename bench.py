@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--e2e-gib", type=float, default=1.0, help="pinned host buffer for the e2e leg")
+    p.add_argument("--updates", type=int, default=65536, help="config-3 updates per batch")
+    p.add_argument("--update-batches", type=int, default=5)
     p.add_argument("--stream-chunks", type=int, default=10000, help="config-4 stream leg (0 = skip)")
     p.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/traffic_*.json)")
     return p.parse_args()
@@ -133,6 +135,43 @@ def stream_leg(args):
     return {"chunks": n, "GiBps_e2e": round(n * (C.CHUNK_SIZE + C.META_PAGE_SIZE) / GiB / el, 2),
             "seconds": round(el, 3), "with_digest_seconds": round(el_all, 3), "copysets": lay.n_groups,
             "scan_maps": int(sc.size + mc.size), "source": "pinned host pool of 64 chunk files, re-referenced"}
+
+
+def partial_write_leg(pool, args):
+    """BASELINE config 3: client partial writes into the resident 1024-chunk pool.
+    U random updates per batch (size uniform in [512, 4096] B, offset uniform and
+    unaligned; ~12 % straddle two pages), applied in order + CRC of every touched
+    page recomputed in place (cc_apply_updates_dev)."""
+    from curve_amd import crc as C
+    dev = pool.data.device
+    U = args.updates
+    rng = np.random.default_rng(0xC3)
+    pool_bytes = pool.data.numel()
+    src = torch.empty(U * 4096, dtype=torch.uint8, device=dev).random_(0, 256)
+    flat = pool.data.view(-1)
+    times, upd_bytes, touched = [], 0, 0
+    for it in range(args.update_batches + 1):
+        lens = rng.integers(512, 4097, U)
+        dst = rng.integers(0, pool_bytes - 4096, U)
+        src_off = rng.integers(0, U * 4096 - 4096, U)
+        p0, p1 = dst // 4096, (dst + lens - 1) // 4096
+        tp = len(np.unique(np.concatenate([p0, p1])))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        C.apply_updates(flat, pool.page_crcs, src, dst, src_off, lens, 4096)
+        torch.cuda.synchronize()
+        if it:  # first batch warms the work buffer
+            times.append(time.perf_counter() - t0)
+            upd_bytes += int(lens.sum())
+            touched += tp
+    el = sum(times)
+    alg = 2 * upd_bytes + touched * (4096 + 4)
+    return {"updates_per_batch": U, "batches": args.update_batches,
+            "ms_per_batch": round(el / len(times) * 1e3, 3),
+            "updates_per_s": round(U * len(times) / el, 1),
+            "touched_pages_per_batch": touched // len(times),
+            "alg_GBps": round(alg / el / 1e9, 1),
+            "note": "wall time incl. host split + descriptor upload; alg bytes = 2*update bytes + 4100*touched pages"}
 
 
 def load_traffic(args):
@@ -273,6 +312,8 @@ def main():
                      "traffic_source": traffic_src},
         "verify": {"GiBps": round(n * chunk / GiB / (verify_ms * 1e-3), 2), "bad_pages": bad},
     }
+    if rank == 0 and world == 1 and args.updates:
+        out["partial_write"] = partial_write_leg(pool, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pool, args, rank)
     if rank == 0 and world == 1 and not args.no_e2e:

@@ -250,6 +250,85 @@ def scan_host(chunks, chunk_bytes: int = CHUNK_SIZE, meta_bytes: int = META_PAGE
     return mc, sc, fc
 
 
+UPDATE_DTYPE = None
+
+
+def _update_dtype():
+    global UPDATE_DTYPE
+    if UPDATE_DTYPE is None:
+        import numpy as np
+        UPDATE_DTYPE = np.dtype([("dst", "<u8"), ("src", "<u8"), ("len", "<u4"), ("reserved", "<u4")])
+    return UPDATE_DTYPE
+
+
+def split_nonoverlapping(dst, lens):
+    """Split an ORDERED list of byte-range writes into consecutive batches whose
+    members do not overlap each other; applying the batches one after another
+    equals applying the writes in order (later writes win on overlaps, as the
+    raft log orders them, op_request.cpp:429-481).  Returns a list of index arrays."""
+    import numpy as np
+    dst = np.asarray(dst, dtype=np.int64)
+    end = dst + np.asarray(lens, dtype=np.int64)
+    n = dst.size
+    if n == 0:
+        return []
+    order = np.argsort(dst, kind="stable")
+    if not (end[order][:-1] > dst[order][1:]).any():
+        return [np.arange(n)]  # no overlaps at all: one batch
+    from sortedcontainers import SortedList
+    batches, cur, ivs = [], [], SortedList()
+    for i in range(n):
+        a, b = int(dst[i]), int(end[i])
+        k = ivs.bisect_left((a, -1))
+        hit = (k < len(ivs) and ivs[k][0] < b) or (k > 0 and ivs[k - 1][1] > a)
+        if hit:
+            batches.append(np.array(cur, dtype=np.int64))
+            cur, ivs = [], SortedList()
+        cur.append(i)
+        ivs.add((a, b))
+    batches.append(np.array(cur, dtype=np.int64))
+    return batches
+
+
+_work_cache = {}
+
+
+def apply_updates(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int = PAGE_SIZE, stream=None):
+    """Client partial-write path on device (cc_apply_updates_dev): write
+    src[src_off[i]:+lens[i]] to pool[dst_off[i]:+lens[i]] in order, then
+    recompute the CRC of every touched page in `page_crcs` (in place).
+    Returns the number of device calls (batches) used."""
+    import numpy as np
+    torch = _torch()
+    dst_off = np.asarray(dst_off, dtype=np.uint64)
+    src_off = np.asarray(src_off, dtype=np.uint64)
+    lens = np.asarray(lens, dtype=np.uint32)
+    if not (dst_off.size == src_off.size == lens.size):
+        raise CurveCrcError(_lib.CC_EINVAL, "dst/src/len size mismatch")
+    if (lens == 0).any() or (dst_off + lens > _nbytes(pool)).any() or (src_off + lens > _nbytes(src)).any():
+        raise CurveCrcError(_lib.CC_EINVAL, "update out of range or empty")
+    n_pages = _nbytes(pool) // page_bytes
+    max_len = int(lens.max()) if lens.size else 1
+    batches = split_nonoverlapping(dst_off, lens)
+    need = int(lib().cc_update_work_bytes(n_pages, max(len(b) for b in batches) if batches else 0, max_len, page_bytes))
+    key = (pool.device, need)
+    work = _work_cache.get(key)
+    if work is None or work.numel() < need:
+        work = torch.empty(need, dtype=torch.uint8, device=pool.device)
+        _work_cache.clear()
+        _work_cache[key] = work
+    for b in batches:
+        rec = np.zeros(b.size, dtype=_update_dtype())
+        rec["dst"], rec["src"], rec["len"] = dst_off[b], src_off[b], lens[b]
+        d_upd = torch.from_numpy(rec.view(np.uint8)).to(pool.device)
+        with torch.cuda.device(pool.device):
+            check(lib().cc_apply_updates_dev(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, _dev_ptr(src, "src"),
+                                             _dev_ptr(d_upd, "updates"), b.size, max_len, _dev_ptr(page_crcs, "page_crcs"),
+                                             _dev_ptr(work, "work"), work.numel(), _stream_handle(stream)),
+                  "cc_apply_updates_dev")
+    return len(batches)
+
+
 def as_u32(t) -> "list[int]":
     """Device/host int32 CRC tensor -> python ints in [0, 2^32)."""
     return [int(x) & 0xFFFFFFFF for x in t.detach().cpu().tolist()]

@@ -391,6 +391,51 @@ int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
     return CC_OK;
 }
 
+uint64_t cc_update_work_bytes(uint64_t n_pages, uint64_t n_updates, uint32_t max_len, uint32_t page_bytes) {
+    if (page_bytes == 0) return 0;
+    const uint64_t span = (uint64_t)max_len / page_bytes + 2;  // pages one update can touch
+    const uint64_t flags = (n_pages * 4 + 255) & ~255ull;
+    const uint64_t list = n_updates * span * 8;
+    return flags + 256 + list;
+}
+
+int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
+                         const cc_update* d_updates, uint64_t n_updates, uint32_t max_len, uint32_t* d_page_crcs,
+                         void* d_work, uint64_t work_bytes, void* stream) {
+    if (!page_size_ok(page_bytes) || page_bytes / kWaveBytes > 32) return CC_EINVAL;
+    if (n_updates == 0) return CC_OK;
+    if (!d_pool || !d_src || !d_updates || !d_page_crcs || !d_work || max_len == 0) return CC_EINVAL;
+    if (pool_bytes % page_bytes || ((uintptr_t)d_pool & 3u) || ((uintptr_t)d_src & 3u)) return CC_EINVAL;
+    const uint64_t n_pages = pool_bytes / page_bytes;
+    if (work_bytes < cc_update_work_bytes(n_pages, n_updates, max_len, page_bytes)) return CC_EINVAL;
+    DevCtx* c = nullptr;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    unsigned char* w = static_cast<unsigned char*>(d_work);
+    const uint64_t flags_bytes = (n_pages * 4 + 255) & ~255ull;
+    UpdateLaunch a = {};
+    a.pool = static_cast<unsigned char*>(d_pool);
+    a.src = static_cast<const unsigned char*>(d_src);
+    a.upd = reinterpret_cast<const UpdateDesc*>(d_updates);
+    a.n_updates = n_updates;
+    a.page_bytes = page_bytes;
+    a.flags = reinterpret_cast<uint32_t*>(w);
+    a.count = reinterpret_cast<unsigned long long*>(w + flags_bytes);
+    a.list = reinterpret_cast<unsigned long long*>(w + flags_bytes + 256);
+    a.list_cap = n_updates * ((uint64_t)max_len / page_bytes + 2);
+    a.image = c->image;
+    a.kconst = kconst_for(page_bytes);
+    a.page_crcs = d_page_crcs;
+    const uint64_t waves = (uint64_t)c->cus * kWavesPerBlock;
+    const uint64_t want = a.list_cap < waves ? a.list_cap : waves;
+    a.blocks = (int)((want + kWavesPerBlock - 1) / kWavesPerBlock);
+    hipError_t e;
+    if ((e = hipMemsetAsync(w, 0, flags_bytes + 256, s)) != hipSuccess) return map_err(e);
+    if ((e = launch_apply_updates(a, s)) != hipSuccess) return map_err(e);
+    return map_err(launch_page_list_crc(a, s));
+}
+
 // Streaming scan.  Each staging slot holds a batch of whole chunks (data and
 // metapages in separate device regions) plus the per-chunk results; a batch is
 // {H2D data+meta, page kernel over data, page kernel over metapages, fold to

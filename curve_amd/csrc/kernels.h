@@ -53,6 +53,29 @@ hipError_t upload_x2k(const uint32_t* t64);
 hipError_t launch_shift(const uint32_t* crcs, const uint64_t* shift_bytes, uint64_t n,
                         uint32_t* out, hipStream_t s);
 
+struct UpdateDesc {
+    uint64_t dst, src;
+    uint32_t len, reserved;
+};
+struct UpdateLaunch {
+    unsigned char* pool;
+    const unsigned char* src;
+    const UpdateDesc* upd;
+    uint64_t n_updates;
+    uint32_t page_bytes;
+    uint32_t* flags;            // one word per pool page, zero on entry
+    unsigned long long* list;   // touched page indices
+    unsigned long long* count;  // number of entries in list
+    uint64_t list_cap;
+    // recompute
+    const void* image;
+    uint32_t kconst;
+    uint32_t* page_crcs;
+    int blocks;
+};
+hipError_t launch_apply_updates(const UpdateLaunch& a, hipStream_t s);
+hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s);
+
 hipError_t launch_combine(const uint32_t* a, const uint32_t* b, uint32_t m_len_b, uint64_t n, uint32_t* out,
                           hipStream_t s);
 

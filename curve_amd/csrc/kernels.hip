@@ -389,6 +389,76 @@ __global__ void shift_kernel(const uint32_t* __restrict__ crcs, const uint64_t* 
     out[i] = (c == 0u || nb == 0u) ? c : mulmod_dev(xpow_dev(nb << 3), c);
 }
 
+// ---------------------------------------------------------------------------
+// Partial-write path (BASELINE config 3)
+// ---------------------------------------------------------------------------
+// One wave per update.  Destination-aligned dwords in the middle of the range
+// are assembled from two source dwords with v_alignbyte and stored whole; the
+// head/tail bytes are stored as bytes, so two non-overlapping updates that
+// share a boundary dword never race.  Lane 0 marks the touched pages and
+// appends first-touchers to the recompute list.
+__global__ __launch_bounds__(256) void apply_updates_kernel(UpdateLaunch a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (u >= a.n_updates) return;
+    const UpdateDesc d = a.upd[u];
+    const uint64_t dst = d.dst, src = d.src, len = d.len;
+    if (len == 0) return;
+    const uint64_t end = dst + len;
+    const uint64_t w0 = (dst + 3) & ~3ull;  // first full dst dword
+    const uint64_t w1 = end & ~3ull;        // end of full dst dwords
+    // head / tail bytes
+    for (uint64_t i = lane; i < len; i += 64) {
+        const uint64_t p = dst + i;
+        if (p < w0 || p >= w1 || w0 >= w1) a.pool[p] = a.src[src + i];
+    }
+    if (w0 < w1) {
+        const uint64_t delta = src - dst;  // modular: source byte of dst byte p is p + delta
+        for (uint64_t w = w0 + 4ull * lane; w < w1; w += 256) {
+            const uint64_t sb = w + delta;  // source byte address of dst word w
+            const uint64_t sa = sb & ~3ull;
+            const uint32_t sh = (uint32_t)(sb & 3u);
+            const uint32_t lo = *reinterpret_cast<const uint32_t*>(a.src + sa);
+            // the high dword is only needed (and only in range) when misaligned
+            const uint32_t hi = sh ? *reinterpret_cast<const uint32_t*>(a.src + sa + 4) : 0u;
+            *reinterpret_cast<uint32_t*>(a.pool + w) = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+        }
+    }
+    if (lane == 0) {
+        const uint64_t p0 = dst / a.page_bytes, p1 = (end - 1) / a.page_bytes;
+        for (uint64_t p = p0; p <= p1; p++) {
+            if (atomicExch(a.flags + p, 1u) == 0u) {
+                const unsigned long long slot = atomicAdd(a.count, 1ull);
+                if (slot < a.list_cap) a.list[slot] = p;
+            }
+        }
+    }
+}
+
+// Recompute the CRCs of the listed pages (count read on the device).
+template <int M>
+__global__ __launch_bounds__(kBlockThreads) void page_list_kernel(UpdateLaunch a) {
+    __shared__ uint32_t tab[kLdsBytes / 4];
+    fill_lds(tab, static_cast<const uint4*>(a.image));
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t cnt_raw = __builtin_nontemporal_load(a.count);
+    const uint64_t cnt = cnt_raw < a.list_cap ? cnt_raw : a.list_cap;
+    const uint32_t c0 = lane << 2 & 0x7Cu;
+    const uint32_t c1 = c0 | 0x10000u;
+    const uint32_t cf = kFinBase + (lane << 2);
+    const uint32_t* pages = reinterpret_cast<const uint32_t*>(a.pool) + lane;
+    for (uint64_t k = (uint64_t)blockIdx.x * kWavesPerBlock + wave; k < cnt; k += (uint64_t)gridDim.x * kWavesPerBlock) {
+        const uint64_t p = __builtin_amdgcn_readfirstlane((uint32_t)a.list[k]) |
+                           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a.list[k] >> 32)) << 32);
+        uint32_t w[M];
+        load_page<M>(w, pages + p * (64u * M));
+        const uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, w, c0, c1), cf)) ^ a.kconst;
+        if (lane == 0) a.page_crcs[p] = crc;
+        a.flags[p] = 0u;  // leave the flag array clean for the next call (every lane writes 0)
+    }
+}
+
 __global__ void combine_kernel(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t m,
                                uint64_t n, uint32_t* __restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -456,6 +526,29 @@ hipError_t launch_shift(const uint32_t* crcs, const uint64_t* shift_bytes, uint6
     if (n == 0) return hipSuccess;
     const uint64_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(shift_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, crcs, shift_bytes, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_updates(const UpdateLaunch& a, hipStream_t s) {
+    if (a.n_updates == 0) return hipSuccess;
+    hipLaunchKernelGGL(apply_updates_kernel, dim3((uint32_t)((a.n_updates + 3) / 4)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s) {
+    const uint32_t m = a.page_bytes / kWaveBytes;
+#define CC_LCASE(MM) \
+    case MM: hipLaunchKernelGGL((page_list_kernel<MM>), dim3(a.blocks), dim3(kBlockThreads), 0, s, a); break;
+    switch (m) {
+        CC_LCASE(1)
+        CC_LCASE(2)
+        CC_LCASE(4)
+        CC_LCASE(8)
+        CC_LCASE(16)
+        CC_LCASE(32)
+        default: return hipErrorInvalidValue;
+    }
+#undef CC_LCASE
     return hipGetLastError();
 }
 

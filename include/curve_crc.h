@@ -129,6 +129,31 @@ int cc_digest_dev(const uint32_t* d_file_crcs, const uint64_t* d_after_bytes,
 int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
                      uint32_t* h_out);
 
+/* One byte-range write into a device-resident pool (client partial write). */
+typedef struct cc_update {
+    uint64_t dst; /* byte offset in the pool */
+    uint64_t src; /* byte offset in the source buffer */
+    uint32_t len; /* bytes, >= 1 */
+    uint32_t reserved;
+} cc_update;
+
+/* Scratch bytes cc_apply_updates_dev needs for a pool of n_pages pages and up
+ * to n_updates updates of at most max_len bytes each. */
+uint64_t cc_update_work_bytes(uint64_t n_pages, uint64_t n_updates, uint32_t max_len, uint32_t page_bytes);
+
+/* Client partial-write path (BASELINE config 3): apply n byte-range updates
+ * (any alignment, may straddle pages) to the device pool, then recompute the
+ * CRC of every page they touch, in place in d_page_crcs (untouched pages keep
+ * their CRC).  Reference write path: WriteChunkRequest::OnApply ->
+ * CSChunkFile::Write (op_request.cpp:429-481, chunkserver_chunkfile.cpp:287-427)
+ * writes in raft-log order; the per-page CRC table is new.  Updates
+ * within ONE call must not overlap (the host binding splits an ordered batch at
+ * overlaps into sequential calls, preserving write order).  d_work: >=
+ * cc_update_work_bytes(...) bytes of device scratch. */
+int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
+                         const cc_update* d_updates, uint64_t n_updates, uint32_t max_len,
+                         uint32_t* d_page_crcs, void* d_work, uint64_t work_bytes, void* stream);
+
 /* One chunk file as the datastore holds it: metapage + data
  * (file = metapage || data, chunkserver_chunkfile.cpp:497-536). */
 typedef struct cc_chunk_src {

@@ -285,3 +285,32 @@ def test_scan_host_stream(dev, oracle, pinned):
         assert mc[i] == ref[0][2]
         assert [int(x) for x in sc[i]] == [c for (_, _, c) in ref[1:]]
         assert fc[i] == oracle.crc32c(m.tobytes() + d.tobytes())
+
+
+@pytest.mark.parametrize("page_bytes,n_upd,overlap", [(4096, 3000, False), (4096, 2000, True), (512, 2500, True)])
+def test_partial_writes(dev, oracle, page_bytes, n_upd, overlap):
+    """cc_apply_updates_dev: unaligned sub-page writes (1 B .. >1 page, straddling
+    pages, overlapping in order) -> pool bytes == in-order host application and
+    every page CRC == oracle on the final bytes (touched pages recomputed,
+    untouched ones kept)."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(n_upd + overlap + page_bytes)
+    pool_bytes = 8 << 20
+    host = rng.integers(0, 256, pool_bytes, dtype=np.uint8)
+    d_pool = to_dev(host, dev)
+    crcs = C.page_crc(d_pool, page_bytes)
+    lens = rng.integers(512, 4097, n_upd)
+    lens[:50] = rng.integers(1, 16, 50)          # tiny writes
+    lens[50:60] = page_bytes + 700                 # longer than a page
+    span = 64 << 10 if overlap else pool_bytes - 9000
+    dst = rng.integers(0, span, n_upd)
+    src_data = rng.integers(0, 256, int(lens.sum()) + 8, dtype=np.uint8)
+    src_off = np.concatenate([[0], np.cumsum(lens)[:-1]]) + rng.integers(0, 4, n_upd) * 0
+    nb = C.apply_updates(d_pool, crcs, to_dev(src_data, dev), dst, src_off, lens, page_bytes)
+    assert (nb > 1) == overlap or not overlap
+    want = host.copy()
+    for i in range(n_upd):
+        want[dst[i]:dst[i] + lens[i]] = src_data[src_off[i]:src_off[i] + lens[i]]
+    got = d_pool.cpu().numpy()
+    assert (got == want).all()
+    assert (u32(crcs) == oracle.page_crcs(want, page_bytes, threads=8)).all()
