@@ -149,7 +149,7 @@ def partial_write_leg(pool, args):
     pool_bytes = pool.data.numel()
     src = torch.empty(U * 4096, dtype=torch.uint8, device=dev).random_(0, 256)
     flat = pool.data.view(-1)
-    times, upd_bytes, touched = [], 0, 0
+    times, dev_ms, calls, upd_bytes, touched = [], [], [], 0, 0
     for it in range(args.update_batches + 1):
         lens = rng.integers(512, 4097, U)
         dst = rng.integers(0, pool_bytes - 4096, U)
@@ -157,17 +157,24 @@ def partial_write_leg(pool, args):
         p0, p1 = dst // 4096, (dst + lens - 1) // 4096
         tp = len(np.unique(np.concatenate([p0, p1])))
         torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
-        C.apply_updates(flat, pool.page_crcs, src, dst, src_off, lens, 4096)
+        e0.record()
+        nbatch = C.apply_updates(flat, pool.page_crcs, src, dst, src_off, lens, 4096)
+        e1.record()
         torch.cuda.synchronize()
         if it:  # first batch warms the work buffer
             times.append(time.perf_counter() - t0)
+            dev_ms.append(e0.elapsed_time(e1))
+            calls.append(nbatch)
             upd_bytes += int(lens.sum())
             touched += tp
     el = sum(times)
     alg = 2 * upd_bytes + touched * (4096 + 4)
     return {"updates_per_batch": U, "batches": args.update_batches,
             "ms_per_batch": round(el / len(times) * 1e3, 3),
+            "device_ms_per_batch": round(float(np.mean(dev_ms)), 3),
+            "device_calls_per_batch": float(np.mean(calls)),
             "updates_per_s": round(U * len(times) / el, 1),
             "touched_pages_per_batch": touched // len(times),
             "alg_GBps": round(alg / el / 1e9, 1),

@@ -262,10 +262,14 @@ def _update_dtype():
 
 
 def split_nonoverlapping(dst, lens):
-    """Split an ORDERED list of byte-range writes into consecutive batches whose
-    members do not overlap each other; applying the batches one after another
-    equals applying the writes in order (later writes win on overlaps, as the
-    raft log orders them, op_request.cpp:429-481).  Returns a list of index arrays."""
+    """Split an ORDERED list of byte-range writes into batches whose members do
+    not overlap each other; applying the batches one after another equals
+    applying the writes in order (later writes win, as the raft log orders them,
+    op_request.cpp:429-481).  Level assignment: level(j) = 1 + max level of the
+    earlier writes j overlaps (0 if none); batch b = writes of level b.  The
+    overlap sweep is vectorised (sort by start, running max of ends): random
+    4 KiB writes over 16 GiB overlap in ~0.8 % of cases and need 2-3 batches.
+    Returns a list of index arrays (ascending)."""
     import numpy as np
     dst = np.asarray(dst, dtype=np.int64)
     end = dst + np.asarray(lens, dtype=np.int64)
@@ -273,21 +277,26 @@ def split_nonoverlapping(dst, lens):
     if n == 0:
         return []
     order = np.argsort(dst, kind="stable")
-    if not (end[order][:-1] > dst[order][1:]).any():
+    s_start, s_end = dst[order], end[order]
+    run_max = np.maximum.accumulate(s_end)
+    new_cluster = np.ones(n, dtype=bool)
+    new_cluster[1:] = s_start[1:] >= run_max[:-1]
+    if new_cluster.all():
         return [np.arange(n)]  # no overlaps at all: one batch
-    from sortedcontainers import SortedList
-    batches, cur, ivs = [], [], SortedList()
-    for i in range(n):
-        a, b = int(dst[i]), int(end[i])
-        k = ivs.bisect_left((a, -1))
-        hit = (k < len(ivs) and ivs[k][0] < b) or (k > 0 and ivs[k - 1][1] > a)
-        if hit:
-            batches.append(np.array(cur, dtype=np.int64))
-            cur, ivs = [], SortedList()
-        cur.append(i)
-        ivs.add((a, b))
-    batches.append(np.array(cur, dtype=np.int64))
-    return batches
+    level = np.zeros(n, dtype=np.int64)
+    cid = np.cumsum(new_cluster) - 1
+    starts = np.flatnonzero(new_cluster)
+    sizes = np.diff(np.append(starts, n))
+    for c in np.flatnonzero(sizes > 1):  # only the (few, small) overlapping clusters
+        mem = np.sort(order[starts[c]:starts[c] + sizes[c]])  # original (write) order
+        for x, j in enumerate(mem):
+            lv = 0
+            for i in mem[:x]:
+                if dst[i] < end[j] and dst[j] < end[i]:
+                    lv = max(lv, level[i] + 1)
+            level[j] = lv
+    del cid
+    return [np.flatnonzero(level == v) for v in range(int(level.max()) + 1)]
 
 
 _work_cache = {}
