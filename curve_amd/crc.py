@@ -181,6 +181,28 @@ def shift_dev(crcs, shift_bytes, out=None, stream=None):
     return out
 
 
+def crc_ranges(buf, offsets, lengths, out=None, stream=None):
+    """CRC32C (Value) of arbitrary byte ranges of the device tensor `buf`
+    (cc_crc_ranges_dev) -> int32 device tensor."""
+    import numpy as np
+    torch = _torch()
+    offs = np.asarray(offsets, dtype=np.uint64)
+    lens = np.asarray(lengths, dtype=np.uint64)
+    if offs.size != lens.size:
+        raise CurveCrcError(_lib.CC_EINVAL, "offsets / lengths mismatch")
+    if (offs + lens > _nbytes(buf)).any():
+        raise CurveCrcError(_lib.CC_EINVAL, "range beyond the buffer")
+    rec = np.empty((offs.size, 2), dtype=np.uint64)
+    rec[:, 0], rec[:, 1] = offs, lens
+    d_rec = torch.from_numpy(rec.view(np.uint8).reshape(-1)).to(buf.device)
+    if out is None:
+        out = torch.empty(offs.size, dtype=torch.int32, device=buf.device)
+    with torch.cuda.device(buf.device):
+        check(lib().cc_crc_ranges_dev(_dev_ptr(buf, "buf"), _dev_ptr(d_rec, "ranges"), offs.size,
+                                      _dev_ptr(out, "out"), _stream_handle(stream)), "cc_crc_ranges_dev")
+    return out
+
+
 def combine_dev(a, b, len_b: int, out=None, stream=None):
     """out[i] = combine(a[i], b[i], len_b) on device."""
     torch = _torch()

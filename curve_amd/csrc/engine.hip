@@ -99,6 +99,10 @@ int get_ctx(DevCtx** out) {
         if (e != hipSuccess) return map_err(e);
         e = upload_x2k(x2k().t);
         if (e != hipSuccess) return map_err(e);
+        uint32_t xinv[260];
+        for (uint32_t t = 0; t < 260; t++) xinv[t] = xinv_bytes(t);
+        e = upload_xinv(xinv);
+        if (e != hipSuccess) return map_err(e);
         c->ready = true;
     }
     *out = c;
@@ -300,6 +304,19 @@ int cc_shift_dev(const uint32_t* d_crcs, const uint64_t* d_shift_bytes, uint64_t
     int rc = get_ctx(&c);
     if (rc) return rc;
     return map_err(launch_shift(d_crcs, d_shift_bytes, n, d_out, static_cast<hipStream_t>(stream)));
+}
+
+int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, uint32_t* d_out, void* stream) {
+    if (n == 0) return CC_OK;
+    if (!d_buf || !d_ranges || !d_out) return CC_EINVAL;
+    DevCtx* c = nullptr;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    const uint64_t need = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int blocks = (int)(need < (uint64_t)c->cus ? need : (uint64_t)c->cus);
+    return map_err(launch_range_crc(static_cast<const unsigned char*>(d_buf),
+                                    reinterpret_cast<const RangeDesc*>(d_ranges), n, c->image, d_out, blocks,
+                                    static_cast<hipStream_t>(stream)));
 }
 
 int cc_combine_dev(const uint32_t* d_a, const uint32_t* d_b, uint64_t len_b, uint64_t n, uint32_t* d_out,

@@ -23,6 +23,19 @@ inline uint32_t mulmod(uint32_t a, uint32_t b) {
     return prod;
 }
 
+// b(x) / x mod P (inverse of the "b *= x" step: bit 31 of b*x is bit 0 of b
+// because P's x^0 coefficient -- bit 31 of kPoly -- is 1).
+inline uint32_t div_x(uint32_t b) {
+    return (b & 0x80000000u) ? (((b ^ kPoly) << 1) | 1u) : (b << 1);
+}
+
+// x^(-8t) mod P.
+inline uint32_t xinv_bytes(uint32_t t) {
+    uint32_t r = kOne;
+    for (uint32_t i = 0; i < 8 * t; i++) r = div_x(r);
+    return r;
+}
+
 // x^(2^k) mod P for k = 0..63, built by repeated squaring.
 struct X2kTable {
     uint32_t t[64];

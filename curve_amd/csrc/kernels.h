@@ -76,6 +76,15 @@ struct UpdateLaunch {
 hipError_t launch_apply_updates(const UpdateLaunch& a, hipStream_t s);
 hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s);
 
+struct RangeDesc {
+    uint64_t off, len;
+};
+// CRC32C (butil Value) of arbitrary byte ranges of one device buffer.
+hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, const void* image,
+                            uint32_t* out, int blocks, hipStream_t s);
+// x^(-8t) mod P for t = 0..259 (undoing a row's trailing zero padding)
+hipError_t upload_xinv(const uint32_t* t260);
+
 hipError_t launch_combine(const uint32_t* a, const uint32_t* b, uint32_t m_len_b, uint64_t n, uint32_t* out,
                           hipStream_t s);
 

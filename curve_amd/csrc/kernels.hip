@@ -349,6 +349,67 @@ __device__ __forceinline__ uint32_t xpow_dev(uint64_t n) {
     return r;
 }
 
+struct XInv {
+    uint32_t t[260];
+};
+__constant__ XInv c_xinv;  // x^(-8t) mod P, t = 0..259
+
+// Product over the wave of per-lane GF(2)[x]/P factors (lane k: x^(2^k) if bit k
+// of n is set, else 1) = x^n mod P; result in every lane.
+__device__ __forceinline__ uint32_t xpow_wave(uint64_t n, uint32_t lane) {
+    uint32_t f = (lane < 64 && ((n >> lane) & 1u)) ? c_x2k.t[lane] : 0x80000000u;
+#pragma unroll
+    for (int t = 1; t < 64; t <<= 1) f = mulmod_dev(f, __shfl_xor(f, t, 64));
+    return f;
+}
+
+// ---------------------------------------------------------------------------
+// CRC32C of arbitrary byte ranges (WAL entries on replay, raw-file hashes).
+// One wave per range.  The range [off, off+len) is viewed as R whole 256-byte
+// rows starting at the 4-byte-aligned address a = off & ~3: bytes before off
+// and at/after off+len are masked to zero.  Leading zeros do not change a
+// zero-init (raw) CRC, so the page-kernel chain yields raw(data || 0^t) =
+// shift(raw(data), t) with t = 256R - (off - a) - len; multiplying by
+// x^(-8t) undoes the trailing pad, and K(len) = ~shift(~0, len) converts to
+// butil's Value.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlockThreads) void range_crc_kernel(const unsigned char* __restrict__ buf,
+                                                                  const RangeDesc* __restrict__ ranges, uint64_t n,
+                                                                  const uint4* __restrict__ image,
+                                                                  uint32_t* __restrict__ out) {
+    __shared__ uint32_t tab[kLdsBytes / 4];
+    fill_lds(tab, image);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t c0 = lane << 2 & 0x7Cu;
+    const uint32_t c1 = c0 | 0x10000u;
+    const uint32_t cf = kFinBase + (lane << 2);
+    for (uint64_t r = (uint64_t)blockIdx.x * kWavesPerBlock + wave; r < n; r += (uint64_t)gridDim.x * kWavesPerBlock) {
+        const uint64_t off = ranges[r].off, len = ranges[r].len;
+        if (len == 0) {
+            if (lane == 0) out[r] = 0u;
+            continue;
+        }
+        const uint64_t a = off & ~3ull, end = off + len;
+        const uint64_t rows = (len + (off - a) + 255) >> 8;
+        const uint32_t t = (uint32_t)((rows << 8) - (off - a) - len);
+        auto word = [&](uint64_t j) -> uint32_t {
+            const uint64_t addr = a + (j << 8) + 4ull * lane;
+            if (addr >= end) return 0u;
+            uint32_t w = *reinterpret_cast<const uint32_t*>(buf + addr);
+            if (addr < off) w &= 0xFFFFFFFFu << (8u * (uint32_t)(off - addr));  // bytes before the range
+            if (addr + 4 > end) w &= 0xFFFFFFFFu >> (8u * (uint32_t)(addr + 4 - end));  // bytes after it
+            return w;
+        };
+        uint32_t s = word(0);
+        for (uint64_t j = 1; j < rows; j++) s = apply_g(tab, s, c0, c1) ^ word(j);
+        const uint32_t raw_pad = wave_xor(apply_fin(tab, s, cf));
+        const uint32_t kz = ~mulmod_dev(xpow_wave(len << 3, lane), 0xFFFFFFFFu);
+        const uint32_t v = mulmod_dev(c_xinv.t[t], raw_pad) ^ kz;
+        if (lane == 0) out[r] = v;
+    }
+}
+
 // Fast path: per_group = 64*q.  One wave per group; lane l folds units
 // [l*q, (l+1)*q) by Horner, then a 6-level shuffle tree merges lanes.
 __global__ __launch_bounds__(256) void fold_kernel_wave(const uint32_t* __restrict__ crcs, uint64_t n_groups,
@@ -516,6 +577,16 @@ hipError_t launch_fold(const FoldLaunch& a, hipStream_t s) {
         hipLaunchKernelGGL(fold_kernel_serial, dim3((uint32_t)blocks), dim3(256), 0, s, a.crcs, a.n_groups,
                            a.per_group, a.m_unit, a.out);
     }
+    return hipGetLastError();
+}
+
+hipError_t upload_xinv(const uint32_t* t260) { return hipMemcpyToSymbol(HIP_SYMBOL(c_xinv), t260, sizeof(XInv)); }
+
+hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, const void* image,
+                            uint32_t* out, int blocks, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(range_crc_kernel, dim3(blocks), dim3(kBlockThreads), 0, s, buf, ranges, n,
+                       static_cast<const uint4*>(image), out);
     return hipGetLastError();
 }
 

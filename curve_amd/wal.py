@@ -1,0 +1,100 @@
+"""Raft WAL segment checksums on the device.
+
+Curve's WAL (src/chunkserver/raftlog/curve_segment.cpp) stores per entry a
+28-byte header packed big-endian by butil::RawPacker (:421-428):
+    term u64 | meta_field u32 = type<<24 | checksum_type<<16 | data_len u32
+    | data_real_len u32 | data_checksum u32 | header_checksum u32
+followed by the data zero-padded so that header + data is a multiple of
+walAlignSize (4096, :54, :407-414).  data_checksum = braft::crc32(data[:real_len])
+and header_checksum = braft::crc32(header[:24]); with CHECKSUM_CRC32 (chosen when
+butil::crc32c::IsFastCrc32Supported, curve_segment_log_storage.cpp:76-80)
+braft::crc32 is butil::crc32c::Value.  The segment starts with a meta page whose
+first 8 bytes hold the used byte count (_load_meta, :231-242).
+
+Replay (CurveSegment::load, :148-190) walks the headers sequentially -- that
+walk stays on the host (28 bytes per entry, 24-byte header CRCs on the CPU
+primitive) -- and the data checksums of all entries, the bulk bytes, are
+verified in ONE device call (cc_crc_ranges_dev).
+"""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass
+from typing import List, Sequence, Tuple
+
+from . import crc as C
+
+ENTRY_HEADER_SIZE = 28          # raftlog/define.h:59
+WAL_ALIGN = 4096                # FLAGS_walAlignSize, curve_segment.cpp:54
+CHECKSUM_MURMURHASH32 = 0       # braft::ChecksumType
+CHECKSUM_CRC32 = 1
+ENTRY_TYPE_NO_OP = 1            # braft::EntryType
+ENTRY_TYPE_DATA = 2
+ENTRY_TYPE_CONFIGURATION = 3
+
+
+@dataclass
+class EntryHeader:
+    offset: int
+    term: int
+    type: int
+    checksum_type: int
+    data_len: int
+    data_real_len: int
+    data_checksum: int
+    header_ok: bool
+
+
+def pack_entry(term: int, etype: int, data: bytes, align: int = WAL_ALIGN) -> bytes:
+    """CurveSegment::append layout (curve_segment.cpp:405-440)."""
+    real = len(data)
+    to_write = ENTRY_HEADER_SIZE + real
+    pad = 0 if to_write % align == 0 else (to_write // align + 1) * align - to_write
+    meta_field = (etype << 24) | (CHECKSUM_CRC32 << 16)
+    hdr = struct.pack(">qIIII", term, meta_field, real + pad, real, C.CRC32(data))
+    hdr += struct.pack(">I", C.CRC32(hdr))
+    return hdr + data + bytes(pad)
+
+
+def build_segment(entries: Sequence[Tuple[int, int, bytes]], meta_page_size: int = 4096) -> bytes:
+    """A whole segment file: meta page (used bytes) + packed entries."""
+    body = b"".join(pack_entry(t, ty, d) for t, ty, d in entries)
+    meta = bytearray(meta_page_size)
+    meta[:8] = struct.pack("<q", meta_page_size + len(body))
+    return bytes(meta) + body
+
+
+def parse_segment(seg, meta_page_size: int = 4096) -> List[EntryHeader]:
+    """Header walk of CurveSegment::load (curve_segment.cpp:148-190): stops at a
+    truncated tail or the first corrupted header (reported with header_ok=False)."""
+    mv = memoryview(seg)
+    used = struct.unpack_from("<q", mv, 0)[0]
+    off, out = meta_page_size, []
+    while off < used:
+        if off + ENTRY_HEADER_SIZE > len(mv):
+            break
+        term, meta_field, data_len, real, dck, hck = struct.unpack_from(">qIIIII", mv, off)
+        ok = C.CRC32(bytes(mv[off:off + ENTRY_HEADER_SIZE - 4])) == hck
+        h = EntryHeader(off, term, meta_field >> 24, (meta_field >> 16) & 0xFF, data_len, real, dck, ok)
+        out.append(h)
+        if not ok:
+            break
+        if off + ENTRY_HEADER_SIZE + data_len > used:
+            out.pop()  # last entry not completely written: truncated on load
+            break
+        off += ENTRY_HEADER_SIZE + data_len
+    return out
+
+
+def verify_segment_dev(dev_seg, headers: Sequence[EntryHeader], stream=None):
+    """Data checksums of every parsed entry on the device in one call.
+    Returns (device CRCs, list of indices whose data checksum mismatches)."""
+    import numpy as np
+    crcs = [h for h in headers if h.checksum_type == CHECKSUM_CRC32]
+    offs = [h.offset + ENTRY_HEADER_SIZE for h in crcs]
+    lens = [h.data_real_len for h in crcs]
+    got = C.crc_ranges(dev_seg, offs, lens, stream=stream)
+    vals = np.asarray(C.as_u32(got), dtype=np.uint64)
+    want = np.asarray([h.data_checksum for h in crcs], dtype=np.uint64)
+    bad = [i for i in np.flatnonzero(vals != want).tolist()]
+    return got, bad

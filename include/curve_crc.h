@@ -98,6 +98,21 @@ int cc_page_verify_dev(const void* d_pages, uint64_t n_pages, uint32_t page_byte
 int cc_fold_dev(const uint32_t* d_crcs, uint64_t n_groups, uint32_t per_group,
                 uint64_t unit_bytes, uint32_t* d_out, void* stream);
 
+/* A byte range of a device buffer. */
+typedef struct cc_range {
+    uint64_t off;
+    uint64_t len;
+} cc_range;
+
+/* d_out[i] = crc32c_value(d_buf + off_i, len_i) for arbitrary offsets,
+ * alignments and lengths (0 allowed).  One wavefront per range: meant for
+ * ranges up to ~1 MiB, e.g. raft WAL entries on replay -- the data and header
+ * checksums CurveSegment::_load_entry verifies with braft::crc32
+ * (= butil::crc32c::Value), src/chunkserver/raftlog/curve_segment.cpp:307-371 --
+ * or GetChunkHash's raw-file range (chunkserver_chunkfile.cpp:785-811). */
+int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, uint32_t* d_out,
+                      void* stream);
+
 /* Linear-domain digest contributions (per-copyset digest):
  * d_out[i] = crc32c_shift(d_crcs[i], d_shift_bytes[i]).  XOR of contributions
  * plus a length-only constant reproduces CopysetNode::GetHash's chain. */

@@ -122,3 +122,71 @@ def tile_walk(n_pages: int, blocks: int, ts: int, waves_per_block: int = 16):
                 break
             k, page = k1, p1
     return hashed, flushes
+
+
+POLY = 0x82F63B78
+
+
+def mulmod(a: int, b: int) -> int:
+    prod = 0
+    for i in range(32):
+        if a & (0x80000000 >> i):
+            prod ^= b
+        b = (b >> 1) ^ (POLY if b & 1 else 0)
+    return prod
+
+
+def div_x(b: int) -> int:
+    return (((b ^ POLY) << 1) | 1) & 0xFFFFFFFF if b & 0x80000000 else (b << 1) & 0xFFFFFFFF
+
+
+def xinv_bytes(t: int) -> int:
+    r = 0x80000000
+    for _ in range(8 * t):
+        r = div_x(r)
+    return r
+
+
+def range_crc_model(buf: np.ndarray, off: int, length: int, img: np.ndarray) -> int:
+    """Replay range_crc_kernel for one range of a uint8 buffer."""
+    from curve_amd import crc as C
+    if length == 0:
+        return 0
+    a, end = off & ~3, off + length
+    rows = (length + (off - a) + 255) >> 8
+    t = (rows << 8) - (off - a) - length
+    lane = np.arange(64, dtype=np.uint64)
+    padded = np.zeros(a + rows * 256 + 8, dtype=np.uint8)
+    padded[:buf.size] = buf[:padded.size] if buf.size > padded.size else buf
+    words = []
+    for j in range(rows):
+        addr = a + (j << 8) + 4 * lane
+        w = np.zeros(64, dtype=np.uint32)
+        for l in range(64):
+            ad = int(addr[l])
+            if ad >= end:
+                continue
+            v = int.from_bytes(bytes(padded[ad:ad + 4]), "little")
+            if ad < off:
+                v &= (0xFFFFFFFF << (8 * (off - ad))) & 0xFFFFFFFF
+            if ad + 4 > end:
+                v &= 0xFFFFFFFF >> (8 * (ad + 4 - end))
+            w[l] = v
+        words.append(w)
+    lanes = np.arange(64, dtype=np.uint32)
+    c0 = (lanes << 2) & np.uint32(0x7C)
+    c1 = c0 | np.uint32(0x10000)
+    cf = np.uint32(K_FIN_BASE) + (lanes << 2)
+    s = words[0].copy()
+    for j in range(1, rows):
+        t0 = lds_read(img, v_perm_b32(c0, s, 0x0C060004))
+        t1 = lds_read(img, v_perm_b32(c0, s, 0x0C060104) + 128)
+        t2 = lds_read(img, v_perm_b32(c1, s, 0x0C060204))
+        t3 = lds_read(img, v_perm_b32(c1, s, 0x0C060304) + 128)
+        s = t0 ^ t1 ^ t2 ^ t3 ^ words[j]
+    r = np.zeros_like(s)
+    for n in range(8):
+        v = (s >> np.uint32(4 * n)) & np.uint32(15)
+        r ^= lds_read(img, ((v << np.uint32(8)) | cf) + np.uint32(4096 * n))
+    raw_pad = int(np.bitwise_xor.reduce(r))
+    return mulmod(xinv_bytes(t), raw_pad) ^ C.zeros(length)

@@ -61,3 +61,20 @@ def test_tile_walk_covers_every_page_once(n_pages, cus):
         assert 1 <= cnt <= (1 << ts) and first % (1 << ts) == 0
         covered += range(first, first + cnt)
     assert sorted(covered) == list(range(n_pages))
+
+
+def test_range_model_matches_oracle(oracle, img):
+    rng = np.random.default_rng(42)
+    buf = rng.integers(0, 256, 3000, dtype=np.uint8)
+    cases = [(0, 0), (0, 1), (1, 1), (3, 2), (5, 3), (0, 4), (2, 7), (0, 256), (1, 256), (3, 255),
+             (0, 257), (7, 600), (1000, 1999), (4, 28), (13, 1)]
+    cases += [(int(rng.integers(0, 1500)), int(rng.integers(0, 1400))) for _ in range(25)]
+    for off, ln in cases:
+        assert km.range_crc_model(buf, off, ln, img) == oracle.crc32c(buf[off:off + ln].tobytes()), (off, ln)
+
+
+def test_div_x_inverts_mul_x():
+    rng = np.random.default_rng(1)
+    for b in rng.integers(0, 2**32, 200, dtype=np.uint64).tolist():
+        assert km.div_x(km.mulmod(0x40000000, b)) == b  # (b * x) / x
+    assert km.mulmod(km.xinv_bytes(3), km.mulmod(0x80000000 >> 24, 0xDEADBEEF)) == 0xDEADBEEF  # x^-24 * x^24
