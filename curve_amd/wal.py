@@ -68,7 +68,10 @@ def parse_segment(seg, meta_page_size: int = 4096) -> List[EntryHeader]:
     """Header walk of CurveSegment::load (curve_segment.cpp:148-190): stops at a
     truncated tail or the first corrupted header (reported with header_ok=False)."""
     mv = memoryview(seg)
-    used = struct.unpack_from("<q", mv, 0)[0]
+    # bytes in use per the meta page, bounded by what was actually read: an entry
+    # whose data is cut cannot have its data checksum verified (the reference
+    # fails that entry's later _load_entry with a short pread, :350-355)
+    used = min(struct.unpack_from("<q", mv, 0)[0], len(mv))
     off, out = meta_page_size, []
     while off < used:
         if off + ENTRY_HEADER_SIZE > len(mv):
