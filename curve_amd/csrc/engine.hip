@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/curve_crc.h"
@@ -62,6 +63,8 @@ struct DevCtx {
     void* image = nullptr;
     std::mutex submit;  // serialises *_host calls on this device
     Staging st;
+    std::unordered_map<void*, uint32_t> work_gen;    // partial-write generation per work buffer
+    std::unordered_map<void*, uint64_t> work_pages;
 };
 
 std::mutex g_mu;
@@ -409,11 +412,10 @@ int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
 }
 
 uint64_t cc_update_work_bytes(uint64_t n_pages, uint64_t n_updates, uint32_t max_len, uint32_t page_bytes) {
+    (void)n_updates;
+    (void)max_len;
     if (page_bytes == 0) return 0;
-    const uint64_t span = (uint64_t)max_len / page_bytes + 2;  // pages one update can touch
-    const uint64_t flags = (n_pages * 4 + 255) & ~255ull;
-    const uint64_t list = n_updates * span * 8;
-    return flags + 256 + list;
+    return (n_pages * 4 + 255) & ~255ull;  // one generation tag per page
 }
 
 int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
@@ -429,26 +431,35 @@ int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes,
     int rc = get_ctx(&c);
     if (rc) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    unsigned char* w = static_cast<unsigned char*>(d_work);
-    const uint64_t flags_bytes = (n_pages * 4 + 255) & ~255ull;
+    hipError_t e;
+    // generation tags: a work buffer seen for the first time (or after 2^32-1
+    // calls) is zeroed once; afterwards each call just bumps its tag
+    uint32_t gen;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        uint32_t& g = c->work_gen[d_work];
+        if (g == 0 || g == 0xFFFFFFFFu || c->work_pages[d_work] != n_pages) {
+            if ((e = hipMemsetAsync(d_work, 0, n_pages * 4, s)) != hipSuccess) return map_err(e);
+            g = 0;
+            c->work_pages[d_work] = n_pages;
+        }
+        gen = ++g;
+    }
     UpdateLaunch a = {};
     a.pool = static_cast<unsigned char*>(d_pool);
     a.src = static_cast<const unsigned char*>(d_src);
     a.upd = reinterpret_cast<const UpdateDesc*>(d_updates);
     a.n_updates = n_updates;
     a.page_bytes = page_bytes;
-    a.flags = reinterpret_cast<uint32_t*>(w);
-    a.count = reinterpret_cast<unsigned long long*>(w + flags_bytes);
-    a.list = reinterpret_cast<unsigned long long*>(w + flags_bytes + 256);
-    a.list_cap = n_updates * ((uint64_t)max_len / page_bytes + 2);
+    a.flags = static_cast<uint32_t*>(d_work);
+    a.gen = gen;
+    a.n_pages = n_pages;
     a.image = c->image;
     a.kconst = kconst_for(page_bytes);
     a.page_crcs = d_page_crcs;
-    const uint64_t waves = (uint64_t)c->cus * kWavesPerBlock;
-    const uint64_t want = a.list_cap < waves ? a.list_cap : waves;
-    a.blocks = (int)((want + kWavesPerBlock - 1) / kWavesPerBlock);
-    hipError_t e;
-    if ((e = hipMemsetAsync(w, 0, flags_bytes + 256, s)) != hipSuccess) return map_err(e);
+    const uint64_t tiles = (n_pages + 63) / 64;
+    const uint64_t need = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    a.blocks = (int)(need < (uint64_t)c->cus ? (need ? need : 1) : (uint64_t)c->cus);
     if ((e = launch_apply_updates(a, s)) != hipSuccess) return map_err(e);
     return map_err(launch_page_list_crc(a, s));
 }

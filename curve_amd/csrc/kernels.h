@@ -63,10 +63,9 @@ struct UpdateLaunch {
     const UpdateDesc* upd;
     uint64_t n_updates;
     uint32_t page_bytes;
-    uint32_t* flags;            // one word per pool page, zero on entry
-    unsigned long long* list;   // touched page indices
-    unsigned long long* count;  // number of entries in list
-    uint64_t list_cap;
+    uint32_t* flags;            // one word per pool page: == gen <=> touched by this call
+    uint32_t gen;               // generation tag of this call (never 0)
+    uint64_t n_pages;
     // recompute
     const void* image;
     uint32_t kconst;
