@@ -200,6 +200,8 @@ def crc_ranges(buf, offsets, lengths, out=None, stream=None):
     with torch.cuda.device(buf.device):
         check(lib().cc_crc_ranges_dev(_dev_ptr(buf, "buf"), _dev_ptr(d_rec, "ranges"), offs.size,
                                       _dev_ptr(out, "out"), _stream_handle(stream)), "cc_crc_ranges_dev")
+    if stream is not None:
+        d_rec.record_stream(stream)
     return out
 
 
@@ -341,22 +343,27 @@ def apply_updates(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int 
     n_pages = _nbytes(pool) // page_bytes
     max_len = int(lens.max()) if lens.size else 1
     batches = split_nonoverlapping(dst_off, lens)
-    need = int(lib().cc_update_work_bytes(n_pages, max(len(b) for b in batches) if batches else 0, max_len, page_bytes))
+    need = int(lib().cc_update_work_bytes(n_pages, dst_off.size, max_len, page_bytes))
     key = (pool.device, need)
     work = _work_cache.get(key)
-    if work is None or work.numel() < need:
+    if work is None:
         work = torch.empty(need, dtype=torch.uint8, device=pool.device)
         _work_cache.clear()
         _work_cache[key] = work
-    for b in batches:
-        rec = np.zeros(b.size, dtype=_update_dtype())
-        rec["dst"], rec["src"], rec["len"] = dst_off[b], src_off[b], lens[b]
-        d_upd = torch.from_numpy(rec.view(np.uint8)).to(pool.device)
-        with torch.cuda.device(pool.device):
-            check(lib().cc_apply_updates_dev(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, _dev_ptr(src, "src"),
-                                             _dev_ptr(d_upd, "updates"), b.size, max_len, _dev_ptr(page_crcs, "page_crcs"),
-                                             _dev_ptr(work, "work"), work.numel(), _stream_handle(stream)),
-                  "cc_apply_updates_dev")
+    order = np.concatenate(batches)
+    ends = np.cumsum([b.size for b in batches]).astype(np.uint64)
+    rec = np.zeros(order.size, dtype=_update_dtype())
+    rec["dst"], rec["src"], rec["len"] = dst_off[order], src_off[order], lens[order]
+    d_upd = torch.from_numpy(rec.view(np.uint8)).to(pool.device, non_blocking=False)
+    with torch.cuda.device(pool.device):
+        check(lib().cc_apply_updates_dev(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, _dev_ptr(src, "src"),
+                                         _dev_ptr(d_upd, "updates"), order.size,
+                                         ctypes.c_void_p(ends.ctypes.data), len(batches), max_len,
+                                         _dev_ptr(page_crcs, "page_crcs"), _dev_ptr(work, "work"), work.numel(),
+                                         _stream_handle(stream)),
+              "cc_apply_updates_dev")
+    if stream is not None:  # temp descriptor buffer must outlive the kernels on `stream`
+        d_upd.record_stream(stream)
     return len(batches)
 
 

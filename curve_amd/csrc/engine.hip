@@ -419,8 +419,9 @@ uint64_t cc_update_work_bytes(uint64_t n_pages, uint64_t n_updates, uint32_t max
 }
 
 int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
-                         const cc_update* d_updates, uint64_t n_updates, uint32_t max_len, uint32_t* d_page_crcs,
-                         void* d_work, uint64_t work_bytes, void* stream) {
+                         const cc_update* d_updates, uint64_t n_updates, const uint64_t* h_batch_ends,
+                         uint32_t n_batches, uint32_t max_len, uint32_t* d_page_crcs, void* d_work,
+                         uint64_t work_bytes, void* stream) {
     if (!page_size_ok(page_bytes) || page_bytes / kWaveBytes > 32) return CC_EINVAL;
     if (n_updates == 0) return CC_OK;
     if (!d_pool || !d_src || !d_updates || !d_page_crcs || !d_work || max_len == 0) return CC_EINVAL;
@@ -460,7 +461,19 @@ int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes,
     const uint64_t tiles = (n_pages + 63) / 64;
     const uint64_t need = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     a.blocks = (int)(need < (uint64_t)c->cus ? (need ? need : 1) : (uint64_t)c->cus);
-    if ((e = launch_apply_updates(a, s)) != hipSuccess) return map_err(e);
+    // batches in order (stream-ordered kernels), then ONE recompute pass
+    uint64_t first = 0;
+    const uint32_t nb = h_batch_ends ? n_batches : 1u;
+    for (uint32_t b = 0; b < nb; b++) {
+        const uint64_t last = h_batch_ends ? h_batch_ends[b] : n_updates;
+        if (last < first || last > n_updates) return CC_EINVAL;
+        UpdateLaunch ab = a;
+        ab.upd = a.upd + first;
+        ab.n_updates = last - first;
+        if ((e = launch_apply_updates(ab, s)) != hipSuccess) return map_err(e);
+        first = last;
+    }
+    if (first != n_updates) return CC_EINVAL;
     return map_err(launch_page_list_crc(a, s));
 }
 

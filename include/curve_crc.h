@@ -161,13 +161,17 @@ uint64_t cc_update_work_bytes(uint64_t n_pages, uint64_t n_updates, uint32_t max
  * CRC of every page they touch, in place in d_page_crcs (untouched pages keep
  * their CRC).  Reference write path: WriteChunkRequest::OnApply ->
  * CSChunkFile::Write (op_request.cpp:429-481, chunkserver_chunkfile.cpp:287-427)
- * writes in raft-log order; the per-page CRC table is new.  Updates
- * within ONE call must not overlap (the host binding splits an ordered batch at
- * overlaps into sequential calls, preserving write order).  d_work: >=
- * cc_update_work_bytes(...) bytes of device scratch. */
+ * writes in raft-log order; the per-page CRC table is new.
+ * d_updates is grouped into n_batches consecutive batches ending at
+ * h_batch_ends[b] (host array; NULL = one batch); updates inside a batch must
+ * not overlap, batches are applied in order -- so an ordered write log with
+ * overlaps is expressed by splitting it into levels (the Python binding does).
+ * One recompute pass covers all batches.  d_work: >= cc_update_work_bytes(...)
+ * bytes of device scratch, reused across calls (generation-tagged). */
 int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
-                         const cc_update* d_updates, uint64_t n_updates, uint32_t max_len,
-                         uint32_t* d_page_crcs, void* d_work, uint64_t work_bytes, void* stream);
+                         const cc_update* d_updates, uint64_t n_updates, const uint64_t* h_batch_ends,
+                         uint32_t n_batches, uint32_t max_len, uint32_t* d_page_crcs, void* d_work,
+                         uint64_t work_bytes, void* stream);
 
 /* One chunk file as the datastore holds it: metapage + data
  * (file = metapage || data, chunkserver_chunkfile.cpp:497-536). */
