@@ -8,7 +8,7 @@ namespace cc {
 
 // LDS image geometry of the page kernel (see DESIGN.md "LDS image").
 constexpr uint32_t kLdsBytes = 163840;  // all 160 KiB of a CU's LDS
-constexpr uint32_t kFinBase = 131072;   // per-lane final-shift nibble tables
+constexpr uint32_t kFinBase = 131072;   // per-lane final-shift nibble tables [128K, 160K)
 constexpr uint32_t kWordsPerWaveStep = 64;  // one dword per lane per step
 constexpr uint32_t kWaveBytes = 256;        // bytes consumed per wave step
 #ifndef CC_WAVES
