@@ -323,6 +323,19 @@ def split_nonoverlapping(dst, lens):
     return [np.flatnonzero(level == v) for v in range(int(level.max()) + 1)]
 
 
+def plan_updates(rec_in, max_batches: int = 1 << 16):
+    """cc_plan_updates: write-ordered update records -> (records grouped by
+    overlap level, batch end indices, number of batches)."""
+    import numpy as np
+    n = rec_in.size
+    out = np.empty_like(rec_in)
+    ends = np.zeros(max(1, min(max_batches, n)), dtype=np.uint64)
+    nb = ctypes.c_uint32(0)
+    check(lib().cc_plan_updates(ctypes.c_void_p(rec_in.ctypes.data), n, ctypes.c_void_p(out.ctypes.data),
+                                ctypes.c_void_p(ends.ctypes.data), ends.size, ctypes.byref(nb)), "cc_plan_updates")
+    return out, ends[:nb.value].copy(), nb.value
+
+
 _work_cache = {}
 
 
@@ -342,7 +355,6 @@ def apply_updates(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int 
         raise CurveCrcError(_lib.CC_EINVAL, "update out of range or empty")
     n_pages = _nbytes(pool) // page_bytes
     max_len = int(lens.max()) if lens.size else 1
-    batches = split_nonoverlapping(dst_off, lens)
     need = int(lib().cc_update_work_bytes(n_pages, dst_off.size, max_len, page_bytes))
     key = (pool.device, need)
     work = _work_cache.get(key)
@@ -350,21 +362,20 @@ def apply_updates(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int 
         work = torch.empty(need, dtype=torch.uint8, device=pool.device)
         _work_cache.clear()
         _work_cache[key] = work
-    order = np.concatenate(batches)
-    ends = np.cumsum([b.size for b in batches]).astype(np.uint64)
-    rec = np.zeros(order.size, dtype=_update_dtype())
-    rec["dst"], rec["src"], rec["len"] = dst_off[order], src_off[order], lens[order]
+    rec_in = np.zeros(dst_off.size, dtype=_update_dtype())
+    rec_in["dst"], rec_in["src"], rec_in["len"] = dst_off, src_off, lens
+    rec, ends, nb = plan_updates(rec_in)
     d_upd = torch.from_numpy(rec.view(np.uint8)).to(pool.device, non_blocking=False)
     with torch.cuda.device(pool.device):
         check(lib().cc_apply_updates_dev(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, _dev_ptr(src, "src"),
-                                         _dev_ptr(d_upd, "updates"), order.size,
-                                         ctypes.c_void_p(ends.ctypes.data), len(batches), max_len,
+                                         _dev_ptr(d_upd, "updates"), rec.size,
+                                         ctypes.c_void_p(ends.ctypes.data), nb, max_len,
                                          _dev_ptr(page_crcs, "page_crcs"), _dev_ptr(work, "work"), work.numel(),
                                          _stream_handle(stream)),
               "cc_apply_updates_dev")
     if stream is not None:  # temp descriptor buffer must outlive the kernels on `stream`
         d_upd.record_stream(stream)
-    return len(batches)
+    return nb
 
 
 def as_u32(t) -> "list[int]":

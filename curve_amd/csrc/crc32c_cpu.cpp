@@ -11,6 +11,9 @@
 #include <nmmintrin.h>
 #include <string.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "../../include/curve_crc.h"
 #include "gf2.h"
 
@@ -111,3 +114,73 @@ uint32_t cc_fold_host(const uint32_t* page_crcs, uint64_t n, uint64_t page_bytes
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Partial-write planner (host logic for cc_apply_updates_dev).
+// ---------------------------------------------------------------------------
+extern "C" int cc_plan_updates(const cc_update* in, uint64_t n, cc_update* out, uint64_t* batch_ends,
+                               uint32_t max_batches, uint32_t* n_batches) {
+    if (!n_batches) return CC_EINVAL;
+    *n_batches = 0;
+    if (n == 0) return CC_OK;
+    if (!in || !out || !batch_ends || max_batches == 0 || n > 0xFFFFFFFFull) return CC_EINVAL;
+    // LSD radix sort of (dst, index) pairs, 12-bit digits (count arrays stay
+    // in L1), only as many passes as the largest dst needs
+    uint64_t maxd = 0;
+    std::vector<uint64_t> key(n), ktmp(n);
+    std::vector<uint32_t> idx(n), tmp(n);
+    for (uint64_t i = 0; i < n; i++) {
+        key[i] = in[i].dst;
+        idx[i] = (uint32_t)i;
+        maxd = std::max(maxd, in[i].dst);
+    }
+    for (int shift = 0; shift < 64 && (maxd >> shift); shift += 12) {
+        uint32_t cnt[4097] = {0};
+        for (uint64_t i = 0; i < n; i++) cnt[((key[i] >> shift) & 0xFFF) + 1]++;
+        for (int d = 0; d < 4096; d++) cnt[d + 1] += cnt[d];
+        for (uint64_t i = 0; i < n; i++) {
+            const uint32_t pos = cnt[(key[i] >> shift) & 0xFFF]++;
+            ktmp[pos] = key[i];
+            tmp[pos] = idx[i];
+        }
+        key.swap(ktmp);
+        idx.swap(tmp);
+    }
+    // sweep: clusters of transitively overlapping writes (running max of ends)
+    std::vector<uint32_t> level(n, 0);
+    uint32_t maxlv = 0;
+    uint64_t i = 0;
+    std::vector<uint32_t> mem;
+    while (i < n) {
+        uint64_t j = i + 1;
+        uint64_t run_end = in[idx[i]].dst + in[idx[i]].len;
+        while (j < n && in[idx[j]].dst < run_end) {
+            run_end = std::max(run_end, in[idx[j]].dst + in[idx[j]].len);
+            j++;
+        }
+        if (j - i > 1) {  // overlapping cluster: levels in WRITE order
+            mem.assign(idx.begin() + i, idx.begin() + j);
+            std::sort(mem.begin(), mem.end());
+            for (size_t x = 0; x < mem.size(); x++) {
+                const cc_update& b = in[mem[x]];
+                uint32_t lv = 0;
+                for (size_t y = 0; y < x; y++) {
+                    const cc_update& a = in[mem[y]];
+                    if (a.dst < b.dst + b.len && b.dst < a.dst + a.len) lv = std::max(lv, level[mem[y]] + 1);
+                }
+                level[mem[x]] = lv;
+                maxlv = std::max(maxlv, lv);
+            }
+        }
+        i = j;
+    }
+    if (maxlv + 1 > max_batches) return CC_EINVAL;
+    // stable counting placement by level (write order kept inside a level)
+    std::vector<uint64_t> start(maxlv + 2, 0);
+    for (uint64_t k = 0; k < n; k++) start[level[k] + 1]++;
+    for (uint32_t l = 0; l <= maxlv; l++) start[l + 1] += start[l];
+    for (uint32_t l = 0; l <= maxlv; l++) batch_ends[l] = start[l + 1];
+    for (uint64_t k = 0; k < n; k++) out[start[level[k]]++] = in[k];
+    *n_batches = maxlv + 1;
+    return CC_OK;
+}

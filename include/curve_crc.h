@@ -173,6 +173,16 @@ int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes,
                          uint32_t n_batches, uint32_t max_len, uint32_t* d_page_crcs, void* d_work,
                          uint64_t work_bytes, void* stream);
 
+/* Host-side planner for cc_apply_updates_dev: reorders an ORDERED write log
+ * (h_in, write order, may overlap) into h_out grouped by level -- level(j) =
+ * 1 + max level of the earlier writes j overlaps, 0 if none -- so that no two
+ * writes of one level overlap and applying levels in order equals applying the
+ * log in order (later writes win, as raft-log order does).  h_batch_ends[b] =
+ * end index of level b in h_out; *n_batches = number of levels (<= max_batches,
+ * else CC_EINVAL).  Radix sort by offset + one sweep: O(n). */
+int cc_plan_updates(const cc_update* h_in, uint64_t n, cc_update* h_out, uint64_t* h_batch_ends,
+                    uint32_t max_batches, uint32_t* n_batches);
+
 /* One chunk file as the datastore holds it: metapage + data
  * (file = metapage || data, chunkserver_chunkfile.cpp:497-536). */
 typedef struct cc_chunk_src {

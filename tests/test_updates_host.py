@@ -47,3 +47,44 @@ def test_no_overlap_is_one_batch():
     dst = np.arange(0, 10000, 100)
     assert len(split_nonoverlapping(dst, np.full(dst.size, 100))) == 1
     assert len(split_nonoverlapping(dst, np.full(dst.size, 101))) > 1
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_cpp_planner_matches_levels(seed):
+    """cc_plan_updates (C++) == the Python level assignment, and applying its
+    levels in order equals applying the log in order."""
+    from curve_amd.crc import _update_dtype, plan_updates
+    rng = np.random.default_rng(100 + seed)
+    n, size = 3000, 60000 if seed % 2 else 10 ** 9
+    dst = rng.integers(0, size, n)
+    lens = rng.integers(1, 700, n)
+    rec = np.zeros(n, dtype=_update_dtype())
+    rec["dst"], rec["src"], rec["len"] = dst, np.arange(n), lens
+    out, ends, nb = plan_updates(rec)
+    py = split_nonoverlapping(dst, lens)
+    assert nb == len(py)
+    starts = np.concatenate([[0], ends[:-1]]).astype(int)
+    for b, (s0, e0) in enumerate(zip(starts, ends.astype(int))):
+        assert sorted(out["src"][s0:e0].tolist()) == py[b].tolist()  # same members, src = write index
+        assert (np.diff(out["src"][s0:e0].astype(np.int64)) > 0).all()  # write order kept in a level
+    if size < 10 ** 6:
+        src = [rng.integers(0, 256, l, dtype=np.uint8) for l in lens]
+        want = apply_in_order(np.zeros(size + 800, np.uint8), dst, src, lens, range(n))
+        got = np.zeros(size + 800, np.uint8)
+        for k in range(n):  # levels in order
+            i = int(out["src"][k])
+            got[dst[i]:dst[i] + lens[i]] = src[i]
+        assert (got == want).all()
+
+
+def test_cpp_planner_speed():
+    import time
+    from curve_amd.crc import _update_dtype, plan_updates
+    rng = np.random.default_rng(9)
+    rec = np.zeros(65536, dtype=_update_dtype())
+    rec["dst"] = rng.integers(0, (16 << 30) - 4096, 65536)
+    rec["len"] = rng.integers(512, 4097, 65536)
+    plan_updates(rec)
+    t = time.perf_counter()
+    _, _, nb = plan_updates(rec)
+    assert 2 <= nb <= 4 and time.perf_counter() - t < 0.05
