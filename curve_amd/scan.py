@@ -14,7 +14,7 @@ libcurvecrc's kernels; torch only owns the memory and the stream.
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 from . import crc as C
 
@@ -34,6 +34,17 @@ class ScanMap:
     crc: int
     offset: int
     len: int
+
+
+def compare_maps(local: Optional[ScanMap], followers: Sequence[ScanMap]) -> Tuple[bool, Optional[ScanMap]]:
+    """ScanManager::CompareMap (scan_manager.cpp:367-409): the leader's map must
+    equal BOTH followers' maps in every field (MessageDifferencer::Equals,
+    `index` included).  Returns (consistent, map to push to FailedScanMap)."""
+    if local is None or len(followers) != 2:
+        return False, None  # "waitingNum is 0 but there isn't three scanmap": logged, not failed
+    if local == followers[0] and local == followers[1]:
+        return True, None
+    return False, local
 
 
 def chunk_file_name(chunk_id: int, snap_sn: Optional[int] = None) -> str:
@@ -127,20 +138,26 @@ class DevicePool:
         return out
 
     def chunk_hash(self, c: int, offset: int = 0, length: Optional[int] = None) -> str:
-        """CSChunkFile::GetHash(offset, length) over the raw FILE (metapage at file
-        offset 0), for page-aligned ranges; decimal string like std::to_string."""
+        """CSChunkFile::GetHash(offset, length): to_string(CRC32(0, rawfile[offset,
+        offset+length))) over the raw FILE (metapage at file offset 0, data after
+        it: chunkserver_chunkfile.cpp:785-811), any offset/length inside the file.
+        The metapage part and the data part are hashed on the device
+        (cc_crc_ranges_dev) and combined."""
         if length is None:
             length = self.chunk_size
-        pb = self.page_bytes
-        if offset % pb or length % pb:
-            raise ValueError("device chunk hash needs page-aligned offset/length")
-        file_pages = [("m", 0)] + [("d", i) for i in range(self.chunk_size // pb)]
-        sel = file_pages[offset // pb:(offset + length) // pb]
-        pcs = C.as_u32(self.page_crcs[c * (self.chunk_size // pb):(c + 1) * (self.chunk_size // pb)])
-        meta = C.as_u32(self.meta_crcs[c:c + 1])[0]
-        crcs = [meta if k == "m" else pcs[i] for k, i in sel]
-        import numpy as np
-        return str(C.fold_host(np.array(crcs, dtype=np.uint32), pb)) if crcs else "0"
+        end = offset + length
+        if offset < 0 or end > self.meta_size + self.chunk_size:
+            raise ValueError("range beyond the chunk file")
+        crc, parts = 0, []
+        if offset < self.meta_size:
+            parts.append((self.meta[c], offset, min(end, self.meta_size) - offset))
+        if end > self.meta_size:
+            d0 = max(offset, self.meta_size) - self.meta_size
+            parts.append((self.data[c], d0, end - self.meta_size - d0))
+        for buf, o, n in parts:
+            v = C.as_u32(C.crc_ranges(buf, [o], [n]))[0]
+            crc = C.combine(crc, v, n)
+        return str(crc)
 
     def copyset_digest_partial(self, names: Sequence[str], after_bytes: Sequence[int], group: Sequence[int],
                                n_groups: int, stream=None):

@@ -67,6 +67,9 @@ def test_golden_chunk(dev, oracle, golden):
         [(s["offset"], s["len"], s["crc"]) for s in g["scan_slices"]]
     assert pool.chunk_hash(0, 0, 16 << 20) == g["chunk_hash_0_chunksize"]
     assert pool.chunk_hash(0, 4096, 8192) == g["chunk_hash_4096_8192"]
+    raw = meta + data.tobytes()
+    for off, ln in ((0, 1), (100, 5000), (4095, 2), (4097, 123457), ((16 << 20) - 7, 4096 + 7), (0, (16 << 20) + 4096)):
+        assert pool.chunk_hash(0, off, ln) == oracle.chunk_hash(raw, off, ln), (off, ln)
     assert (int(u32(pool.file_crcs)[0])) == g["whole_file_crc"]
 
 
@@ -351,3 +354,21 @@ def test_wal_segment_replay_verify(dev, oracle):
     d = to_dev(np.frombuffer(bytes(seg), dtype=np.uint8), dev)
     _, bad = wal.verify_segment_dev(d, hs)
     assert bad == [123]
+
+
+def test_copyset_dir_real_chunk_files(dev, oracle, tmp_path):
+    """CopysetNode::GetHash over a directory of real chunk files (+ a stray file):
+    pread into pinned buffers -> cc_scan_host -> combine in std::sort order ==
+    the oracle's chained CRC over the same files."""
+    from curve_amd import chunkfile as CF
+    rng = np.random.default_rng(12)
+    chunk = 1 << 20
+    files = {}
+    for cid in (1, 2, 10, 11, 100, 3):
+        meta = CF.ChunkFileMetaPage(sn=cid).encode()
+        data = rng.integers(0, 256, chunk, dtype=np.uint8).tobytes()
+        CF.write_chunk_file(str(tmp_path / CF.chunk_file_name(cid)), meta, data)
+        files[CF.chunk_file_name(cid)] = meta + data
+    (tmp_path / "chunk_5_snap_1").write_bytes(b"x" * 5000)  # other geometry -> CPU
+    files["chunk_5_snap_1"] = b"x" * 5000
+    assert CF.copyset_hash_dir(str(tmp_path), chunk_size=chunk, batch=4) == oracle.copyset_hash(files)
