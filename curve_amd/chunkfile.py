@@ -132,7 +132,7 @@ def copyset_hash_dir(data_dir: str, chunk_size: int = C.CHUNK_SIZE, meta_size: i
                 if read_into(os.path.join(data_dir, names[i]), pinned[k]) != fsize:
                     raise IOError(f"short read on {names[i]}")
             _, _, fc = C.scan_host([(pinned[k, :meta_size], pinned[k, meta_size:]) for k in range(len(part))],
-                                   chunk_size, meta_size)
+                                   chunk_size, meta_size, C.PAGE_SIZE, min(C.SCAN_SIZE, chunk_size))
             for k, i in enumerate(part):
                 file_crc[i] = int(fc[k])
     crc = 0
