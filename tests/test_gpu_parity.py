@@ -372,3 +372,47 @@ def test_copyset_dir_real_chunk_files(dev, oracle, tmp_path):
     (tmp_path / "chunk_5_snap_1").write_bytes(b"x" * 5000)  # other geometry -> CPU
     files["chunk_5_snap_1"] = b"x" * 5000
     assert CF.copyset_hash_dir(str(tmp_path), chunk_size=chunk, batch=4) == oracle.copyset_hash(files)
+
+
+def test_integrity_job_sidecars(dev, oracle, tmp_path):
+    """IntegrityService over real chunk files: first job creates the per-page CRC
+    sidecars (== oracle page CRCs); after flipping one data byte and one sidecar
+    byte a second job reports exactly that page and the corrupt table."""
+    import os
+    from curve_amd import chunkfile as CF
+    from curve_amd import integrity as I
+    rng = np.random.default_rng(21)
+    chunk = 1 << 20
+    datas = {}
+    for cid in range(1, 8):
+        data = rng.integers(0, 256, chunk, dtype=np.uint8)
+        CF.write_chunk_file(str(tmp_path / CF.chunk_file_name(cid)), CF.ChunkFileMetaPage(sn=cid).encode(), data.tobytes())
+        datas[cid] = data
+    svc = I.IntegrityService(chunk_size=chunk, batch=3)
+    try:
+        svc.ScheduleJob(1, 1, str(tmp_path))
+        j = svc.wait(1, 120)
+        assert j.state == I.IntegrityJobState.FINISHED, j.error
+        assert all(r.table == "created" for r in j.results) and len(j.results) == 7
+        for cid, data in datas.items():
+            with open(I.sidecar_path(str(tmp_path / CF.chunk_file_name(cid))), "rb") as f:
+                _, sn, tab = I.decode_table(f.read())
+            assert sn == cid and (tab == oracle.page_crcs(data, 4096)).all()
+        p3 = str(tmp_path / CF.chunk_file_name(3))
+        with open(p3, "r+b") as f:  # data page 77 of chunk 3
+            f.seek(4096 + 77 * 4096 + 5)
+            b = f.read(1)
+            f.seek(4096 + 77 * 4096 + 5)
+            f.write(bytes([b[0] ^ 0xFF]))
+        s5 = I.sidecar_path(str(tmp_path / CF.chunk_file_name(5)))
+        raw = bytearray(open(s5, "rb").read())
+        raw[100] ^= 1
+        open(s5, "wb").write(bytes(raw))
+        svc.ScheduleJob(2, 1, str(tmp_path))
+        j = svc.wait(2, 120)
+        res = {r.name: r for r in j.results}
+        assert res["chunk_3"].bad_pages == 1 and res["chunk_3"].first_bad == 77
+        assert res["chunk_5"].table == "corrupt"
+        assert all(r.bad_pages == 0 for n, r in res.items() if n != "chunk_3")
+    finally:
+        svc.close()
