@@ -5,7 +5,10 @@ chunk metapage holds version/sn/correctedSn/location/bitmap + a header CRC,
 chunkserver_chunkfile.cpp:64-88), so verify-on-read needs a NEW artefact.  This
 module defines it and drives it through the engine:
 
-Sidecar `<chunk file>.pcrc` (little-endian):
+Sidecar `<copyset dir>/pcrc/<chunk file name>.pcrc` -- deliberately NOT in the
+data directory, because CopysetNode::GetHash (copyset_node.cpp:931-970) chains
+every file listed there and a sidecar would change the copyset hash.
+Layout (little-endian):
     0  magic  b"CVPCRC01"
     8  version u32 (=1) | page_bytes u32 | n_pages u32 | reserved u32
    24  chunk_sn u64       (sn of the chunk when the table was computed)
@@ -80,8 +83,14 @@ def decode_table(buf: bytes):
     return page_bytes, sn, np.frombuffer(body, dtype="<u4").copy()
 
 
-def sidecar_path(chunk_path: str) -> str:
-    return chunk_path + ".pcrc"
+def table_dir_for(data_dir: str) -> str:
+    """<copyset>/data -> <copyset>/pcrc (sibling of the data directory)."""
+    return os.path.join(os.path.dirname(os.path.abspath(data_dir)), "pcrc")
+
+
+def sidecar_path(chunk_path: str, table_dir: Optional[str] = None) -> str:
+    d = table_dir or table_dir_for(os.path.dirname(os.path.abspath(chunk_path)))
+    return os.path.join(d, os.path.basename(chunk_path) + ".pcrc")
 
 
 @dataclass
@@ -227,8 +236,8 @@ class IntegrityService:
 
     def _do(self, job: IntegrityJob):
         fsize = self.chunk_size + self.meta_size
-        names = sorted(n for n in os.listdir(job.data_dir)
-                       if not n.endswith(".pcrc") and os.path.getsize(os.path.join(job.data_dir, n)) == fsize)
+        names = sorted(n for n in os.listdir(job.data_dir) if os.path.getsize(os.path.join(job.data_dir, n)) == fsize)
+        os.makedirs(table_dir_for(job.data_dir), exist_ok=True)
         done = {r.name for r in job.results}
         todo = [n for n in names if n not in done]
         for b0 in range(0, len(todo), self.batch):

@@ -384,6 +384,8 @@ def test_integrity_job_sidecars(dev, oracle, tmp_path):
     rng = np.random.default_rng(21)
     chunk = 1 << 20
     datas = {}
+    tmp_path = tmp_path / "data"  # <copyset>/data; sidecars go to <copyset>/pcrc
+    tmp_path.mkdir()
     for cid in range(1, 8):
         data = rng.integers(0, 256, chunk, dtype=np.uint8)
         CF.write_chunk_file(str(tmp_path / CF.chunk_file_name(cid)), CF.ChunkFileMetaPage(sn=cid).encode(), data.tobytes())
@@ -394,6 +396,7 @@ def test_integrity_job_sidecars(dev, oracle, tmp_path):
         j = svc.wait(1, 120)
         assert j.state == I.IntegrityJobState.FINISHED, j.error
         assert all(r.table == "created" for r in j.results) and len(j.results) == 7
+        assert sorted(os.listdir(tmp_path)) == sorted(CF.chunk_file_name(c) for c in datas)  # data dir untouched
         for cid, data in datas.items():
             with open(I.sidecar_path(str(tmp_path / CF.chunk_file_name(cid))), "rb") as f:
                 _, sn, tab = I.decode_table(f.read())
