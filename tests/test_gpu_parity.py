@@ -419,3 +419,28 @@ def test_integrity_job_sidecars(dev, oracle, tmp_path):
         assert all(r.bad_pages == 0 for n, r in res.items() if n != "chunk_3")
     finally:
         svc.close()
+
+
+def test_host_calls_from_many_threads(dev, oracle):
+    """Blocking *_host calls from 6 threads at once (apply-thread shape): the
+    per-device submission lock serialises them, every result is exact."""
+    import threading
+    from curve_amd import crc as C
+    rng = np.random.default_rng(44)
+    bufs = [rng.integers(0, 256, 4096 * int(rng.integers(1, 3000)), dtype=np.uint8) for _ in range(6)]
+    out = [None] * 6
+    errs = []
+
+    def work(i):
+        try:
+            for _ in range(3):
+                out[i] = C.page_crc_host(bufs[i], 4096)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(6)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errs
+    for i in range(6):
+        assert (out[i] == oracle.page_crcs(bufs[i], 4096)).all()
