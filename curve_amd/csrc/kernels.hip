@@ -407,24 +407,34 @@ __global__ __launch_bounds__(kBlockThreads) void range_crc_kernel(const unsigned
     }
 }
 
-// Fast path: per_group = 64*q.  One wave per group; lane l folds units
-// [l*q, (l+1)*q) by Horner, then a 6-level shuffle tree merges lanes.
+// Fast path: per_group = 64*q.  One wave per group, grid-stride over groups;
+// lane l folds units [l*q, (l+1)*q) by Horner with the constant multiplier
+// m_unit applied through a 4 x 256-entry product table in LDS (4 lookups +
+// 2 v_bitop3 instead of a 32-step multiply), then a 6-level shuffle tree merges
+// lanes (one multiply per level).
 __global__ __launch_bounds__(256) void fold_kernel_wave(const uint32_t* __restrict__ crcs, uint64_t n_groups,
                                                         uint32_t per_group, FoldLaunch a,
                                                         uint32_t* __restrict__ out) {
+    __shared__ uint32_t mt[4][256];
+    for (uint32_t i = threadIdx.x; i < 1024; i += 256) mt[i >> 8][i & 255] = mulmod_dev(a.m_unit, (i & 255u) << (8 * (i >> 8)));
+    __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (g >= n_groups) return;
     const uint32_t q = per_group >> 6;
-    const uint32_t* p = crcs + g * per_group + (uint64_t)lane * q;
-    uint32_t s = p[0];
-    for (uint32_t i = 1; i < q; i++) s = mulmod_dev(a.m_unit, s) ^ p[i];
+    for (uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < n_groups; g += (uint64_t)gridDim.x * 4) {
+        const uint32_t* p = crcs + g * per_group + (uint64_t)lane * q;
+        uint32_t s = p[0];
+        for (uint32_t i = 1; i < q; i++) {
+            const uint32_t t = __builtin_amdgcn_bitop3_b32(mt[0][s & 255u], mt[1][(s >> 8) & 255u],
+                                                           mt[2][(s >> 16) & 255u], 0x96);
+            s = __builtin_amdgcn_bitop3_b32(t, mt[3][s >> 24], p[i], 0x96);
+        }
 #pragma unroll
-    for (int t = 0; t < 6; t++) {
-        const uint32_t other = __shfl_down(s, 1u << t, 64);
-        if ((lane & ((2u << t) - 1u)) == 0) s = mulmod_dev(a.m_tree[t], s) ^ other;
+        for (int t = 0; t < 6; t++) {
+            const uint32_t other = __shfl_down(s, 1u << t, 64);
+            if ((lane & ((2u << t) - 1u)) == 0) s = mulmod_dev(a.m_tree[t], s) ^ other;
+        }
+        if (lane == 0) out[g] = s;
     }
-    if (lane == 0) out[g] = s;
 }
 
 // Generic path: one thread per group, serial combine.
@@ -538,14 +548,19 @@ __global__ void combine_kernel(const uint32_t* __restrict__ a, const uint32_t* _
     out[i] = mulmod_dev(m, a[i]) ^ b[i];
 }
 
-__global__ void digest_kernel(const uint32_t* __restrict__ crcs, const uint64_t* __restrict__ after,
-                              const uint32_t* __restrict__ group, uint64_t n, uint32_t* __restrict__ digest) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t c = crcs[i];
-    const uint64_t nb = after[i];
-    const uint32_t v = (c == 0u || nb == 0u) ? c : mulmod_dev(xpow_dev(nb << 3), c);
-    atomicXor(digest + group[i], v);
+// One wave per file: x^(8*after) as a wave-parallel product of x^(2^k)
+// factors (6 shuffle-multiply levels instead of ~40 serial multiplies).
+__global__ __launch_bounds__(256) void digest_kernel(const uint32_t* __restrict__ crcs,
+                                                     const uint64_t* __restrict__ after,
+                                                     const uint32_t* __restrict__ group, uint64_t n,
+                                                     uint32_t* __restrict__ digest) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += (uint64_t)gridDim.x * 4) {
+        const uint32_t c = crcs[i];
+        const uint64_t nb = after[i];
+        const uint32_t m = xpow_wave(nb << 3, lane);
+        if (lane == 0) atomicXor(digest + group[i], mulmod_dev(m, c));
+    }
 }
 
 template <int MODE>
@@ -580,7 +595,8 @@ hipError_t launch_page_verify(const PageLaunch& a, hipStream_t s) { return launc
 hipError_t launch_fold(const FoldLaunch& a, hipStream_t s) {
     if (a.n_groups == 0) return hipSuccess;
     if (a.per_group >= 64 && a.per_group % 64 == 0) {
-        const uint64_t blocks = (a.n_groups + 3) / 4;
+        uint64_t blocks = (a.n_groups + 3) / 4;
+        if (blocks > 2048) blocks = 2048;  // grid-stride: the LDS product table is built once per block
         hipLaunchKernelGGL(fold_kernel_wave, dim3((uint32_t)blocks), dim3(256), 0, s, a.crcs, a.n_groups,
                            a.per_group, a, a.out);
     } else {
@@ -645,7 +661,8 @@ hipError_t launch_combine(const uint32_t* a, const uint32_t* b, uint32_t m_len_b
 hipError_t launch_digest(const uint32_t* crcs, const uint64_t* after_bytes, const uint32_t* group, uint64_t n,
                          uint32_t* digest, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const uint64_t blocks = (n + 255) / 256;
+    uint64_t blocks = (n + 3) / 4;
+    if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(digest_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, crcs, after_bytes, group, n, digest);
     return hipGetLastError();
 }
