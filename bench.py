@@ -252,11 +252,10 @@ def main():
             e1.record(stream)
             ev.append((e0, e1))
         C.page_crc(pool.meta, meta_sz, out=pool.meta_crcs[:n])
-        C.fold(pool.page_crcs, C.SCAN_SIZE // pb, pb, out=pool.slice_crcs)
-        C.fold(pool.slice_crcs, chunk // C.SCAN_SIZE, C.SCAN_SIZE, out=pool.data_crcs)
-        C.combine_dev(pool.meta_crcs[:n], pool.data_crcs, chunk, out=pool.file_crcs)
         digest.zero_()
-        C.digest_dev(pool.file_crcs, after, group, lay.n_groups, out=digest)
+        # fused epilogue: slice CRCs (ScanMap.crc) + file CRCs + digest partials, one launch
+        C.scan_epilogue(pool.page_crcs, pool.meta_crcs[:n], n, chunk // pb, pb, C.SCAN_SIZE // pb,
+                        pool.slice_crcs, pool.file_crcs, after, group, digest)
         full_digest[0] = reduce_digests(digest, dist) if world > 1 else digest
 
     for _ in range(args.warmup):
@@ -308,7 +307,7 @@ def main():
         "dtype": "u32",
         "data": "synthetic (uniform random bytes generated in HBM)",
         "config": {"workload": f"{n} x 16 MiB chunk files per GPU (+4 KiB metapages), 4 KiB pages: "
-                               "page CRC + 4 MiB slice fold + file CRC + per-copyset digest"
+                               "page CRC + fused epilogue (4 MiB slice CRCs, file CRC, per-copyset digest)"
                                + (" + RCCL all_gather of digests" if world > 1 else ""),
                    "chunks_per_gpu": n, "page_bytes": pb, "copysets": N_COPYSETS,
                    "parallelism": f"chunk-range shard x{world}"},

@@ -205,6 +205,21 @@ def crc_ranges(buf, offsets, lengths, out=None, stream=None):
     return out
 
 
+def scan_epilogue(page_crcs, meta_crcs, n_chunks: int, pages_per_chunk: int, page_bytes: int,
+                  pages_per_slice: int, slice_out, file_out=None, after_bytes=None, group=None, digest=None,
+                  stream=None):
+    """Fused epilogue (cc_scan_epilogue_dev): slices, file CRCs, digest partials in one launch."""
+    torch = _torch()
+    opt = lambda t, w: _dev_ptr(t, w) if t is not None else None  # noqa: E731
+    with torch.cuda.device(page_crcs.device):
+        check(lib().cc_scan_epilogue_dev(_dev_ptr(page_crcs, "page_crcs"), _dev_ptr(meta_crcs, "meta_crcs"),
+                                         n_chunks, pages_per_chunk, page_bytes, pages_per_slice,
+                                         _dev_ptr(slice_out, "slice_out"), opt(file_out, "file_out"),
+                                         opt(after_bytes, "after_bytes"), opt(group, "group"), opt(digest, "digest"),
+                                         _stream_handle(stream)), "cc_scan_epilogue_dev")
+    return slice_out
+
+
 def combine_dev(a, b, len_b: int, out=None, stream=None):
     """out[i] = combine(a[i], b[i], len_b) on device."""
     torch = _torch()

@@ -322,6 +322,52 @@ int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, u
                                     static_cast<hipStream_t>(stream)));
 }
 
+namespace cc {
+namespace {
+// Geometry check + multipliers for the fused epilogue; false if unsupported.
+bool epilogue_geometry(uint32_t pages_per_chunk, uint32_t page_bytes, uint32_t pages_per_slice, EpilogueLaunch* a) {
+    if (pages_per_chunk == 0 || pages_per_chunk % 256 || pages_per_slice == 0) return false;
+    const uint32_t q = pages_per_chunk / 256;
+    if (pages_per_slice % q) return false;
+    const uint32_t tps = pages_per_slice / q;  // threads per slice
+    if (tps & (tps - 1) || tps > 256) return false;
+    uint32_t j = 0;
+    while ((1u << j) < tps) j++;
+    a->pages_per_chunk = pages_per_chunk;
+    a->q = q;
+    a->slice_shift = j;
+    a->m_page = xpow((uint64_t)page_bytes << 3);
+    for (int k = 0; k < 8; k++) a->m_level[k] = xpow(((uint64_t)page_bytes * q << k) << 3);
+    a->m_chunk = xpow((uint64_t)pages_per_chunk * page_bytes << 3);
+    return true;
+}
+}  // namespace
+}  // namespace cc
+
+int cc_scan_epilogue_dev(const uint32_t* d_page_crcs, const uint32_t* d_meta_crcs, uint64_t n_chunks,
+                         uint32_t pages_per_chunk, uint32_t page_bytes, uint32_t pages_per_slice,
+                         uint32_t* d_slice_crcs, uint32_t* d_file_crcs, const uint64_t* d_after_bytes,
+                         const uint32_t* d_group, uint32_t* d_digest, void* stream) {
+    if (n_chunks == 0) return CC_OK;
+    if (!d_page_crcs || !d_meta_crcs || !d_slice_crcs || page_bytes == 0) return CC_EINVAL;
+    const bool dig = d_after_bytes || d_group || d_digest;
+    if (dig && !(d_after_bytes && d_group && d_digest)) return CC_EINVAL;
+    EpilogueLaunch a = {};
+    if (!epilogue_geometry(pages_per_chunk, page_bytes, pages_per_slice, &a)) return CC_EINVAL;
+    DevCtx* c = nullptr;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    a.page_crcs = d_page_crcs;
+    a.meta_crcs = d_meta_crcs;
+    a.n_chunks = n_chunks;
+    a.slice_crcs = d_slice_crcs;
+    a.file_crcs = d_file_crcs;
+    a.after_bytes = d_after_bytes;
+    a.group = d_group;
+    a.digest = d_digest;
+    return map_err(launch_epilogue(a, static_cast<hipStream_t>(stream)));
+}
+
 int cc_combine_dev(const uint32_t* d_a, const uint32_t* d_b, uint64_t len_b, uint64_t n, uint32_t* d_out,
                    void* stream) {
     if (n == 0) return CC_OK;
@@ -514,6 +560,9 @@ int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_b
     f2.m_unit = xpow((uint64_t)slice_bytes << 3);
     for (int t = 0; t < 6; t++) f2.m_tree[t] = xpow(((uint64_t)slice_bytes * (slices / 64) << t) << 3);
     const uint32_t m_chunk = xpow((uint64_t)chunk_bytes << 3);
+    EpilogueLaunch epi = {};
+    const bool use_epi = chunk_bytes % page_bytes == 0 &&
+                         epilogue_geometry((uint32_t)pages_per_chunk, page_bytes, slice_bytes / page_bytes, &epi);
 
     const bool pinned0 = is_pinned(chunks[0].data) && is_pinned(chunks[0].meta);
     uint64_t pend_first[2] = {0, 0}, pend_n[2] = {0, 0};
@@ -582,15 +631,25 @@ int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_b
         a.out = d_meta;
         geometry_for(c, nb, &a);
         if ((e = launch_page_crc(a, s)) != hipSuccess) return map_err(e);
-        f1.crcs = d_pages;
-        f1.n_groups = nb * slices;
-        f1.out = d_slices;
-        if ((e = launch_fold(f1, s)) != hipSuccess) return map_err(e);
-        f2.crcs = d_slices;
-        f2.n_groups = nb;
-        f2.out = d_data;
-        if ((e = launch_fold(f2, s)) != hipSuccess) return map_err(e);
-        if ((e = launch_combine(d_meta, d_data, m_chunk, nb, d_file, s)) != hipSuccess) return map_err(e);
+        if (use_epi) {  // one fused launch: slices + file CRCs
+            EpilogueLaunch ea = epi;
+            ea.page_crcs = d_pages;
+            ea.meta_crcs = d_meta;
+            ea.n_chunks = nb;
+            ea.slice_crcs = d_slices;
+            ea.file_crcs = d_file;
+            if ((e = launch_epilogue(ea, s)) != hipSuccess) return map_err(e);
+        } else {
+            f1.crcs = d_pages;
+            f1.n_groups = nb * slices;
+            f1.out = d_slices;
+            if ((e = launch_fold(f1, s)) != hipSuccess) return map_err(e);
+            f2.crcs = d_slices;
+            f2.n_groups = nb;
+            f2.out = d_data;
+            if ((e = launch_fold(f2, s)) != hipSuccess) return map_err(e);
+            if ((e = launch_combine(d_meta, d_data, m_chunk, nb, d_file, s)) != hipSuccess) return map_err(e);
+        }
         if ((e = hipMemcpyAsync(st.hcrc[slot], res, nb * (2 + (uint64_t)slices) * 4, hipMemcpyDeviceToHost, s)) !=
             hipSuccess)
             return map_err(e);

@@ -84,6 +84,25 @@ hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, u
 // x^(-8t) mod P for t = 0..259 (undoing a row's trailing zero padding)
 hipError_t upload_xinv(const uint32_t* t260);
 
+// Fused scan epilogue: one 256-thread block per chunk.
+struct EpilogueLaunch {
+    const uint32_t* page_crcs;  // [n_chunks * pages_per_chunk]
+    const uint32_t* meta_crcs;  // [n_chunks]
+    uint64_t n_chunks;
+    uint32_t pages_per_chunk;   // 256 * q
+    uint32_t q;                 // pages per thread
+    uint32_t slice_shift;       // log2(threads per slice)
+    uint32_t m_page;            // x^(8 * page_bytes)
+    uint32_t m_level[8];        // x^(8 * page_bytes * q * 2^k)
+    uint32_t m_chunk;           // x^(8 * chunk_bytes)
+    uint32_t* slice_crcs;       // [n_chunks * 256 >> slice_shift]
+    uint32_t* file_crcs;        // [n_chunks] (may be null)
+    const uint64_t* after_bytes;  // digest inputs (all three null = no digest)
+    const uint32_t* group;
+    uint32_t* digest;
+};
+hipError_t launch_epilogue(const EpilogueLaunch& a, hipStream_t s);
+
 hipError_t launch_combine(const uint32_t* a, const uint32_t* b, uint32_t m_len_b, uint64_t n, uint32_t* out,
                           hipStream_t s);
 

@@ -437,6 +437,64 @@ __global__ __launch_bounds__(256) void fold_kernel_wave(const uint32_t* __restri
     }
 }
 
+// ---------------------------------------------------------------------------
+// Fused scan epilogue (one launch per batch instead of fold + fold + combine +
+// digest): block b = chunk b, 256 threads.  Thread t loads its q page CRCs
+// (coalesced), folds them by Horner through an LDS product table of
+// x^(8*page_bytes), then a combine tree over threads (shuffles inside a wave,
+// LDS across the 4 waves): after slice_shift levels thread (k << slice_shift)
+// holds slice k's CRC (ScanMap.crc), after 8 levels thread 0 holds the chunk
+// data CRC -> file CRC = combine(metapage CRC, data CRC, chunk_bytes) -> digest
+// contribution atomicXor'ed into its copyset.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void epilogue_kernel(EpilogueLaunch a) {
+    __shared__ uint32_t mt[4][256];
+    __shared__ uint32_t part[4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    for (uint32_t i = t; i < 1024; i += 256) mt[i >> 8][i & 255] = mulmod_dev(a.m_page, (i & 255u) << (8 * (i >> 8)));
+    __syncthreads();
+    const uint32_t slices = 256u >> a.slice_shift;
+    for (uint64_t c = blockIdx.x; c < a.n_chunks; c += gridDim.x) {
+        const uint32_t* p = a.page_crcs + c * a.pages_per_chunk + (uint64_t)t * a.q;
+        uint32_t s = p[0];
+        for (uint32_t i = 1; i < a.q; i++) {
+            const uint32_t u = __builtin_amdgcn_bitop3_b32(mt[0][s & 255u], mt[1][(s >> 8) & 255u],
+                                                           mt[2][(s >> 16) & 255u], 0x96);
+            s = __builtin_amdgcn_bitop3_b32(u, mt[3][s >> 24], p[i], 0x96);
+        }
+        if (a.slice_shift == 0) a.slice_crcs[c * 256 + t] = s;  // one thread per slice
+        // levels 0..5 inside the wave
+#pragma unroll
+        for (uint32_t k = 0; k < 6; k++) {
+            const uint32_t other = __shfl_down(s, 1u << k, 64);
+            if ((lane & ((2u << k) - 1u)) == 0) s = mulmod_dev(a.m_level[k], s) ^ other;
+            if (k + 1 == a.slice_shift && (t & ((2u << k) - 1u)) == 0) a.slice_crcs[c * slices + (t >> a.slice_shift)] = s;
+        }
+        // levels 6..7 across the 4 waves
+        if (lane == 0) part[wv] = s;
+        __syncthreads();
+        if (t == 0) {
+            uint32_t w0 = mulmod_dev(a.m_level[6], part[0]) ^ part[1];
+            uint32_t w1 = mulmod_dev(a.m_level[6], part[2]) ^ part[3];
+            if (a.slice_shift == 7) {
+                a.slice_crcs[c * 2] = w0;
+                a.slice_crcs[c * 2 + 1] = w1;
+            }
+            const uint32_t data = mulmod_dev(a.m_level[7], w0) ^ w1;
+            if (a.slice_shift == 8) a.slice_crcs[c] = data;
+            const uint32_t file = mulmod_dev(a.m_chunk, a.meta_crcs[c]) ^ data;
+            if (a.file_crcs) a.file_crcs[c] = file;
+            part[0] = file;
+        }
+        __syncthreads();
+        if (a.digest && wv == 0) {  // digest contribution: x^(8*after) as a wave product
+            const uint32_t m = xpow_wave(a.after_bytes[c] << 3, lane);
+            if (lane == 0) atomicXor(a.digest + a.group[c], mulmod_dev(m, part[0]));
+        }
+        __syncthreads();
+    }
+}
+
 // Generic path: one thread per group, serial combine.
 __global__ void fold_kernel_serial(const uint32_t* __restrict__ crcs, uint64_t n_groups, uint32_t per_group,
                                    uint32_t m_unit, uint32_t* __restrict__ out) {
@@ -647,6 +705,13 @@ hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s) {
         default: return hipErrorInvalidValue;
     }
 #undef CC_LCASE
+    return hipGetLastError();
+}
+
+hipError_t launch_epilogue(const EpilogueLaunch& a, hipStream_t s) {
+    if (a.n_chunks == 0) return hipSuccess;
+    const uint64_t blocks = a.n_chunks < 8192 ? a.n_chunks : 8192;
+    hipLaunchKernelGGL(epilogue_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

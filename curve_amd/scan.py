@@ -105,15 +105,31 @@ class DevicePool:
         C.page_crc(self.data, self.page_bytes, out=self.page_crcs, stream=stream)
         return self.page_crcs
 
-    def scan(self, stream=None):
-        """Page CRCs -> 4 MiB slice CRCs (ScanMap.crc), metapage CRCs, chunk-data
-        and chunk-file CRCs; everything stays on the device."""
+    def epilogue_ok(self) -> bool:
+        ppc, pps = self.chunk_size // self.page_bytes, self.scan_size // self.page_bytes
+        if ppc % 256:
+            return False
+        q = ppc // 256
+        return pps % q == 0 and (pps // q) & (pps // q - 1) == 0 and pps // q <= 256
+
+    def scan(self, stream=None, after_bytes=None, group=None, digest=None):
+        """Page CRCs -> 4 MiB slice CRCs (ScanMap.crc), metapage CRCs and
+        chunk-file CRCs (+ optionally the per-copyset digest partials); all on
+        the device.  The epilogue is ONE fused launch (cc_scan_epilogue_dev)
+        when the geometry allows, else fold + fold + combine (+ digest)."""
         self.hash_pages(stream)
         C.page_crc(self.meta, self.meta_size, out=self.meta_crcs[: self.n], stream=stream)
         per_slice = self.scan_size // self.page_bytes
+        if self.epilogue_ok():
+            C.scan_epilogue(self.page_crcs, self.meta_crcs[: self.n], self.n, self.chunk_size // self.page_bytes,
+                            self.page_bytes, per_slice, self.slice_crcs, self.file_crcs,
+                            after_bytes, group, digest, stream=stream)
+            return self.slice_crcs
         C.fold(self.page_crcs, per_slice, self.page_bytes, out=self.slice_crcs, stream=stream)
         C.fold(self.slice_crcs, self.chunk_size // self.scan_size, self.scan_size, out=self.data_crcs, stream=stream)
         C.combine_dev(self.meta_crcs[: self.n], self.data_crcs, self.chunk_size, out=self.file_crcs, stream=stream)
+        if digest is not None:
+            C.digest_dev(self.file_crcs, after_bytes, group, digest.numel(), out=digest, stream=stream)
         return self.slice_crcs
 
     def verify(self, expected_page_crcs, stream=None):

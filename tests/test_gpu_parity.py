@@ -444,3 +444,32 @@ def test_host_calls_from_many_threads(dev, oracle):
     assert not errs
     for i in range(6):
         assert (out[i] == oracle.page_crcs(bufs[i], 4096)).all()
+
+
+@pytest.mark.parametrize("ppc,pps", [(4096, 1024), (256, 64), (256, 256), (512, 2), (1024, 512), (1024, 4), (768, 96)])
+def test_scan_epilogue_geometries(dev, oracle, ppc, pps):
+    """cc_scan_epilogue_dev (one launch) == fold_host per slice / file, and the
+    digest partials == shifted file CRCs XORed per group."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(ppc * 7 + pps)
+    n, pb = 9, 4096
+    pages = rng.integers(0, 2**32, n * ppc, dtype=np.uint64).astype(np.uint32)
+    metas = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    S = ppc // pps
+    sl = torch.zeros(n * S, dtype=torch.int32, device=dev)
+    fc = torch.zeros(n, dtype=torch.int32, device=dev)
+    after = rng.integers(0, 1 << 36, n, dtype=np.int64)
+    grp = rng.integers(0, 3, n).astype(np.int32)
+    dig = torch.zeros(3, dtype=torch.int32, device=dev)
+    C.scan_epilogue(to_dev(pages.view(np.int32), dev), to_dev(metas.view(np.int32), dev), n, ppc, pb, pps,
+                    sl, fc, to_dev(after, dev), to_dev(grp, dev), dig)
+    want_sl, want_fc, want_dig = [], [], [0, 0, 0]
+    for c in range(n):
+        pc = pages[c * ppc:(c + 1) * ppc]
+        want_sl += [C.fold_host(pc[k * pps:(k + 1) * pps], pb) for k in range(S)]
+        f = C.combine(int(metas[c]), C.fold_host(pc, pb), ppc * pb)
+        want_fc.append(f)
+        want_dig[grp[c]] ^= C.shift(f, int(after[c]))
+    assert [int(x) for x in u32(sl)] == want_sl
+    assert [int(x) for x in u32(fc)] == want_fc
+    assert [int(x) for x in u32(dig)] == want_dig
