@@ -50,6 +50,7 @@ SIGNATURES = {
     "cc_fold_dev": (_int, [_vp, _u64, _u32, _u64, _vp, _vp]),
     "cc_shift_dev": (_int, [_vp, _vp, _u64, _vp, _vp]),
     "cc_crc_ranges_dev": (_int, [_vp, _vp, _u64, _vp, _vp]),
+    "cc_xpow8_dev": (_int, [_vp, _u64, _vp, _vp]),
     "cc_scan_epilogue_dev": (_int, [_vp, _vp, _u64, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "cc_combine_dev": (_int, [_vp, _vp, _u64, _u64, _vp, _vp]),
     "cc_digest_dev": (_int, [_vp, _vp, _vp, _u64, _vp, _vp]),

@@ -205,17 +205,29 @@ def crc_ranges(buf, offsets, lengths, out=None, stream=None):
     return out
 
 
+def xpow8(nbytes, out=None, stream=None):
+    """x^(8*n) mod P per element (cc_xpow8_dev): the shift multipliers of a static layout."""
+    torch = _torch()
+    if out is None:
+        out = torch.empty(nbytes.numel(), dtype=torch.int32, device=nbytes.device)
+    with torch.cuda.device(nbytes.device):
+        check(lib().cc_xpow8_dev(_dev_ptr(nbytes, "nbytes"), nbytes.numel(), _dev_ptr(out, "out"),
+                                 _stream_handle(stream)), "cc_xpow8_dev")
+    return out
+
+
 def scan_epilogue(page_crcs, meta_crcs, n_chunks: int, pages_per_chunk: int, page_bytes: int,
-                  pages_per_slice: int, slice_out, file_out=None, after_bytes=None, group=None, digest=None,
+                  pages_per_slice: int, slice_out, file_out=None, after_mult=None, group=None, digest=None,
                   stream=None):
-    """Fused epilogue (cc_scan_epilogue_dev): slices, file CRCs, digest partials in one launch."""
+    """Fused epilogue (cc_scan_epilogue_dev): slices, file CRCs, digest partials in
+    one launch.  after_mult = xpow8(after_bytes) (int32 view of the multipliers)."""
     torch = _torch()
     opt = lambda t, w: _dev_ptr(t, w) if t is not None else None  # noqa: E731
     with torch.cuda.device(page_crcs.device):
         check(lib().cc_scan_epilogue_dev(_dev_ptr(page_crcs, "page_crcs"), _dev_ptr(meta_crcs, "meta_crcs"),
                                          n_chunks, pages_per_chunk, page_bytes, pages_per_slice,
                                          _dev_ptr(slice_out, "slice_out"), opt(file_out, "file_out"),
-                                         opt(after_bytes, "after_bytes"), opt(group, "group"), opt(digest, "digest"),
+                                         opt(after_mult, "after_mult"), opt(group, "group"), opt(digest, "digest"),
                                          _stream_handle(stream)), "cc_scan_epilogue_dev")
     return slice_out
 

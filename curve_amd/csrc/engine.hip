@@ -63,6 +63,7 @@ struct DevCtx {
     void* image = nullptr;
     std::mutex submit;  // serialises *_host calls on this device
     Staging st;
+    std::unordered_map<uint64_t, void*> epi_tables;  // epilogue product tables per (page_bytes, q)
     std::unordered_map<void*, uint32_t> work_gen;    // partial-write generation per work buffer
     std::unordered_map<void*, uint64_t> work_pages;
 };
@@ -235,6 +236,8 @@ int cc_engine_fini(void) {
         if (hipSetDevice((int)d) == hipSuccess) {
             staging_free(c->st);
             if (c->image) hipFree(c->image);
+            for (auto& kv : c->epi_tables)
+                if (kv.second) hipFree(kv.second);
         }
         delete c;
         g_ctx[d] = nullptr;
@@ -325,7 +328,8 @@ int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, u
 namespace cc {
 namespace {
 // Geometry check + multipliers for the fused epilogue; false if unsupported.
-bool epilogue_geometry(uint32_t pages_per_chunk, uint32_t page_bytes, uint32_t pages_per_slice, EpilogueLaunch* a) {
+bool epilogue_geometry(DevCtx* c, uint32_t pages_per_chunk, uint32_t page_bytes, uint32_t pages_per_slice,
+                       EpilogueLaunch* a) {
     if (pages_per_chunk == 0 || pages_per_chunk % 256 || pages_per_slice == 0) return false;
     const uint32_t q = pages_per_chunk / 256;
     if (pages_per_slice % q) return false;
@@ -336,33 +340,60 @@ bool epilogue_geometry(uint32_t pages_per_chunk, uint32_t page_bytes, uint32_t p
     a->pages_per_chunk = pages_per_chunk;
     a->q = q;
     a->slice_shift = j;
-    a->m_page = xpow((uint64_t)page_bytes << 3);
-    for (int k = 0; k < 8; k++) a->m_level[k] = xpow(((uint64_t)page_bytes * q << k) << 3);
-    a->m_chunk = xpow((uint64_t)pages_per_chunk * page_bytes << 3);
+    // product tables of the 10 geometry constants, built on the host once per
+    // (page_bytes, q) and kept on the device
+    const uint64_t key = ((uint64_t)page_bytes << 32) | q;
+    std::lock_guard<std::mutex> lk(g_mu);
+    void*& dev = c->epi_tables[key];
+    if (!dev) {
+        uint32_t m[10];
+        m[0] = xpow((uint64_t)page_bytes << 3);
+        for (int k = 0; k < 8; k++) m[1 + k] = xpow(((uint64_t)page_bytes * q << k) << 3);
+        m[9] = xpow((uint64_t)pages_per_chunk * page_bytes << 3);
+        std::vector<uint32_t> h(10 * 1024);
+        for (int t = 0; t < 10; t++)
+            for (uint32_t k = 0; k < 4; k++)
+                for (uint32_t b = 0; b < 256; b++) h[t * 1024 + k * 256 + b] = mulmod(m[t], b << (8 * k));
+        if (hipMalloc(&dev, h.size() * 4) != hipSuccess) {
+            dev = nullptr;
+            return false;
+        }
+        if (hipMemcpy(dev, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
+    }
+    a->mtab = static_cast<const uint32_t*>(dev);
     return true;
 }
 }  // namespace
 }  // namespace cc
 
-int cc_scan_epilogue_dev(const uint32_t* d_page_crcs, const uint32_t* d_meta_crcs, uint64_t n_chunks,
-                         uint32_t pages_per_chunk, uint32_t page_bytes, uint32_t pages_per_slice,
-                         uint32_t* d_slice_crcs, uint32_t* d_file_crcs, const uint64_t* d_after_bytes,
-                         const uint32_t* d_group, uint32_t* d_digest, void* stream) {
-    if (n_chunks == 0) return CC_OK;
-    if (!d_page_crcs || !d_meta_crcs || !d_slice_crcs || page_bytes == 0) return CC_EINVAL;
-    const bool dig = d_after_bytes || d_group || d_digest;
-    if (dig && !(d_after_bytes && d_group && d_digest)) return CC_EINVAL;
-    EpilogueLaunch a = {};
-    if (!epilogue_geometry(pages_per_chunk, page_bytes, pages_per_slice, &a)) return CC_EINVAL;
+int cc_xpow8_dev(const uint64_t* d_nbytes, uint64_t n, uint32_t* d_out, void* stream) {
+    if (n == 0) return CC_OK;
+    if (!d_nbytes || !d_out) return CC_EINVAL;
     DevCtx* c = nullptr;
     int rc = get_ctx(&c);
     if (rc) return rc;
+    return map_err(launch_xpow8(d_nbytes, n, d_out, static_cast<hipStream_t>(stream)));
+}
+
+int cc_scan_epilogue_dev(const uint32_t* d_page_crcs, const uint32_t* d_meta_crcs, uint64_t n_chunks,
+                         uint32_t pages_per_chunk, uint32_t page_bytes, uint32_t pages_per_slice,
+                         uint32_t* d_slice_crcs, uint32_t* d_file_crcs, const uint32_t* d_after_mult,
+                         const uint32_t* d_group, uint32_t* d_digest, void* stream) {
+    if (n_chunks == 0) return CC_OK;
+    if (!d_page_crcs || !d_meta_crcs || !d_slice_crcs || page_bytes == 0) return CC_EINVAL;
+    const bool dig = d_after_mult || d_group || d_digest;
+    if (dig && !(d_after_mult && d_group && d_digest)) return CC_EINVAL;
+    DevCtx* c = nullptr;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    EpilogueLaunch a = {};
+    if (!epilogue_geometry(c, pages_per_chunk, page_bytes, pages_per_slice, &a)) return CC_EINVAL;
     a.page_crcs = d_page_crcs;
     a.meta_crcs = d_meta_crcs;
     a.n_chunks = n_chunks;
     a.slice_crcs = d_slice_crcs;
     a.file_crcs = d_file_crcs;
-    a.after_bytes = d_after_bytes;
+    a.after_mult = d_after_mult;
     a.group = d_group;
     a.digest = d_digest;
     return map_err(launch_epilogue(a, static_cast<hipStream_t>(stream)));
@@ -562,7 +593,7 @@ int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_b
     const uint32_t m_chunk = xpow((uint64_t)chunk_bytes << 3);
     EpilogueLaunch epi = {};
     const bool use_epi = chunk_bytes % page_bytes == 0 &&
-                         epilogue_geometry((uint32_t)pages_per_chunk, page_bytes, slice_bytes / page_bytes, &epi);
+                         epilogue_geometry(c, (uint32_t)pages_per_chunk, page_bytes, slice_bytes / page_bytes, &epi);
 
     const bool pinned0 = is_pinned(chunks[0].data) && is_pinned(chunks[0].meta);
     uint64_t pend_first[2] = {0, 0}, pend_n[2] = {0, 0};

@@ -92,16 +92,15 @@ struct EpilogueLaunch {
     uint32_t pages_per_chunk;   // 256 * q
     uint32_t q;                 // pages per thread
     uint32_t slice_shift;       // log2(threads per slice)
-    uint32_t m_page;            // x^(8 * page_bytes)
-    uint32_t m_level[8];        // x^(8 * page_bytes * q * 2^k)
-    uint32_t m_chunk;           // x^(8 * chunk_bytes)
+    const uint32_t* mtab;       // product tables [10][4][256]: 0 = x^(8 page), 1..8 = level k-1, 9 = chunk
     uint32_t* slice_crcs;       // [n_chunks * 256 >> slice_shift]
     uint32_t* file_crcs;        // [n_chunks] (may be null)
-    const uint64_t* after_bytes;  // digest inputs (all three null = no digest)
+    const uint32_t* after_mult; // digest inputs x^(8 * after_bytes) (all three null = no digest)
     const uint32_t* group;
     uint32_t* digest;
 };
 hipError_t launch_epilogue(const EpilogueLaunch& a, hipStream_t s);
+hipError_t launch_xpow8(const uint64_t* nbytes, uint64_t n, uint32_t* out, hipStream_t s);
 
 hipError_t launch_combine(const uint32_t* a, const uint32_t* b, uint32_t m_len_b, uint64_t n, uint32_t* out,
                           hipStream_t s);

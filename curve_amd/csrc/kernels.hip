@@ -447,51 +447,63 @@ __global__ __launch_bounds__(256) void fold_kernel_wave(const uint32_t* __restri
 // data CRC -> file CRC = combine(metapage CRC, data CRC, chunk_bytes) -> digest
 // contribution atomicXor'ed into its copyset.
 // ---------------------------------------------------------------------------
+// multiply by a constant through its 4 x 256 product table (global, L1-resident)
+__device__ __forceinline__ uint32_t mul_tab(const uint32_t* __restrict__ t, uint32_t s) {
+    return __builtin_amdgcn_bitop3_b32(
+        __builtin_amdgcn_bitop3_b32(t[s & 255u], t[256 + ((s >> 8) & 255u)], t[512 + ((s >> 16) & 255u)], 0x96),
+        t[768 + (s >> 24)], 0u, 0x96);
+}
+
 __global__ __launch_bounds__(256) void epilogue_kernel(EpilogueLaunch a) {
-    __shared__ uint32_t mt[4][256];
+    __shared__ uint32_t mt[1024];  // x^(8 page_bytes) product table (Horner), copied once per block
     __shared__ uint32_t part[4];
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    for (uint32_t i = t; i < 1024; i += 256) mt[i >> 8][i & 255] = mulmod_dev(a.m_page, (i & 255u) << (8 * (i >> 8)));
+    for (uint32_t i = t; i < 1024; i += 256) mt[i] = a.mtab[i];
     __syncthreads();
     const uint32_t slices = 256u >> a.slice_shift;
+    const uint32_t* lvl = a.mtab + 1024;           // level k table at lvl + 1024 k
+    const uint32_t* chk = a.mtab + 9 * 1024;
     for (uint64_t c = blockIdx.x; c < a.n_chunks; c += gridDim.x) {
         const uint32_t* p = a.page_crcs + c * a.pages_per_chunk + (uint64_t)t * a.q;
         uint32_t s = p[0];
         for (uint32_t i = 1; i < a.q; i++) {
-            const uint32_t u = __builtin_amdgcn_bitop3_b32(mt[0][s & 255u], mt[1][(s >> 8) & 255u],
-                                                           mt[2][(s >> 16) & 255u], 0x96);
-            s = __builtin_amdgcn_bitop3_b32(u, mt[3][s >> 24], p[i], 0x96);
+            const uint32_t u = __builtin_amdgcn_bitop3_b32(mt[s & 255u], mt[256 + ((s >> 8) & 255u)],
+                                                           mt[512 + ((s >> 16) & 255u)], 0x96);
+            s = __builtin_amdgcn_bitop3_b32(u, mt[768 + (s >> 24)], p[i], 0x96);
         }
         if (a.slice_shift == 0) a.slice_crcs[c * 256 + t] = s;  // one thread per slice
         // levels 0..5 inside the wave
 #pragma unroll
         for (uint32_t k = 0; k < 6; k++) {
             const uint32_t other = __shfl_down(s, 1u << k, 64);
-            if ((lane & ((2u << k) - 1u)) == 0) s = mulmod_dev(a.m_level[k], s) ^ other;
+            if ((lane & ((2u << k) - 1u)) == 0) s = mul_tab(lvl + 1024 * k, s) ^ other;
             if (k + 1 == a.slice_shift && (t & ((2u << k) - 1u)) == 0) a.slice_crcs[c * slices + (t >> a.slice_shift)] = s;
         }
         // levels 6..7 across the 4 waves
         if (lane == 0) part[wv] = s;
         __syncthreads();
         if (t == 0) {
-            uint32_t w0 = mulmod_dev(a.m_level[6], part[0]) ^ part[1];
-            uint32_t w1 = mulmod_dev(a.m_level[6], part[2]) ^ part[3];
+            const uint32_t w0 = mul_tab(lvl + 6 * 1024, part[0]) ^ part[1];
+            const uint32_t w1 = mul_tab(lvl + 6 * 1024, part[2]) ^ part[3];
             if (a.slice_shift == 7) {
                 a.slice_crcs[c * 2] = w0;
                 a.slice_crcs[c * 2 + 1] = w1;
             }
-            const uint32_t data = mulmod_dev(a.m_level[7], w0) ^ w1;
+            const uint32_t data = mul_tab(lvl + 7 * 1024, w0) ^ w1;
             if (a.slice_shift == 8) a.slice_crcs[c] = data;
-            const uint32_t file = mulmod_dev(a.m_chunk, a.meta_crcs[c]) ^ data;
+            const uint32_t file = mul_tab(chk, a.meta_crcs[c]) ^ data;
             if (a.file_crcs) a.file_crcs[c] = file;
-            part[0] = file;
+            if (a.digest) atomicXor(a.digest + a.group[c], mulmod_dev(a.after_mult[c], file));
         }
         __syncthreads();
-        if (a.digest && wv == 0) {  // digest contribution: x^(8*after) as a wave product
-            const uint32_t m = xpow_wave(a.after_bytes[c] << 3, lane);
-            if (lane == 0) atomicXor(a.digest + a.group[c], mulmod_dev(m, part[0]));
-        }
-        __syncthreads();
+    }
+}
+
+__global__ void xpow8_kernel(const uint64_t* __restrict__ nbytes, uint64_t n, uint32_t* __restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += (uint64_t)gridDim.x * 4) {
+        const uint32_t m = xpow_wave(nbytes[i] << 3, lane);
+        if (lane == 0) out[i] = m;
     }
 }
 
@@ -712,6 +724,14 @@ hipError_t launch_epilogue(const EpilogueLaunch& a, hipStream_t s) {
     if (a.n_chunks == 0) return hipSuccess;
     const uint64_t blocks = a.n_chunks < 8192 ? a.n_chunks : 8192;
     hipLaunchKernelGGL(epilogue_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_xpow8(const uint64_t* nbytes, uint64_t n, uint32_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    uint64_t blocks = (n + 3) / 4;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(xpow8_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, nbytes, n, out);
     return hipGetLastError();
 }
 

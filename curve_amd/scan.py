@@ -121,9 +121,10 @@ class DevicePool:
         C.page_crc(self.meta, self.meta_size, out=self.meta_crcs[: self.n], stream=stream)
         per_slice = self.scan_size // self.page_bytes
         if self.epilogue_ok():
+            mult = C.xpow8(after_bytes, stream=stream) if digest is not None else None
             C.scan_epilogue(self.page_crcs, self.meta_crcs[: self.n], self.n, self.chunk_size // self.page_bytes,
                             self.page_bytes, per_slice, self.slice_crcs, self.file_crcs,
-                            after_bytes, group, digest, stream=stream)
+                            mult, group, digest, stream=stream)
             return self.slice_crcs
         C.fold(self.page_crcs, per_slice, self.page_bytes, out=self.slice_crcs, stream=stream)
         C.fold(self.slice_crcs, self.chunk_size // self.scan_size, self.scan_size, out=self.data_crcs, stream=stream)

@@ -113,17 +113,24 @@ typedef struct cc_range {
 int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, uint32_t* d_out,
                       void* stream);
 
+/* d_out[i] = x^(8 * d_nbytes[i]) mod P: the multiplier that shifts a CRC by
+ * d_nbytes[i] bytes (precompute once per static pool layout for the epilogue's
+ * digest). */
+int cc_xpow8_dev(const uint64_t* d_nbytes, uint64_t n, uint32_t* d_out, void* stream);
+
 /* Fused scan epilogue for whole chunks, ONE launch (replaces fold + fold +
  * combine + digest): from the page CRCs of n_chunks chunks (pages_per_chunk
  * each, contiguous) and their metapage CRCs produce
  *   d_slice_crcs[c*S + k]  S = pages_per_chunk / pages_per_slice   (ScanMap.crc)
  *   d_file_crcs[c]         CRC of metapage || data  (NULL = skip)
- *   d_digest[d_group[c]] ^= shift(file CRC, d_after_bytes[c])      (all three NULL = skip)
- * Geometry: pages_per_chunk = 256*q; pages_per_slice = q * 2^j, j in [0, 8].
- * (16 MiB chunks, 4 KiB pages, 4 MiB slices: q = 16, j = 6.)  CC_EINVAL otherwise. */
+ *   d_digest[d_group[c]] ^= file CRC * d_after_mult[c]             (all three NULL = skip)
+ * with d_after_mult[c] = x^(8 * bytes after file c in its copyset's sorted-name
+ * chain) from cc_xpow8_dev.  Geometry: pages_per_chunk = 256*q; pages_per_slice
+ * = q * 2^j, j in [0, 8] (16 MiB chunks, 4 KiB pages, 4 MiB slices: q = 16,
+ * j = 6); CC_EINVAL otherwise. */
 int cc_scan_epilogue_dev(const uint32_t* d_page_crcs, const uint32_t* d_meta_crcs, uint64_t n_chunks,
                          uint32_t pages_per_chunk, uint32_t page_bytes, uint32_t pages_per_slice,
-                         uint32_t* d_slice_crcs, uint32_t* d_file_crcs, const uint64_t* d_after_bytes,
+                         uint32_t* d_slice_crcs, uint32_t* d_file_crcs, const uint32_t* d_after_mult,
                          const uint32_t* d_group, uint32_t* d_digest, void* stream);
 
 /* Linear-domain digest contributions (per-copyset digest):

@@ -461,8 +461,10 @@ def test_scan_epilogue_geometries(dev, oracle, ppc, pps):
     after = rng.integers(0, 1 << 36, n, dtype=np.int64)
     grp = rng.integers(0, 3, n).astype(np.int32)
     dig = torch.zeros(3, dtype=torch.int32, device=dev)
+    mult = C.xpow8(to_dev(after, dev))
+    assert [int(x) for x in u32(mult)] == [C.shift(0x80000000, int(a)) for a in after]  # x^(8a) * 1
     C.scan_epilogue(to_dev(pages.view(np.int32), dev), to_dev(metas.view(np.int32), dev), n, ppc, pb, pps,
-                    sl, fc, to_dev(after, dev), to_dev(grp, dev), dig)
+                    sl, fc, mult, to_dev(grp, dev), dig)
     want_sl, want_fc, want_dig = [], [], [0, 0, 0]
     for c in range(n):
         pc = pages[c * ppc:(c + 1) * ppc]
