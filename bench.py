@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--updates", type=int, default=65536, help="config-3 updates per batch")
     p.add_argument("--update-batches", type=int, default=5)
     p.add_argument("--stream-chunks", type=int, default=10000, help="config-4 stream leg (0 = skip)")
+    p.add_argument("--file-chunks", type=int, default=128, help="datastore read-path leg (0 = skip)")
     p.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/traffic_*.json)")
     return p.parse_args()
 
@@ -135,6 +136,39 @@ def stream_leg(args):
     return {"chunks": n, "GiBps_e2e": round(n * (C.CHUNK_SIZE + C.META_PAGE_SIZE) / GiB / el, 2),
             "seconds": round(el, 3), "with_digest_seconds": round(el_all, 3), "copysets": lay.n_groups,
             "scan_maps": int(sc.size + mc.size), "source": "pinned host pool of 64 chunk files, re-referenced"}
+
+
+def files_leg(args):
+    """The datastore read path: `--file-chunks` real chunk files (metapage ||
+    16 MiB data) in a temp directory (page-cache / tmpfs resident, as a hot
+    copyset would be), read AND scanned by the engine itself (cc_scan_files:
+    native pread by io threads into pinned staging, overlapped with H2D +
+    kernels).  Reports whole-file GiB/s per io-thread count."""
+    import shutil
+    import tempfile
+    from curve_amd import crc as C
+    n = args.file_chunks
+    d = tempfile.mkdtemp(prefix="cc_files_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        rng = np.random.default_rng(3)
+        body = rng.integers(0, 256, C.CHUNK_SIZE + C.META_PAGE_SIZE, dtype=np.uint8)
+        paths = []
+        for i in range(n):
+            body[:8] = np.frombuffer(np.uint64(i).tobytes(), dtype=np.uint8)
+            p = os.path.join(d, f"chunk_{i}")
+            body.tofile(p)
+            paths.append(p)
+        out = {"files": n, "file_bytes": C.CHUNK_SIZE + C.META_PAGE_SIZE, "source": "tmp dir, page-cache resident"}
+        C.scan_files(paths[:4])  # warm
+        for t in (4, 8, 16):
+            t0 = time.perf_counter()
+            st, _, _, _ = C.scan_files(paths, io_threads=t)
+            el = time.perf_counter() - t0
+            assert (st == 0).all()
+            out[f"GiBps_io{t}"] = round(n * (C.CHUNK_SIZE + C.META_PAGE_SIZE) / GiB / el, 2)
+        return out
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def partial_write_leg(pool, args):
@@ -327,6 +361,8 @@ def main():
         out["e2e_pinned_GiBps"] = e2e_leg(args, dev)
         if args.stream_chunks:
             out["stream"] = stream_leg(args)
+        if args.file_chunks:
+            out["files"] = files_leg(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -29,6 +29,10 @@ class CcOpts(ctypes.Structure):
     _fields_ = [("page_bytes", _u32), ("slice_bytes", _u32), ("staging_bytes", _u64)]
 
 
+class CcFileResult(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("meta_crc", _u32), ("file_crc", _u32), ("reserved", _u32)]
+
+
 class CcChunkSrc(ctypes.Structure):
     _fields_ = [("meta", _vp), ("data", _vp)]
 
@@ -59,6 +63,8 @@ SIGNATURES = {
     "cc_plan_updates": (_int, [_vp, _u64, _vp, _vp, _u32, ctypes.POINTER(_u32)]),
     "cc_update_work_bytes": (_u64, [_u64, _u64, _u32, _u32]),
     "cc_apply_updates_dev": (_int, [_vp, _u64, _u32, _vp, _vp, _u64, _vp, _u32, _u32, _vp, _vp, _u64, _vp]),
+    "cc_scan_files": (_int, [ctypes.POINTER(ctypes.c_char_p), _u64, _u32, _u32, _u32, _u32, _u32, _vp,
+                              ctypes.POINTER(CcFileResult)]),
     "cc_scan_host": (_int, [ctypes.POINTER(CcChunkSrc), _u64, _u32, _u32, _u32, _u32, _vp, _vp, _vp]),
 }
 

@@ -108,15 +108,14 @@ def read_into(path: str, dst) -> int:
 
 
 def copyset_hash_dir(data_dir: str, chunk_size: int = C.CHUNK_SIZE, meta_size: int = C.META_PAGE_SIZE,
-                     batch: int = 64) -> str:
+                     io_threads: int = 8) -> str:
     """CopysetNode::GetHash over a real data directory: list, std::sort the
     names, chain CRC32 over whole files.  Chunk files (meta || data of the
-    configured geometry) are hashed by the GPU engine in batches read into
-    pinned buffers; any other file is hashed on the CPU primitive.  The chain
-    is assembled with crc32c_combine in sorted-name order -- identical to
-    `crc = CRC32(crc, file)` over the same order."""
-    import numpy as np
-    import torch
+    configured geometry) are read AND hashed by the engine (cc_scan_files:
+    native pread into pinned staging overlapped with the GPU scan); any other
+    file -- or one the engine could not read -- is hashed on the CPU primitive.
+    The chain is assembled with crc32c_combine in sorted-name order, identical
+    to `crc = CRC32(crc, file)` over the same order."""
     names = sorted(os.listdir(data_dir))  # std::sort on std::string: bytewise
     if not names:
         return "0"
@@ -125,15 +124,10 @@ def copyset_hash_dir(data_dir: str, chunk_size: int = C.CHUNK_SIZE, meta_size: i
     file_crc: Dict[int, int] = {}
     chunk_idx = [i for i, s in enumerate(sizes) if s == fsize]
     if chunk_idx:
-        pinned = torch.empty((min(batch, len(chunk_idx)), fsize), dtype=torch.uint8, pin_memory=True).numpy()
-        for b0 in range(0, len(chunk_idx), batch):
-            part = chunk_idx[b0:b0 + batch]
-            for k, i in enumerate(part):
-                if read_into(os.path.join(data_dir, names[i]), pinned[k]) != fsize:
-                    raise IOError(f"short read on {names[i]}")
-            _, _, fc = C.scan_host([(pinned[k, :meta_size], pinned[k, meta_size:]) for k in range(len(part))],
-                                   chunk_size, meta_size, C.PAGE_SIZE, min(C.SCAN_SIZE, chunk_size))
-            for k, i in enumerate(part):
+        st, _, _, fc = C.scan_files([os.path.join(data_dir, names[i]) for i in chunk_idx], chunk_size, meta_size,
+                                    C.PAGE_SIZE, min(C.SCAN_SIZE, chunk_size), io_threads)
+        for k, i in enumerate(chunk_idx):
+            if st[k] == 0:
                 file_crc[i] = int(fc[k])
     crc = 0
     for i, n in enumerate(names):

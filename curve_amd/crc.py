@@ -9,6 +9,7 @@ on any failure -- there is no CPU fallback for them.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Union
 
 from . import _lib
@@ -403,6 +404,24 @@ def apply_updates(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int 
     if stream is not None:  # temp descriptor buffer must outlive the kernels on `stream`
         d_upd.record_stream(stream)
     return nb
+
+
+def scan_files(paths, chunk_bytes: int = CHUNK_SIZE, meta_bytes: int = META_PAGE_SIZE,
+               page_bytes: int = PAGE_SIZE, slice_bytes: int = SCAN_SIZE, io_threads: int = 8):
+    """cc_scan_files: native pread + scan of chunk files.
+    Returns (status[n] int32, meta_crcs[n], slice_crcs[n, S], file_crcs[n]) numpy."""
+    import numpy as np
+    n = len(paths)
+    arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+    res = (_lib.CcFileResult * max(n, 1))()
+    S = chunk_bytes // slice_bytes
+    sc = np.zeros((n, S), dtype=np.uint32)
+    check(lib().cc_scan_files(arr, n, chunk_bytes, meta_bytes, page_bytes, slice_bytes, io_threads,
+                              ctypes.c_void_p(sc.ctypes.data), res), "cc_scan_files")
+    st = np.array([res[i].status for i in range(n)], dtype=np.int32)
+    mc = np.array([res[i].meta_crc for i in range(n)], dtype=np.uint32)
+    fc = np.array([res[i].file_crc for i in range(n)], dtype=np.uint32)
+    return st, mc, sc, fc
 
 
 def as_u32(t) -> "list[int]":

@@ -9,7 +9,14 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <errno.h>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -663,6 +670,194 @@ int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_b
         geometry_for(c, nb, &a);
         if ((e = launch_page_crc(a, s)) != hipSuccess) return map_err(e);
         if (use_epi) {  // one fused launch: slices + file CRCs
+            EpilogueLaunch ea = epi;
+            ea.page_crcs = d_pages;
+            ea.meta_crcs = d_meta;
+            ea.n_chunks = nb;
+            ea.slice_crcs = d_slices;
+            ea.file_crcs = d_file;
+            if ((e = launch_epilogue(ea, s)) != hipSuccess) return map_err(e);
+        } else {
+            f1.crcs = d_pages;
+            f1.n_groups = nb * slices;
+            f1.out = d_slices;
+            if ((e = launch_fold(f1, s)) != hipSuccess) return map_err(e);
+            f2.crcs = d_slices;
+            f2.n_groups = nb;
+            f2.out = d_data;
+            if ((e = launch_fold(f2, s)) != hipSuccess) return map_err(e);
+            if ((e = launch_combine(d_meta, d_data, m_chunk, nb, d_file, s)) != hipSuccess) return map_err(e);
+        }
+        if ((e = hipMemcpyAsync(st.hcrc[slot], res, nb * (2 + (uint64_t)slices) * 4, hipMemcpyDeviceToHost, s)) !=
+            hipSuccess)
+            return map_err(e);
+        if ((e = hipEventRecord(st.done[slot], s)) != hipSuccess) return map_err(e);
+        pend_first[slot] = first;
+        pend_n[slot] = nb;
+        slot ^= 1;
+    }
+    if ((rc = drain(slot))) return rc;
+    if ((rc = drain(slot ^ 1))) return rc;
+    return CC_OK;
+}
+
+// Native file scan.  Batch layout in a staging slot = the pageable layout of
+// cc_scan_host (data of the batch's files back to back, then their metapages),
+// so one H2D per batch; files that fail get status != 0 and their slots are
+// zero-filled (their CRCs are discarded).
+namespace {
+constexpr uint64_t kReadPiece = 2ull << 20;  // io work item
+
+int read_full(int fd, void* dst, size_t n, off_t off) {
+    char* p = static_cast<char*>(dst);
+    size_t got = 0;
+    while (got < n) {
+        const ssize_t r = pread(fd, p + got, n - got, off + (off_t)got);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return -errno;
+        }
+        if (r == 0) return -EIO;  // short file
+        got += (size_t)r;
+    }
+    return 0;
+}
+}  // namespace
+
+int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_bytes, uint32_t meta_bytes,
+                  uint32_t page_bytes, uint32_t slice_bytes, uint32_t io_threads, uint32_t* h_slice_crcs,
+                  cc_file_result* h_results) {
+    if (n_files == 0) return CC_OK;
+    if (!paths || !h_results || !page_size_ok(page_bytes) || !page_size_ok(meta_bytes) || chunk_bytes == 0 ||
+        slice_bytes == 0 || chunk_bytes % slice_bytes || slice_bytes % page_bytes)
+        return CC_EINVAL;
+    DevCtx* c = nullptr;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->submit);
+    if ((rc = staging_init(c))) return rc;
+    Staging& st = c->st;
+    const uint64_t per_file = (uint64_t)chunk_bytes + meta_bytes;
+    const uint64_t batch = st.bytes / per_file;
+    if (batch == 0) return CC_EINVAL;
+    const uint32_t slices = chunk_bytes / slice_bytes;
+    const uint64_t pages_per_chunk = chunk_bytes / page_bytes;
+    if (batch * pages_per_chunk + batch * (3 + (uint64_t)slices) > st.bytes / 256) return CC_EINVAL;
+    EpilogueLaunch epi = {};
+    const bool use_epi = epilogue_geometry(c, (uint32_t)pages_per_chunk, page_bytes, slice_bytes / page_bytes, &epi);
+    FoldLaunch f1 = {}, f2 = {};
+    f1.per_group = slice_bytes / page_bytes;
+    f1.m_unit = xpow((uint64_t)page_bytes << 3);
+    for (int t = 0; t < 6; t++) f1.m_tree[t] = xpow(((uint64_t)page_bytes * (f1.per_group / 64) << t) << 3);
+    f2.per_group = slices;
+    f2.m_unit = xpow((uint64_t)slice_bytes << 3);
+    for (int t = 0; t < 6; t++) f2.m_tree[t] = xpow(((uint64_t)slice_bytes * (slices / 64) << t) << 3);
+    const uint32_t m_chunk = xpow((uint64_t)chunk_bytes << 3);
+    const uint32_t threads = io_threads ? (io_threads > 64 ? 64 : io_threads) : 8;
+
+    uint64_t pend_first[2] = {0, 0}, pend_n[2] = {0, 0};
+    auto drain = [&](int s) -> int {
+        if (!pend_n[s]) return CC_OK;
+        hipError_t ee = hipEventSynchronize(st.done[s]);
+        if (ee != hipSuccess) return map_err(ee);
+        const uint32_t* r = st.hcrc[s];
+        const uint64_t nb = pend_n[s], f = pend_first[s];
+        for (uint64_t i = 0; i < nb; i++) {
+            cc_file_result& fr = h_results[f + i];
+            if (fr.status != 0) continue;
+            fr.meta_crc = r[i];
+            fr.file_crc = r[nb + nb * slices + i];
+            if (h_slice_crcs) memcpy(h_slice_crcs + (f + i) * slices, r + nb + i * slices, slices * 4);
+        }
+        pend_n[s] = 0;
+        return CC_OK;
+    };
+    int slot = 0;
+    hipError_t e;
+    for (uint64_t first = 0; first < n_files; first += batch) {
+        const uint64_t nb = (n_files - first < batch) ? n_files - first : batch;
+        if ((rc = drain(slot))) return rc;  // slot's previous batch done: its staging is free
+        unsigned char* hstage = static_cast<unsigned char*>(st.host[slot]);
+        // open + size check serially (cheap), then the reads as ~2 MiB pieces
+        // pulled by the io threads (a batch holds only a few 16 MiB files)
+        std::vector<int> fds(nb, -1);
+        std::vector<std::atomic<int>> fst(nb);
+        for (uint64_t i = 0; i < nb; i++) {
+            const char* p = paths[first + i];
+            int status = 0;
+            const int fd = p ? open(p, O_RDONLY | O_CLOEXEC) : -1;
+            if (fd < 0) status = p ? -errno : CC_EINVAL;
+            struct stat sb;
+            if (!status && fstat(fd, &sb) != 0) status = -errno;
+            if (!status && (uint64_t)sb.st_size != per_file) status = CC_EINVAL;
+            fds[i] = fd;
+            fst[i].store(status);
+        }
+        const uint64_t pieces = (chunk_bytes + kReadPiece - 1) / kReadPiece;
+        const uint64_t items = nb * (1 + pieces);
+        std::atomic<uint64_t> next{0};
+        auto reader = [&]() {
+            for (uint64_t it; (it = next.fetch_add(1)) < items;) {
+                const uint64_t i = it / (1 + pieces), k = it % (1 + pieces);
+                if (fst[i].load(std::memory_order_relaxed)) continue;
+                int r;
+                if (k == 0) {
+                    r = read_full(fds[i], hstage + nb * (uint64_t)chunk_bytes + i * (uint64_t)meta_bytes, meta_bytes, 0);
+                } else {
+                    const uint64_t off = (k - 1) * kReadPiece;
+                    const uint64_t len = chunk_bytes - off < kReadPiece ? chunk_bytes - off : kReadPiece;
+                    r = read_full(fds[i], hstage + i * (uint64_t)chunk_bytes + off, len, (off_t)(meta_bytes + off));
+                }
+                if (r) {
+                    int zero = 0;
+                    fst[i].compare_exchange_strong(zero, r);
+                }
+            }
+        };
+        {
+            std::vector<std::thread> pool;
+            const uint32_t nt = (uint32_t)(items < threads ? items : threads);
+            for (uint32_t t = 1; t < nt; t++) pool.emplace_back(reader);
+            reader();
+            for (auto& th : pool) th.join();
+        }
+        for (uint64_t i = 0; i < nb; i++) {
+            if (fds[i] >= 0) close(fds[i]);
+            cc_file_result& fr = h_results[first + i];
+            fr = cc_file_result{fst[i].load(), 0, 0, 0};
+            if (fr.status) {  // keep the batch well-defined; its CRCs are discarded
+                memset(hstage + i * (uint64_t)chunk_bytes, 0, chunk_bytes);
+                memset(hstage + nb * (uint64_t)chunk_bytes + i * (uint64_t)meta_bytes, 0, meta_bytes);
+            }
+        }
+        hipStream_t s = st.stream[slot];
+        unsigned char* ddata = static_cast<unsigned char*>(st.dev[slot]);
+        unsigned char* dmeta = ddata + nb * (uint64_t)chunk_bytes;
+        if ((e = hipMemcpyAsync(ddata, hstage, nb * per_file, hipMemcpyHostToDevice, s)) != hipSuccess)
+            return map_err(e);
+        uint32_t* res = st.dcrc[slot];
+        uint32_t* d_pages = res + nb * (3 + (uint64_t)slices);
+        uint32_t* d_meta = res;
+        uint32_t* d_slices = res + nb;
+        uint32_t* d_file = res + nb + nb * slices;
+        uint32_t* d_data = d_file + nb;
+        PageLaunch a = {};
+        a.pages = reinterpret_cast<const uint32_t*>(ddata);
+        a.n_pages = nb * pages_per_chunk;
+        a.words_per_lane = page_bytes / kWaveBytes;
+        a.image = c->image;
+        a.kconst = kconst_for(page_bytes);
+        a.out = d_pages;
+        geometry_for(c, a.n_pages, &a);
+        if ((e = launch_page_crc(a, s)) != hipSuccess) return map_err(e);
+        a.pages = reinterpret_cast<const uint32_t*>(dmeta);
+        a.n_pages = nb;
+        a.words_per_lane = meta_bytes / kWaveBytes;
+        a.kconst = kconst_for(meta_bytes);
+        a.out = d_meta;
+        geometry_for(c, nb, &a);
+        if ((e = launch_page_crc(a, s)) != hipSuccess) return map_err(e);
+        if (use_epi) {
             EpilogueLaunch ea = epi;
             ea.page_crcs = d_pages;
             ea.meta_crcs = d_meta;

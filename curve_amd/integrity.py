@@ -116,27 +116,15 @@ class IntegrityJob:  # proto/integrity.proto:32-39
 
 
 def hash_chunk_files(paths: List[str], chunk_size: int, meta_size: int, page_bytes: int):
-    """Page CRCs of the DATA part of each chunk file (file = metapage || data),
-    read into one pinned buffer and hashed on the GPU.  -> list of uint32 arrays."""
-    import torch
-    n = len(paths)
-    host = torch.empty((n, chunk_size), dtype=torch.uint8, pin_memory=True)
-    hv = host.numpy()
-    for k, p in enumerate(paths):
-        fd = os.open(p, os.O_RDONLY)
-        try:  # data part only: CSChunkFile::Read reads at offset + metaPageSize
-            got = 0
-            while got < chunk_size:
-                r = os.preadv(fd, [memoryview(hv[k])[got:]], meta_size + got)
-                if r <= 0:
-                    raise IOError(f"short read: {p}")
-                got += r
-        finally:
-            os.close(fd)
-    dev = torch.device("cuda", torch.cuda.current_device())
-    pcs = C.page_crc(host.to(dev, non_blocking=True), page_bytes).view(n, -1)
-    out = pcs.cpu().numpy().view(np.uint32)
-    return [out[k].copy() for k in range(n)]
+    """Page CRCs of the DATA part of each chunk file (file = metapage || data;
+    CSChunkFile::Read reads at offset + metaPageSize).  The engine preads the
+    files itself (cc_scan_files, slice = one page, so the per-slice CRCs ARE the
+    page CRCs).  -> list of uint32 arrays; IOError for an unreadable file."""
+    st, _, pcs, _ = C.scan_files(paths, chunk_size, meta_size, page_bytes, page_bytes)
+    bad = np.flatnonzero(st)
+    if bad.size:
+        raise IOError(f"cannot read {paths[bad[0]]}: status {int(st[bad[0]])}")
+    return [pcs[k].copy() for k in range(len(paths))]
 
 
 class IntegrityService:

@@ -226,6 +226,26 @@ int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_b
                  uint32_t meta_bytes, uint32_t page_bytes, uint32_t slice_bytes,
                  uint32_t* h_meta_crcs, uint32_t* h_slice_crcs, uint32_t* h_file_crcs);
 
+/* Per-file outcome of cc_scan_files. */
+typedef struct cc_file_result {
+    int32_t status;    /* 0 ok; -errno from open/fstat/pread; CC_EINVAL: size != meta+chunk */
+    uint32_t meta_crc; /* CRC32(metapage) */
+    uint32_t file_crc; /* CRC32(metapage || data) == CopysetNode::GetHash's per-file chain step */
+    uint32_t reserved;
+} cc_file_result;
+
+/* Native datastore read path + scan: open/fstat/pread every chunk FILE (the
+ * whole-file read of CopysetNode::GetHash, copyset_node.cpp:942-962, and the
+ * metapage + data reads of the scan ops, chunkserver_chunkfile.cpp:497-548)
+ * with `io_threads` reader threads into pinned staging, overlapping the reads
+ * of batch i+1 with the H2D copy + kernels of batch i.  Outputs as
+ * cc_scan_host (slice CRCs may be NULL); a file whose size is not
+ * meta_bytes + chunk_bytes, or that cannot be read, gets a non-zero status and
+ * no CRCs (the caller chains such files on the CPU).  Blocking, thread-safe. */
+int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_bytes, uint32_t meta_bytes,
+                  uint32_t page_bytes, uint32_t slice_bytes, uint32_t io_threads, uint32_t* h_slice_crcs,
+                  cc_file_result* h_results);
+
 /* ------------------------------------------------------------------------
  * Diagnostics (new; no reference counterpart)
  * ------------------------------------------------------------------------ */

@@ -50,6 +50,9 @@ def test_no_gpu_fails_loudly_here():
     assert L.cc_page_crc_dev(buf, 1, 4096, out, None) == _lib.CC_ENODEV
     assert L.cc_page_crc_host(buf, 1, 4096, out) == _lib.CC_ENODEV
     assert L.cc_engine_init(None) == _lib.CC_ENODEV
+    paths = (ctypes.c_char_p * 1)(b"/nonexistent")
+    res = (_lib.CcFileResult * 1)()
+    assert L.cc_scan_files(paths, 1, 1 << 20, 4096, 4096, 4096, 2, None, res) == _lib.CC_ENODEV
 
 
 def test_argument_checks_need_no_gpu():
@@ -62,4 +65,7 @@ def test_argument_checks_need_no_gpu():
     assert L.cc_page_crc_dev(None, 1, 4096, out, None) == _lib.CC_EINVAL
     assert L.cc_page_crc_dev(buf, 0, 4096, out, None) == _lib.CC_OK       # empty batch is a no-op
     assert L.cc_lds_image(None, 0) == _lib.CC_EINVAL
+    res = (_lib.CcFileResult * 1)()
+    assert L.cc_scan_files(None, 1, 1 << 20, 4096, 4096, 4096, 2, None, res) == _lib.CC_EINVAL
+    assert L.cc_scan_files(None, 0, 1 << 20, 4096, 4096, 4096, 2, None, res) == _lib.CC_OK
     assert L.cc_strerror(_lib.CC_ENODEV) == b"no usable HIP device"

@@ -225,6 +225,31 @@ def test_large_pool_properties(dev, oracle):
     assert int(cnt[0]) == 0
 
 
+def test_beyond_4gib_offsets(dev, oracle):
+    """Maximum-size addressing: a 4.25 GiB buffer (byte offsets past 2^32):
+    every page CRC, verify finding a page past 4 GiB, and ranges at offsets
+    > 2^32 -- no 32-bit index truncation anywhere on the path."""
+    from curve_amd import crc as C
+    nbytes = (4 << 30) + (256 << 20)
+    d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    d.random_(0, 256)
+    pc = C.page_crc(d, 4096)
+    host = d.cpu().numpy()
+    assert (u32(pc) == oracle.page_crcs(host, 4096, threads=16)).all()
+    bad_page = (nbytes >> 12) - 7  # lives above 4 GiB
+    d[bad_page * 4096 + 11] ^= 0x40
+    cnt = C.page_verify(d, pc, 4096)
+    torch.cuda.synchronize()
+    assert int(cnt[0]) == 1 and int(cnt[1]) == bad_page
+    d[bad_page * 4096 + 11] ^= 0x40
+    offs = [(4 << 30) + 1, (4 << 30) - 100, nbytes - 5000, 123]
+    lens = [70001, 4096, 5000, (1 << 20)]
+    got = u32(C.crc_ranges(d, offs, lens))
+    assert [int(x) for x in got] == [oracle.crc32c(host[o:o + l].tobytes()) for o, l in zip(offs, lens)]
+    del d, pc
+    torch.cuda.empty_cache()
+
+
 def test_streams_and_multithread_callers(dev, oracle):
     """Device calls on side streams from several Python threads (apply-thread shape)."""
     import threading
@@ -358,7 +383,7 @@ def test_wal_segment_replay_verify(dev, oracle):
 
 def test_copyset_dir_real_chunk_files(dev, oracle, tmp_path):
     """CopysetNode::GetHash over a directory of real chunk files (+ a stray file):
-    pread into pinned buffers -> cc_scan_host -> combine in std::sort order ==
+    native pread into pinned staging (cc_scan_files) -> combine in std::sort order ==
     the oracle's chained CRC over the same files."""
     from curve_amd import chunkfile as CF
     rng = np.random.default_rng(12)
@@ -371,7 +396,45 @@ def test_copyset_dir_real_chunk_files(dev, oracle, tmp_path):
         files[CF.chunk_file_name(cid)] = meta + data
     (tmp_path / "chunk_5_snap_1").write_bytes(b"x" * 5000)  # other geometry -> CPU
     files["chunk_5_snap_1"] = b"x" * 5000
-    assert CF.copyset_hash_dir(str(tmp_path), chunk_size=chunk, batch=4) == oracle.copyset_hash(files)
+    assert CF.copyset_hash_dir(str(tmp_path), chunk_size=chunk) == oracle.copyset_hash(files)
+
+
+def test_scan_files(dev, oracle, tmp_path):
+    """cc_scan_files: the engine opens/preads real chunk files itself (3 staging
+    batches of 1 MiB chunks), metapage / slice / file CRCs == oracle; a missing
+    file and a wrong-size file get a status and leave the others intact."""
+    from curve_amd import crc as C
+    chunk, meta_b, sl = 1 << 20, 4096, 256 << 10
+    rng = np.random.default_rng(77)
+    paths, raws = [], []
+    for i in range(260):
+        raw = rng.integers(0, 256, meta_b + chunk, dtype=np.uint8).tobytes()
+        p = tmp_path / f"chunk_{i}"
+        p.write_bytes(raw)
+        paths.append(str(p))
+        raws.append(raw)
+    (tmp_path / "short").write_bytes(b"y" * 1000)
+    paths.insert(5, str(tmp_path / "missing"))
+    raws.insert(5, None)
+    paths.insert(140, str(tmp_path / "short"))
+    raws.insert(140, None)
+    st, mc, sc, fc = C.scan_files(paths, chunk, meta_b, 4096, sl, io_threads=4)
+    assert st[5] == -2 and st[140] == -22  # -ENOENT, CC_EINVAL (size)
+    for i, raw in enumerate(raws):
+        if raw is None:
+            continue
+        assert st[i] == 0
+        m, d = raw[:meta_b], raw[meta_b:]
+        want = oracle.scan_slices(m, d, sl)
+        assert int(mc[i]) == want[0][2]
+        assert [int(x) for x in sc[i]] == [w[2] for w in want[1:]]
+        assert int(fc[i]) == oracle.crc32c(raw)
+    # slice == page: the per-slice CRCs are the page CRCs of the data part
+    st, _, pc, _ = C.scan_files(paths[:3], chunk, meta_b, 4096, 4096)
+    assert (st == 0).all()
+    for i in range(3):
+        d = np.frombuffer(raws[i][meta_b:], dtype=np.uint8)
+        assert (pc[i] == oracle.page_crcs(d, 4096)).all()
 
 
 def test_integrity_job_sidecars(dev, oracle, tmp_path):
