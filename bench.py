@@ -87,7 +87,19 @@ def cpu_baseline(pool, args, rank):
                   f"single-stream crc32q as butil builds it)",
         "value_16_threads": round(v16, 3),
         "parity_vs_device": parity,
+        "cpu_model": cpu_model(),
     }
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def e2e_leg(args, dev):
@@ -322,6 +334,19 @@ def main():
     verify_ms = ve0.elapsed_time(ve1)
     bad = int(cnt[0].item())
 
+    # measured read ceiling of THIS device: pure nt read of the same 16 GiB, same stream
+    sink = torch.empty(2 * 1024 * 16, dtype=torch.int32, device=dev)
+    probe_ms = []
+    for r in range(6):
+        pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        pe0.record(stream)
+        C.hbm_read_probe(pool.data, sink)
+        pe1.record(stream)
+        torch.cuda.synchronize()
+        if r:
+            probe_ms.append(pe0.elapsed_time(pe1))
+    probe_gbs = pool.data.numel() / (float(np.mean(probe_ms)) * 1e-3) / 1e9
+
     n_pages = n * chunk // pb
     per_step_bytes = n * chunk * world
     value = per_step_bytes * args.steps / GiB / el
@@ -350,7 +375,9 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "page_crc_kernel<16,0>", "kernel_ms_avg": round(kern_ms, 4),
                      "alg_bytes_per_launch": n_pages * ALG_BYTES_PER_PAGE,
-                     "traffic_source": traffic_src},
+                     "traffic_source": traffic_src,
+                     "read_probe_GBps": round(probe_gbs, 1),
+                     "frac_of_read_probe": round(achieved / probe_gbs, 4)},
         "verify": {"GiBps": round(n * chunk / GiB / (verify_ms * 1e-3), 2), "bad_pages": bad},
     }
     if rank == 0 and world == 1 and args.updates:

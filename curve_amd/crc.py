@@ -152,6 +152,35 @@ def page_verify(pages, expected, page_bytes: int = PAGE_SIZE, stream=None, count
     return counters
 
 
+def hbm_read_probe(buf, sink, stream=None):
+    """cc_hbm_read_probe_dev (diagnostic): pure nt read of `buf`; sink must hold
+    2*CUs*16 int32."""
+    check(lib().cc_hbm_read_probe_dev(_dev_ptr(buf, "buf"), _nbytes(buf), _dev_ptr(sink, "sink"),
+                                      _stream_handle(stream)), "cc_hbm_read_probe_dev")
+
+
+def page_verify_list(pages, expected, page_bytes: int = PAGE_SIZE, max_bad: int = 4096, stream=None):
+    """cc_page_verify_list_dev: -> (counters [bad_count, first_bad] int64 device
+    tensor, bad page indices int64 device tensor of max_bad slots; the first
+    min(bad_count, max_bad) are valid, unordered).  No host sync."""
+    torch = _torch()
+    nb = _nbytes(pages)
+    if nb % page_bytes:
+        raise CurveCrcError(_lib.CC_EINVAL, "pages size is not a multiple of page_bytes")
+    n = nb // page_bytes
+    if expected.numel() < n or expected.element_size() != 4:
+        raise CurveCrcError(_lib.CC_EINVAL, "expected must hold one 32-bit CRC per page")
+    counters = torch.tensor([0, -1], dtype=torch.int64, device=pages.device)
+    bad = torch.full((max(1, max_bad),), -1, dtype=torch.int64, device=pages.device)
+    base = counters.data_ptr()
+    with torch.cuda.device(pages.device):
+        check(lib().cc_page_verify_list_dev(_dev_ptr(pages, "pages"), n, page_bytes, _dev_ptr(expected, "expected"),
+                                            ctypes.c_void_p(base), ctypes.c_void_p(base + 8),
+                                            ctypes.c_void_p(bad.data_ptr()), max_bad,
+                                            _stream_handle(stream)), "cc_page_verify_list_dev")
+    return counters, bad
+
+
 def fold(crcs, per_group: int, unit_bytes: int, out=None, stream=None):
     """Group fold on device: out[g] = CRC of the concatenation of `per_group`
     consecutive units (each `unit_bytes`) given their CRCs."""

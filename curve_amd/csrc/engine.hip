@@ -213,6 +213,15 @@ int cc_lds_image(void* out, size_t bytes) {
     return CC_OK;
 }
 
+int cc_hbm_read_probe_dev(const void* d_buf, uint64_t bytes, uint32_t* d_sink, void* stream) {
+    if (!d_buf || !d_sink || bytes % 4096 || ((uintptr_t)d_buf & 15u)) return CC_EINVAL;
+    if (bytes == 0) return CC_OK;
+    DevCtx* c = nullptr;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    return map_err(launch_read_probe(d_buf, bytes, d_sink, 2 * c->cus, static_cast<hipStream_t>(stream)));
+}
+
 int cc_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -271,11 +280,13 @@ int cc_page_crc_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes, 
     return map_err(launch_page_crc(a, static_cast<hipStream_t>(stream)));
 }
 
-int cc_page_verify_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes, const uint32_t* d_expected,
-                       uint64_t* d_bad_count, uint64_t* d_first_bad, void* stream) {
+int cc_page_verify_list_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes, const uint32_t* d_expected,
+                            uint64_t* d_bad_count, uint64_t* d_first_bad, uint64_t* d_bad_pages,
+                            uint64_t max_bad_pages, void* stream) {
     if (!page_size_ok(page_bytes)) return CC_EINVAL;
     if (n_pages == 0) return CC_OK;
     if (!d_pages || !d_expected || !d_bad_count || !d_first_bad || ((uintptr_t)d_pages & 3u)) return CC_EINVAL;
+    if (max_bad_pages && !d_bad_pages) return CC_EINVAL;
     DevCtx* c = nullptr;
     int rc = get_ctx(&c);
     if (rc) return rc;
@@ -286,10 +297,18 @@ int cc_page_verify_dev(const void* d_pages, uint64_t n_pages, uint32_t page_byte
     a.image = c->image;
     a.kconst = kconst_for(page_bytes);
     a.expected = d_expected;
-    a.bad_count = reinterpret_cast<unsigned long long*>(d_bad_count);
-    a.first_bad = reinterpret_cast<unsigned long long*>(d_first_bad);
+    a.sink.bad_count = reinterpret_cast<unsigned long long*>(d_bad_count);
+    a.sink.first_bad = reinterpret_cast<unsigned long long*>(d_first_bad);
+    a.sink.list = max_bad_pages ? reinterpret_cast<unsigned long long*>(d_bad_pages) : nullptr;
+    a.sink.max_list = max_bad_pages;
     geometry_for(c, n_pages, &a);
     return map_err(launch_page_verify(a, static_cast<hipStream_t>(stream)));
+}
+
+int cc_page_verify_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes, const uint32_t* d_expected,
+                       uint64_t* d_bad_count, uint64_t* d_first_bad, void* stream) {
+    return cc_page_verify_list_dev(d_pages, n_pages, page_bytes, d_expected, d_bad_count, d_first_bad, nullptr, 0,
+                                   stream);
 }
 
 int cc_fold_dev(const uint32_t* d_crcs, uint64_t n_groups, uint32_t per_group, uint64_t unit_bytes,

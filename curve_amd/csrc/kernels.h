@@ -20,6 +20,15 @@ constexpr int kBlockThreads = 64 * kWavesPerBlock;
 // Host builder of the 160 KiB LDS image (engine.hip).
 void build_lds_image(uint32_t* image /* kLdsBytes/4 words */);
 
+// Verify outputs: mismatch count, first bad page, and (optional) the list of
+// bad page indices (unordered, at most max_list kept; count may exceed it).
+struct VerifySink {
+    unsigned long long* bad_count;
+    unsigned long long* first_bad;
+    unsigned long long* list;
+    unsigned long long max_list;
+};
+
 struct PageLaunch {
     const uint32_t* pages;
     uint64_t n_pages;
@@ -28,13 +37,13 @@ struct PageLaunch {
     uint32_t kconst;          // V-domain correction for this page size
     uint32_t* out;            // compute: CRC per page
     const uint32_t* expected; // verify: expected CRC per page
-    unsigned long long* bad_count;
-    unsigned long long* first_bad;
+    VerifySink sink;          // verify only
     int blocks;
     uint32_t tile_shift;      // 2^tile_shift consecutive pages per wave tile (0..6)
 };
 
 hipError_t launch_page_crc(const PageLaunch& a, hipStream_t s);
+hipError_t launch_read_probe(const void* buf, uint64_t bytes, uint32_t* sink, int blocks, hipStream_t s);
 hipError_t launch_page_verify(const PageLaunch& a, hipStream_t s);
 
 struct FoldLaunch {

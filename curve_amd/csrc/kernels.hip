@@ -133,16 +133,15 @@ __device__ __forceinline__ uint32_t chain(const uint32_t* tab, const uint32_t (&
 
 template <int MODE>
 __device__ __forceinline__ void emit(uint32_t crc, uint64_t page, uint32_t lane, uint32_t* __restrict__ out,
-                                     const uint32_t* __restrict__ expected,
-                                     unsigned long long* __restrict__ bad_count,
-                                     unsigned long long* __restrict__ first_bad) {
+                                     const uint32_t* __restrict__ expected, const VerifySink& vs) {
     if (MODE == 0) {
         if (lane == 0) out[page] = crc;
     } else {
         const uint32_t want = expected[page];
         if (crc != want && lane == 0) {
-            atomicAdd(bad_count, 1ull);
-            atomicMin(first_bad, (unsigned long long)page);
+            const unsigned long long at = atomicAdd(vs.bad_count, 1ull);
+            atomicMin(vs.first_bad, (unsigned long long)page);
+            if (vs.list && at < vs.max_list) vs.list[at] = page;
         }
     }
 }
@@ -155,8 +154,7 @@ __device__ __forceinline__ void emit(uint32_t crc, uint64_t page, uint32_t lane,
 template <int MODE>
 __device__ __forceinline__ void flush_tile(uint32_t acc, uint64_t tile_first, uint32_t cnt, uint32_t lane,
                                            uint32_t* __restrict__ out, const uint32_t* __restrict__ expected,
-                                           unsigned long long* __restrict__ bad_count,
-                                           unsigned long long* __restrict__ first_bad) {
+                                           const VerifySink& vs) {
     if (MODE == 0) {
 #if CC_STORE == 1  // diagnostic: no store (wrong output), keeps acc live
         asm volatile("" ::"v"(acc));
@@ -170,9 +168,17 @@ __device__ __forceinline__ void flush_tile(uint32_t acc, uint64_t tile_first, ui
     } else {
         const uint32_t want = lane < cnt ? __builtin_nontemporal_load(expected + tile_first + lane) : acc;
         const uint64_t bad = __ballot(want != acc);
-        if (bad && lane == 0) {
-            atomicAdd(bad_count, (unsigned long long)__popcll(bad));
-            atomicMin(first_bad, (unsigned long long)(tile_first + __ffsll((long long)bad) - 1));
+        if (bad) {  // rare: wave-uniform branch
+            unsigned long long at = 0;
+            if (lane == 0) {
+                at = atomicAdd(vs.bad_count, (unsigned long long)__popcll(bad));
+                atomicMin(vs.first_bad, (unsigned long long)(tile_first + __ffsll((long long)bad) - 1));
+            }
+            if (vs.list) {  // every bad page of the tile gets a slot after `at`
+                at = (unsigned long long)__shfl((long long)at, 0);
+                const unsigned long long idx = at + (unsigned long long)__popcll(bad & ((1ull << lane) - 1ull));
+                if (((bad >> lane) & 1ull) && idx < vs.max_list) vs.list[idx] = tile_first + lane;
+            }
         }
     }
 }
@@ -242,8 +248,8 @@ __device__ __forceinline__ void chains(const uint32_t* tab, const uint32_t (&w)[
 template <int M, int MODE>
 __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
     const uint32_t* __restrict__ pages, uint64_t n_pages, const uint4* __restrict__ image,
-    uint32_t kconst, uint32_t* __restrict__ out, const uint32_t* __restrict__ expected,
-    unsigned long long* __restrict__ bad_count, unsigned long long* __restrict__ first_bad, uint32_t tshift) {
+    uint32_t kconst, uint32_t* __restrict__ out, const uint32_t* __restrict__ expected, VerifySink vs,
+    uint32_t tshift) {
     __shared__ uint32_t tab[kLdsBytes / 4];
     fill_lds(tab, image);
 
@@ -290,7 +296,7 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
                     const uint32_t slot = (uint32_t)(kq & W.tmask);
                     acc = lane == slot ? crc : acc;
                     if (slot == W.tmask || pn >= n_pages)
-                        flush_tile<MODE>(acc, pc - slot, slot + 1u, lane, out, expected, bad_count, first_bad);
+                        flush_tile<MODE>(acc, pc - slot, slot + 1u, lane, out, expected, vs);
                 }
             }
         }
@@ -302,8 +308,7 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
 template <int MODE>
 __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
     const uint32_t* __restrict__ pages, uint64_t n_pages, uint32_t M, const uint4* __restrict__ image,
-    uint32_t kconst, uint32_t* __restrict__ out, const uint32_t* __restrict__ expected,
-    unsigned long long* __restrict__ bad_count, unsigned long long* __restrict__ first_bad) {
+    uint32_t kconst, uint32_t* __restrict__ out, const uint32_t* __restrict__ expected, VerifySink vs) {
     __shared__ uint32_t tab[kLdsBytes / 4];
     fill_lds(tab, image);
 
@@ -317,7 +322,7 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
         const uint32_t* p = pages + page * (64ull * M) + lane;
         uint32_t s = p[0];
         for (uint32_t j = 1; j < M; j++) s = apply_g_xor(tab, s, p[64ull * j], c0, c1);
-        emit<MODE>(wave_xor(apply_fin(tab, s, cf)) ^ kconst, page, lane, out, expected, bad_count, first_bad);
+        emit<MODE>(wave_xor(apply_fin(tab, s, cf)) ^ kconst, page, lane, out, expected, vs);
     }
 }
 
@@ -640,7 +645,7 @@ hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
 #define CC_CASE(MM)                                                                                     \
     case MM:                                                                                            \
         hipLaunchKernelGGL((page_crc_kernel<MM, MODE>), grid, block, 0, s, a.pages, a.n_pages, img,    \
-                           a.kconst, a.out, a.expected, a.bad_count, a.first_bad, a.tile_shift);        \
+                           a.kconst, a.out, a.expected, a.sink, a.tile_shift);                         \
         break;
     switch (a.words_per_lane) {
         CC_CASE(1)
@@ -651,7 +656,7 @@ hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
         CC_CASE(32)
         default:
             hipLaunchKernelGGL((page_crc_kernel_dyn<MODE>), grid, block, 0, s, a.pages, a.n_pages,
-                               a.words_per_lane, img, a.kconst, a.out, a.expected, a.bad_count, a.first_bad);
+                               a.words_per_lane, img, a.kconst, a.out, a.expected, a.sink);
     }
 #undef CC_CASE
     return hipGetLastError();
@@ -660,6 +665,34 @@ hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_page_crc(const PageLaunch& a, hipStream_t s) { return launch_page<0>(a, s); }
+
+// Read-only probe (diagnostic): dwordx4 nt loads, 4 in flight per lane, the
+// fastest pure-read shape found by scripts/hbm_probe.hip.
+__global__ __launch_bounds__(1024) void read_probe_kernel(const uint4* __restrict__ p, uint64_t n16,
+                                                          uint32_t* __restrict__ sink) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint64_t lane = threadIdx.x & 63u;
+    const uint64_t wave = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
+    const uint64_t waves = (uint64_t)gridDim.x * 16;
+    constexpr uint64_t kStep = 64 * 4;  // 16-byte elements per wave per step
+    uint32_t acc = 0;
+    const u32x4* q = reinterpret_cast<const u32x4*>(p);
+    for (uint64_t b = wave * kStep; b + kStep <= n16; b += waves * kStep) {
+        u32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = __builtin_nontemporal_load(q + b + u * 64 + lane);
+#pragma unroll
+        for (int u = 0; u < 4; u++) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    acc ^= __shfl_xor(acc, 32);
+    if (lane == 0) sink[wave] = acc;
+}
+
+hipError_t launch_read_probe(const void* buf, uint64_t bytes, uint32_t* sink, int blocks, hipStream_t s) {
+    hipLaunchKernelGGL(read_probe_kernel, dim3(blocks), dim3(1024), 0, s, static_cast<const uint4*>(buf), bytes / 16,
+                       sink);
+    return hipGetLastError();
+}
 hipError_t launch_page_verify(const PageLaunch& a, hipStream_t s) { return launch_page<1>(a, s); }
 
 hipError_t launch_fold(const FoldLaunch& a, hipStream_t s) {

@@ -136,6 +136,18 @@ class DevicePool:
     def verify(self, expected_page_crcs, stream=None):
         return C.page_verify(self.data, expected_page_crcs, self.page_bytes, stream=stream)
 
+    def bad_pages(self, expected_page_crcs, max_bad: int = 4096, stream=None):
+        """Every mismatching page as sorted (chunk index, page in chunk) pairs
+        -- what a scan reports per chunk (FailedScanMap granularity is the
+        chunk; the page pinpoints the repair).  Raises if more than max_bad."""
+        cnt, lst = C.page_verify_list(self.data, expected_page_crcs, self.page_bytes, max_bad, stream=stream)
+        n = int(cnt[0])
+        if n > max_bad:
+            raise C.CurveCrcError(-74, f"{n} bad pages > max_bad={max_bad}")
+        ppc = self.chunk_size // self.page_bytes
+        pages = sorted(int(p) for p in lst[:n].cpu().tolist())
+        return [(p // ppc, p % ppc) for p in pages]
+
     # -- reference surfaces built on the device results ----------------------
     def scan_maps(self, logical_pool_id: int, copyset_id: int, first_index: int = 0) -> List[ScanMap]:
         """ScanMaps as ScanChunkRequest::OnApply builds them (op_request.cpp:795-803),

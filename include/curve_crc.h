@@ -92,6 +92,16 @@ int cc_page_verify_dev(const void* d_pages, uint64_t n_pages, uint32_t page_byte
                        const uint32_t* d_expected, uint64_t* d_bad_count,
                        uint64_t* d_first_bad, void* stream);
 
+/* cc_page_verify_dev plus the indices of the mismatching pages: the first
+ * min(count, max_bad_pages) of them land in d_bad_pages[*d_bad_count_before ..]
+ * in no particular order (the caller sorts).  Lets a scan report every bad page
+ * (SURVEY §8d C1 "verify must flag exactly those") without a second pass.
+ * d_bad_pages may be NULL only when max_bad_pages == 0. */
+int cc_page_verify_list_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes,
+                            const uint32_t* d_expected, uint64_t* d_bad_count,
+                            uint64_t* d_first_bad, uint64_t* d_bad_pages,
+                            uint64_t max_bad_pages, void* stream);
+
 /* Group fold: d_out[g] = CRC of the concatenation of units g*per_group ..
  * g*per_group+per_group-1, each unit_bytes long, from their CRCs d_crcs.
  * E.g. 1024 page CRCs -> one 4 MiB ScanMap.crc (proto/scan.proto:28). */
@@ -253,6 +263,13 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
  * + per-lane final maps, DESIGN.md "LDS image") so host tests can replay the
  * kernel's arithmetic on the CPU.  Needs no GPU. */
 int cc_lds_image(void* out, size_t bytes);
+
+/* Read-only HBM probe: streams `bytes` (multiple of 4096, 16-byte aligned) from
+ * d_buf with the page kernel's access style (nontemporal, grid-stride,
+ * persistent blocks) and XOR-reduces into d_sink[0 .. 2*CUs*16).  What a pure
+ * read achieves on THIS device: bench.py reports the page kernel against it
+ * beside the 8 TB/s spec.  Enqueue only. */
+int cc_hbm_read_probe_dev(const void* d_buf, uint64_t bytes, uint32_t* d_sink, void* stream);
 
 #ifdef __cplusplus
 }

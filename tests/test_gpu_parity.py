@@ -110,6 +110,41 @@ def test_verify_clean_and_corrupt(dev, oracle):
     assert int(cnt[0]) == len(bad) and int(cnt[1]) == min(bad)
 
 
+def test_verify_flags_exactly_the_corrupted_pages(dev, oracle):
+    """SURVEY §8d C1 sub-case: one corrupted byte in a known page per chunk (plus
+    a cluster inside one 64-page tile); the listed bad pages are exactly those."""
+    from curve_amd import crc as C
+    from curve_amd.scan import DevicePool
+    rng = np.random.default_rng(99)
+    n, chunk = 64, 1 << 20
+    data = torch.empty((n, chunk), dtype=torch.uint8, device=dev)
+    data.random_(0, 256)
+    meta = torch.zeros((n, 4096), dtype=torch.uint8, device=dev)
+    pool = DevicePool(data, meta, list(range(n)), scan_size=chunk)
+    good = pool.hash_pages().clone()
+    want = set()
+    for c in range(n):
+        p = int(rng.integers(0, 256))
+        data[c, p * 4096 + int(rng.integers(0, 4096))] ^= 0x01
+        want.add((c, p))
+    for p in (3, 4, 5, 9, 63):  # several bad pages in one tile of chunk 7
+        data[7, p * 4096] ^= 0x80
+        want.add((7, p))
+    assert pool.bad_pages(good) == sorted(want)
+    cnt, lst = C.page_verify_list(data, good, 4096, max_bad=10)  # truncated list, full count
+    assert int(cnt[0]) == len(want)
+    got = [int(x) for x in lst.cpu()]
+    assert len(set(got)) == 10 and all((g // 256, g % 256) in want for g in got)
+    # the dynamic-M kernel (768-byte pages) through the same sink
+    buf = rng.integers(0, 256, 768 * 1000, dtype=np.uint8)
+    exp = to_dev(oracle.page_crcs(buf, 768).view(np.int32), dev)
+    buf[768 * 17 + 5] ^= 1
+    buf[768 * 999] ^= 1
+    cnt, lst = C.page_verify_list(to_dev(buf, dev), exp, 768, max_bad=8)
+    assert int(cnt[0]) == 2 and int(cnt[1]) == 17
+    assert sorted(int(x) for x in lst[:2].cpu()) == [17, 999]
+
+
 @pytest.mark.parametrize("per_group,unit", [(1024, 4096), (64, 4096), (128, 512), (4, 4 << 20), (3, 4096), (100, 4096), (1, 4096)])
 def test_fold(dev, oracle, per_group, unit):
     from curve_amd import crc as C
