@@ -78,6 +78,16 @@ def cpu_baseline(pool, args, rank):
             if el >= budget:
                 break
         res[threads] = (nbytes / GiB / el, nbytes, el)
+    # libcurvecrc's own CPU primitive (3-way crc32q, the drop-in for
+    # curve::common::CRC32 on small/CPU-side buffers), whole chunks per call
+    from curve_amd import _lib
+    L = _lib.lib()
+    nbytes, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 2.0:
+        for k in range(sample_chunks):
+            L.crc32c_value(host[k].ctypes.data, host[k].nbytes)
+            nbytes += host[k].nbytes
+    prim = nbytes / GiB / (time.perf_counter() - t0)
     v1, nb1, el1 = res[1]
     v16, _, _ = res[16]
     return {
@@ -88,6 +98,7 @@ def cpu_baseline(pool, args, rank):
         "value_16_threads": round(v16, 3),
         "parity_vs_device": parity,
         "cpu_model": cpu_model(),
+        "lib_cpu_primitive_GiBps": round(prim, 3),
     }
 
 

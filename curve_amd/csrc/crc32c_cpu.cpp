@@ -19,21 +19,28 @@
 
 namespace {
 
-constexpr size_t kBlock = 4096;  // bytes per stream per round in the 3-way loop
+// Block sizes of the 3-way loop, largest first: a round hashes 3 blocks of b
+// bytes as three independent crc32q chains and merges them with two
+// shift-by-constant table lookups.  The small sizes make 4 KiB pages (3 x 1360
+// + 16) and other short buffers 3-way too.
+constexpr size_t kBlocks[] = {4096, 2048, 1360, 1024, 680, 512, 336, 256, 168};
+constexpr int kNumBlocks = sizeof(kBlocks) / sizeof(kBlocks[0]);
 
-// x^(8*kBlock) and x^(16*kBlock) as 4x256 byte tables: shift-by-constant
+// x^(8b) and x^(16b) as 4x256 byte tables per block size: shift-by-constant
 // in 4 lookups instead of a 32-step multiply.
 struct ShiftTables {
-    uint32_t t1[4][256];  // register * x^(8*kBlock)
-    uint32_t t2[4][256];  // register * x^(16*kBlock)
+    uint32_t t1[kNumBlocks][4][256];  // register * x^(8*b)
+    uint32_t t2[kNumBlocks][4][256];  // register * x^(16*b)
     ShiftTables() {
-        const uint32_t m1 = cc::xpow(8ull * kBlock);
-        const uint32_t m2 = cc::xpow(16ull * kBlock);
-        for (int k = 0; k < 4; k++)
-            for (uint32_t b = 0; b < 256; b++) {
-                t1[k][b] = cc::mulmod(m1, b << (8 * k));
-                t2[k][b] = cc::mulmod(m2, b << (8 * k));
-            }
+        for (int i = 0; i < kNumBlocks; i++) {
+            const uint32_t m1 = cc::xpow(8ull * kBlocks[i]);
+            const uint32_t m2 = cc::xpow(16ull * kBlocks[i]);
+            for (int k = 0; k < 4; k++)
+                for (uint32_t v = 0; v < 256; v++) {
+                    t1[i][k][v] = cc::mulmod(m1, v << (8 * k));
+                    t2[i][k][v] = cc::mulmod(m2, v << (8 * k));
+                }
+        }
     }
     static inline uint32_t apply(const uint32_t (&t)[4][256], uint32_t r) {
         return t[0][r & 0xFF] ^ t[1][(r >> 8) & 0xFF] ^ t[2][(r >> 16) & 0xFF] ^ t[3][r >> 24];
@@ -50,6 +57,18 @@ inline uint64_t load64(const unsigned char* p) {
     return v;
 }
 
+template <size_t B>
+inline uint64_t three_way(uint64_t l, const unsigned char* p, const ShiftTables& st, int i) {
+    uint64_t a = l, b = 0, c = 0;
+    for (size_t k = 0; k < B; k += 8) {
+        a = _mm_crc32_u64(a, load64(p + k));
+        b = _mm_crc32_u64(b, load64(p + B + k));
+        c = _mm_crc32_u64(c, load64(p + 2 * B + k));
+    }
+    return ShiftTables::apply(st.t2[i], static_cast<uint32_t>(a)) ^
+           ShiftTables::apply(st.t1[i], static_cast<uint32_t>(b)) ^ static_cast<uint32_t>(c);
+}
+
 // raw register update over [p, p+n)
 uint32_t raw_update(uint32_t reg, const unsigned char* p, size_t n) {
     uint64_t l = reg;
@@ -57,22 +76,24 @@ uint32_t raw_update(uint32_t reg, const unsigned char* p, size_t n) {
         l = _mm_crc32_u8(static_cast<uint32_t>(l), *p++);
         n--;
     }
-    if (n >= 3 * kBlock) {
+    if (n >= 3 * kBlocks[kNumBlocks - 1]) {
         const ShiftTables& st = shift_tables();
-        while (n >= 3 * kBlock) {
-            uint64_t a = l, b = 0, c = 0;
-            const unsigned char* pa = p;
-            const unsigned char* pb = p + kBlock;
-            const unsigned char* pc = p + 2 * kBlock;
-            for (size_t i = 0; i < kBlock; i += 8) {
-                a = _mm_crc32_u64(a, load64(pa + i));
-                b = _mm_crc32_u64(b, load64(pb + i));
-                c = _mm_crc32_u64(c, load64(pc + i));
+        int i = 0;
+        while (n >= 3 * kBlocks[kNumBlocks - 1]) {
+            while (3 * kBlocks[i] > n) i++;  // sizes only shrink as n does
+            switch (i) {  // compile-time trip counts
+                case 0: l = three_way<4096>(l, p, st, 0); break;
+                case 1: l = three_way<2048>(l, p, st, 1); break;
+                case 2: l = three_way<1360>(l, p, st, 2); break;
+                case 3: l = three_way<1024>(l, p, st, 3); break;
+                case 4: l = three_way<680>(l, p, st, 4); break;
+                case 5: l = three_way<512>(l, p, st, 5); break;
+                case 6: l = three_way<336>(l, p, st, 6); break;
+                case 7: l = three_way<256>(l, p, st, 7); break;
+                default: l = three_way<168>(l, p, st, 8); break;
             }
-            l = ShiftTables::apply(st.t2, static_cast<uint32_t>(a)) ^
-                ShiftTables::apply(st.t1, static_cast<uint32_t>(b)) ^ static_cast<uint32_t>(c);
-            p += 3 * kBlock;
-            n -= 3 * kBlock;
+            p += 3 * kBlocks[i];
+            n -= 3 * kBlocks[i];
         }
     }
     while (n >= 8) {

@@ -384,7 +384,11 @@ bool epilogue_geometry(DevCtx* c, uint32_t pages_per_chunk, uint32_t page_bytes,
             dev = nullptr;
             return false;
         }
-        if (hipMemcpy(dev, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
+        if (hipMemcpy(dev, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            hipFree(dev);  // never leave a half-initialised table in the cache
+            dev = nullptr;
+            return false;
+        }
     }
     a->mtab = static_cast<const uint32_t*>(dev);
     return true;

@@ -26,7 +26,8 @@ def test_reference_chains(golden):
     assert crc == 599727352
 
 
-@pytest.mark.parametrize("n", [0, 1, 7, 8, 15, 16, 63, 4095, 4096, 12287, 12288, 12289, 3 * 4096 * 5 + 13, 1 << 20])
+@pytest.mark.parametrize("n", [0, 1, 7, 8, 15, 16, 63, 503, 504, 768, 1008, 1536, 2040, 3072, 4080, 4095, 4096, 4104,
+                               6144, 8191, 12287, 12288, 12289, 3 * 4096 * 5 + 13, 1 << 20])
 def test_lengths_and_alignments(oracle, n):
     rng = np.random.default_rng(n)
     buf = rng.integers(0, 256, n + 16, dtype=np.uint8)
