@@ -71,10 +71,18 @@ def main():
     g["copyset_hash"] = {"files": COPYSET_FILES, "zero_file_bytes": 7680, "hash": "1355371765"}
     g["conf_epoch"] = {"logicPoolId": 123, "copysetId": 1345, "epoch": 0,
                        "magic": 0x6225929368674119, "crc": 599727352}
+    # GetChunkHash of a chunk whose first 4 KiB block was written with 'a'
+    # (test/chunkserver/chunk_service_test.cpp:505-523 write, :563-578 hash)
+    g["chunk_service_hash"] = {"data_byte": "a", "bytes": 4096, "hash": "650595490",
+                               "note": "= CRC32('a' x 4096), i.e. the DATA block; CSChunkFile::GetHash "
+                                       "preads the raw file (chunkserver_chunkfile.cpp:796, mock test "
+                                       "datastore_mock_unittest.cpp:4238 pins Read(fd, buf, 0, 4096)), "
+                                       "which at offset 0 returns the metapage -- see metapage_residue"}
     # verify the oracle reproduces them before deriving anything else
     assert O.copyset_hash(copyset_bytes()) == g["copyset_hash"]["hash"]
     assert O.conf_epoch_crc(123, 1345, 0) == 599727352
     assert O.crc32c(bytes(32)) == 0x8a9136aa
+    assert str(O.crc32c(b"a" * 4096)) == g["chunk_service_hash"]["hash"]
 
     # ---- derived vectors ----
     g["zero_page"] = {"bytes": 4096, "crc": O.crc32c(bytes(4096))}
@@ -91,6 +99,21 @@ def main():
     p512 = O.splitmix64_bytes(0x512, 64 * 512)
     g["seeded_pages_512"] = {"generator": "splitmix64", "seed": 0x512, "page_bytes": 512, "n_pages": 64,
                              "crcs": [int(c) for c in O.page_crcs(p512, 512)]}
+
+    # every zero-padded metapage of a given header length has the same CRC:
+    # encode appends CRC32(header) little-endian, so CRC32(header || crc) is
+    # the CRC-32C residue whatever the header bytes, and the zero padding to
+    # 4 KiB shifts it by an amount fixed by the header length (25 B non-clone)
+    res = {O.crc32c(metapage_v2(sn, csn)) for sn, csn in ((1, 0), (7, 3), (2**63, 5))}
+    assert len(res) == 1
+    hdr = struct.pack("<BQQQ", 1, 3, 1, 0)
+    residue = O.crc32c(hdr + struct.pack("<I", O.crc32c(hdr)))
+    clone_hdr = struct.pack("<BQQQ", 2, 9, 0, 13) + b"curvefs:/f@1x" + struct.pack("<I", 20) + bytes([0xA5, 0x0F, 0x03])
+    assert O.crc32c(clone_hdr + struct.pack("<I", O.crc32c(clone_hdr))) == residue
+    g["metapage_residue"] = {"page_bytes": 4096, "crc": res.pop(), "residue": residue,
+                             "note": "CRC32 of ANY encoded non-clone 4 KiB metapage (ScanMap.crc of the metapage "
+                                     "op; GetChunkHash(offset 0, 4096)); residue = CRC32(h || CRC32(h)_le) for "
+                                     "every header h"}
 
     # one synthetic 16 MiB chunk: slices, metapage, chunk hash, page CRCs
     meta, data = synthetic_chunk(0xC0FFEE)

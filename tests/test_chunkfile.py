@@ -31,6 +31,34 @@ def test_metapage_clone_and_errors(oracle):
     assert CF.ChunkFileMetaPage.decode(bad)[0] == CF.CSErrorCode.IncompatibleError
 
 
+def test_metapage_crc_is_the_residue_constant(oracle, golden):
+    """Every encoded non-clone 4 KiB metapage hashes to the same value (CRC-32C
+    residue property), so the metapage ScanMap.crc is 317729701 on every chunk;
+    a clone metapage's CRC depends only on its header length."""
+    g = golden["metapage_residue"]
+    for sn, csn, ver in ((1, 0, 2), (123, 45, 1), (2**64 - 1, 2**63, 2)):
+        page = CF.ChunkFileMetaPage(version=ver, sn=sn, correctedSn=csn).encode()
+        assert oracle.crc32c(page) == g["crc"]
+        hdr = page[:25]
+        assert oracle.crc32c(page[:29]) == g["residue"] == oracle.crc32c(hdr + struct.pack("<I", oracle.crc32c(hdr)))
+    a = CF.ChunkFileMetaPage(sn=1, location=b"x" * 10, bitmap_bits=16, bitmap=b"\x01\x02").encode()
+    b = CF.ChunkFileMetaPage(sn=9, location=b"y" * 10, bitmap_bits=16, bitmap=b"\xff\x00").encode()
+    assert oracle.crc32c(a) == oracle.crc32c(b) != g["crc"]
+
+
+def test_chunk_service_hash_vector(oracle, golden):
+    """chunk_service_test.cpp:563-578: hash of the 'a'-filled first block is
+    650595490 = CRC32 of the DATA block.  CSChunkFile::GetHash as written
+    preads the raw file, whose [0, 4096) is the metapage (-> 317729701); the
+    engine follows the code (DevicePool.chunk_hash takes raw file offsets), so
+    the reference test's value is reproduced at raw offset 4096."""
+    g = golden["chunk_service_hash"]
+    assert str(oracle.crc32c(b"a" * 4096)) == g["hash"]
+    raw = CF.ChunkFileMetaPage(sn=1).encode() + b"a" * 4096 + bytes(8192)
+    assert oracle.chunk_hash(raw, 4096, 4096) == g["hash"]
+    assert oracle.chunk_hash(raw, 0, 4096) == str(golden["metapage_residue"]["crc"])
+
+
 def test_compare_maps_semantics():
     # scan_manager_test.cpp CompareMapSuccessTest / CompareMapFailTest / MismatchedCRCTest shapes
     a = ScanMap(1, 1, 1, 5, 100, 0, 4 << 20)

@@ -434,6 +434,24 @@ def test_copyset_dir_real_chunk_files(dev, oracle, tmp_path):
     assert CF.copyset_hash_dir(str(tmp_path), chunk_size=chunk) == oracle.copyset_hash(files)
 
 
+def test_chunk_service_hash_on_device(dev, golden):
+    """GetChunkHash vectors on the device path: the 'a'-filled block of
+    chunk_service_test.cpp:563-578 at raw offset 4096 -> "650595490"; raw
+    [0, 4096) is the metapage -> the residue constant; ScanMap of the metapage
+    op carries the same constant."""
+    from curve_amd import chunkfile as CF
+    from curve_amd.scan import DevicePool
+    data = torch.zeros((2, 1 << 20), dtype=torch.uint8, device=dev)
+    data[:, :4096] = ord("a")
+    meta = torch.from_numpy(np.frombuffer(CF.ChunkFileMetaPage(sn=1).encode() * 2, dtype=np.uint8).reshape(2, -1).copy()).to(dev)
+    pool = DevicePool(data, meta, [1, 2], scan_size=256 << 10)
+    pool.scan()
+    assert pool.chunk_hash(0, 4096, 4096) == golden["chunk_service_hash"]["hash"]
+    assert pool.chunk_hash(1, 0, 4096) == str(golden["metapage_residue"]["crc"])
+    maps = pool.scan_maps(1, 1)
+    assert maps[0].crc == golden["metapage_residue"]["crc"] and maps[0].len == 4096
+
+
 def test_scan_files(dev, oracle, tmp_path):
     """cc_scan_files: the engine opens/preads real chunk files itself (3 staging
     batches of 1 MiB chunks), metapage / slice / file CRCs == oracle; a missing
