@@ -78,11 +78,19 @@ def main():
                                        "preads the raw file (chunkserver_chunkfile.cpp:796, mock test "
                                        "datastore_mock_unittest.cpp:4238 pins Read(fd, buf, 0, 4096)), "
                                        "which at offset 0 returns the metapage -- see metapage_residue"}
+    # GetCopysetStatus(queryhash) after 25 x 4 KiB writes of 'b' at offsets
+    # 4096*i to chunk 1 of a one-chunk copyset, 16 MiB chunks, 4 KiB metapage
+    # (test/chunkserver/chunkserver_snapshot_test.cpp:339-388; writes:
+    # test/integration/common/peer_cluster.cpp:459-495)
+    g["copyset_hash_one_chunk"] = {"chunk_bytes": 16 << 20, "meta_bytes": 4096, "fill": "b", "blocks": 25,
+                                   "block_bytes": 4096, "file": "chunk_1", "hash": "3049021227"}
     # verify the oracle reproduces them before deriving anything else
     assert O.copyset_hash(copyset_bytes()) == g["copyset_hash"]["hash"]
     assert O.conf_epoch_crc(123, 1345, 0) == 599727352
     assert O.crc32c(bytes(32)) == 0x8a9136aa
     assert str(O.crc32c(b"a" * 4096)) == g["chunk_service_hash"]["hash"]
+    one = metapage_v2() + b"b" * (25 * 4096) + bytes((16 << 20) - 25 * 4096)
+    assert O.copyset_hash({"chunk_1": one}) == g["copyset_hash_one_chunk"]["hash"]
 
     # ---- derived vectors ----
     g["zero_page"] = {"bytes": 4096, "crc": O.crc32c(bytes(4096))}

@@ -197,6 +197,29 @@ def test_copyset_digest_matches_reference_chain(dev, oracle, golden):
     assert str(parts[0] ^ parts[1]) == "1355371765"
 
 
+def test_copyset_hash_one_chunk_golden(dev, golden, tmp_path):
+    """chunkserver_snapshot_test.cpp:339-388 -> "3049021227", on the device
+    path twice: the resident pool's fused epilogue digest, and GetHash over a
+    real data directory (cc_scan_files preads chunk_1 itself)."""
+    from curve_amd import chunkfile as CF
+    from curve_amd import crc as C
+    from curve_amd.pool import digests_as_hash_strings
+    from curve_amd.scan import DevicePool
+    g = golden["copyset_hash_one_chunk"]
+    data = torch.zeros((1, g["chunk_bytes"]), dtype=torch.uint8, device=dev)
+    data[0, : g["blocks"] * g["block_bytes"]] = ord(g["fill"])
+    meta_np = np.frombuffer(CF.ChunkFileMetaPage(sn=1).encode(), dtype=np.uint8).reshape(1, -1).copy()
+    pool = DevicePool(data, to_dev(meta_np, dev), [1])
+    digest = torch.zeros(1, dtype=torch.int32, device=dev)
+    pool.scan(after_bytes=torch.zeros(1, dtype=torch.int64, device=dev),
+              group=torch.zeros(1, dtype=torch.int32, device=dev), digest=digest)
+    assert digests_as_hash_strings(digest) == [g["hash"]]
+    d = tmp_path / "data"
+    d.mkdir()
+    CF.write_chunk_file(str(d / g["file"]), meta_np.tobytes(), data[0].cpu().numpy().tobytes())
+    assert CF.copyset_hash_dir(str(d)) == g["hash"]
+
+
 def test_pool_digest_equals_chained_copyset_hash(dev, oracle):
     """A small pool of real chunk files (metapage + data): the device digest
     equals CopysetNode::GetHash's sorted-name chain computed by the oracle."""

@@ -42,6 +42,16 @@ def test_copyset_hash_golden(oracle, golden):
     assert oracle.copyset_hash(rev) == "1355371765"
 
 
+def test_copyset_hash_one_chunk_golden(oracle, golden):
+    # chunkserver_snapshot_test.cpp:339-388: one 16 MiB chunk file, 25 x 4 KiB of 'b'
+    g = golden["copyset_hash_one_chunk"]
+    from curve_amd.chunkfile import ChunkFileMetaPage
+    blocks = g["fill"].encode() * (g["blocks"] * g["block_bytes"])
+    for sn in (1, 2):  # metapage content does not matter (residue property)
+        raw = ChunkFileMetaPage(sn=sn).encode() + blocks + bytes(g["chunk_bytes"] - len(blocks))
+        assert oracle.copyset_hash({g["file"]: raw}) == g["hash"] == "3049021227"
+
+
 def test_conf_epoch_golden(oracle, golden):
     # test/chunkserver/conf_epoch_file_test.cpp:103-106
     c = golden["conf_epoch"]
