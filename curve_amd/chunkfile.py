@@ -137,3 +137,13 @@ def copyset_hash_dir(data_dir: str, chunk_size: int = C.CHUNK_SIZE, meta_size: i
             with open(os.path.join(data_dir, n), "rb") as f:
                 crc = C.CRC32(crc, f.read())
     return str(crc)
+
+
+def get_hash(data_dir: str, chunk_size: int = C.CHUNK_SIZE, meta_size: int = C.META_PAGE_SIZE) -> Tuple[int, str]:
+    """CopysetNode::GetHash's contract (copyset_node.cpp:925-975): (0, hash) on
+    success, (-1, "") when listing, opening, fstat or reading any file fails
+    (copyset_node_test.cpp:864-997 pins these cases)."""
+    try:
+        return 0, copyset_hash_dir(data_dir, chunk_size, meta_size)
+    except OSError:
+        return -1, ""

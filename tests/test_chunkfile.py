@@ -87,5 +87,17 @@ def test_copyset_dir_golden_files(tmp_path, golden):
     assert CF.copyset_hash_dir(str(tmp_path)) == "1355371765"
 
 
+def test_get_hash_error_contract(tmp_path, golden):
+    """copyset_node_test.cpp:864-997: open/fstat/read failure -> -1; empty -> (0, "0")."""
+    from conftest import copyset_files
+    assert CF.get_hash(str(tmp_path)) == (0, "0")
+    for name, data in copyset_files(golden).items():
+        (tmp_path / name).write_bytes(data)
+    assert CF.get_hash(str(tmp_path)) == (0, "1355371765")
+    os.symlink(str(tmp_path / "missing-target"), str(tmp_path / "test-6.txt"))  # listed, cannot be opened
+    assert CF.get_hash(str(tmp_path)) == (-1, "")
+    assert CF.get_hash(str(tmp_path / "no-such-dir")) == (-1, "")
+
+
 def test_empty_copyset_dir(tmp_path):
     assert CF.copyset_hash_dir(str(tmp_path)) == "0"
