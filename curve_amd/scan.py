@@ -22,6 +22,7 @@ CHUNK_SIZE = C.CHUNK_SIZE
 META_PAGE_SIZE = C.META_PAGE_SIZE
 SCAN_SIZE = C.SCAN_SIZE
 PAGE_SIZE = C.PAGE_SIZE
+FORMAT_VERSION_V2 = 2  # datastore/define.h:40
 
 
 @dataclass(frozen=True)
@@ -152,12 +153,16 @@ class DevicePool:
     def scan_maps(self, logical_pool_id: int, copyset_id: int, first_index: int = 0) -> List[ScanMap]:
         """ScanMaps as ScanChunkRequest::OnApply builds them (op_request.cpp:795-803),
         one per scan op in ScanJobProcess order; `index` is the raft log index,
-        here a running counter from first_index."""
+        here a running counter from first_index.  Chunks whose metapage version
+        is not FORMAT_VERSION_V2 are not scanned (scan_manager.cpp:228-231)."""
         slices = C.as_u32(self.slice_crcs)
         metas = C.as_u32(self.meta_crcs[: self.n])
+        versions = self.meta[:, 0].cpu().tolist()
         per_chunk = self.chunk_size // self.scan_size
         out, idx = [], first_index
         for c, cid in enumerate(self.chunk_ids):
+            if versions[c] != FORMAT_VERSION_V2:
+                continue
             out.append(ScanMap(logical_pool_id, copyset_id, cid, idx, metas[c], 0, self.meta_size))
             idx += 1
             for k in range(per_chunk):
@@ -197,3 +202,39 @@ class DevicePool:
         after = torch.tensor(list(after_bytes), dtype=torch.int64, device=dev)
         grp = torch.tensor(list(group), dtype=torch.int32, device=dev)
         return C.digest_dev(self.file_crcs, after, grp, n_groups, stream=stream)
+
+
+def scan_copyset_dir(data_dir: str, logical_pool_id: int, copyset_id: int, first_index: int = 0,
+                     chunk_size: int = CHUNK_SIZE, meta_size: int = META_PAGE_SIZE, scan_size: int = SCAN_SIZE,
+                     io_threads: int = 8) -> List[ScanMap]:
+    """ScanManager::ScanJobProcess over a copyset's chunk files on disk
+    (scan_manager.cpp:210-296): for every chunk (`chunk_<id>`, the ChunkMap;
+    snapshots are not scanned) with a V2 metapage, the metapage op then the
+    data slices, each a ScanMap as ScanChunkRequest::OnApply builds it.  The
+    engine reads the files itself and hashes them on the GPU (cc_scan_files);
+    the reference's per-slice CRC32(readBuffer, size) (op_request.cpp:794) is
+    the same value.  Chunks in ascending id order (the reference iterates an
+    unordered map).  Unreadable chunk files raise OSError (InternalError ->
+    LOG(FATAL) in the reference, op_request.cpp:813-815)."""
+    import os
+    import re
+    if scan_size > chunk_size or chunk_size % scan_size:
+        raise ValueError("scanSize must divide chunkSize")
+    pat = re.compile(r"^chunk_(\d+)$")
+    ids = sorted(int(m.group(1)) for n in os.listdir(data_dir) if (m := pat.match(n)))
+    paths = [os.path.join(data_dir, chunk_file_name(i)) for i in ids]
+    st, mc, sc, _ = C.scan_files(paths, chunk_size, meta_size, PAGE_SIZE, scan_size, io_threads)
+    out, idx = [], first_index
+    for k, cid in enumerate(ids):
+        if st[k] != 0:
+            raise OSError(-int(st[k]) if st[k] < 0 else 22, f"cannot scan {paths[k]}")
+        with open(paths[k], "rb") as f:
+            version = f.read(1)[0]
+        if version != FORMAT_VERSION_V2:
+            continue
+        out.append(ScanMap(logical_pool_id, copyset_id, cid, idx, int(mc[k]), 0, meta_size))
+        idx += 1
+        for j in range(chunk_size // scan_size):
+            out.append(ScanMap(logical_pool_id, copyset_id, cid, idx, int(sc[k, j]), j * scan_size, scan_size))
+            idx += 1
+    return out

@@ -230,6 +230,8 @@ def test_pool_digest_equals_chained_copyset_hash(dev, oracle):
     rng = np.random.default_rng(9)
     data = rng.integers(0, 256, (n, chunk), dtype=np.uint8)
     meta = rng.integers(0, 256, (n, 4096), dtype=np.uint8)
+    meta[:, 0] = 2  # FORMAT_VERSION_V2 ...
+    meta[4, 0] = 1  # ... except one V1 chunk, which ScanJobProcess skips
     ids = [1, 2, 3, 10, 11, 20, 100, 5, 7, 9, 12, 21]
     pool = DevicePool(to_dev(data, dev), to_dev(meta, dev), ids, scan_size=256 << 10)
     pool.scan()
@@ -247,7 +249,10 @@ def test_pool_digest_equals_chained_copyset_hash(dev, oracle):
     # ScanMaps of every chunk vs the oracle's slice schedule
     maps = pool.scan_maps(1, 1)
     k = 0
+    assert len(maps) == 5 * (n - 1)
     for c in range(n):
+        if c == 4:
+            continue
         ref = oracle.scan_slices(meta[c].tobytes(), data[c].tobytes(), 256 << 10)
         for off, ln, crc in ref:
             m = maps[k]
@@ -473,6 +478,39 @@ def test_chunk_service_hash_on_device(dev, golden):
     assert pool.chunk_hash(1, 0, 4096) == str(golden["metapage_residue"]["crc"])
     maps = pool.scan_maps(1, 1)
     assert maps[0].crc == golden["metapage_residue"]["crc"] and maps[0].len == 4096
+
+
+def test_scan_copyset_dir(dev, oracle, tmp_path):
+    """ScanJobProcess over real chunk files: V2 chunks give metapage + slice
+    ScanMaps equal to the oracle's scan_slices; a V1 chunk and a snapshot file
+    are not scanned; a follower copy with one flipped byte fails CompareMap on
+    exactly the slice holding it."""
+    from curve_amd import chunkfile as CF
+    from curve_amd.scan import compare_maps, scan_copyset_dir
+    chunk, sl = 1 << 20, 256 << 10
+    rng = np.random.default_rng(41)
+    lead, foll = tmp_path / "lead", tmp_path / "foll"
+    lead.mkdir()
+    foll.mkdir()
+    raws = {}
+    for cid, ver in ((3, 2), (12, 2), (7, 1), (40, 2)):
+        raw = CF.ChunkFileMetaPage(version=ver, sn=cid).encode() + rng.integers(0, 256, chunk, dtype=np.uint8).tobytes()
+        (lead / CF.chunk_file_name(cid)).write_bytes(raw)
+        bad = bytearray(raw)
+        if cid == 12:
+            bad[4096 + 2 * sl + 77] ^= 4  # slice 2 of chunk 12
+        (foll / CF.chunk_file_name(cid)).write_bytes(bytes(bad))
+        raws[cid] = raw
+    (lead / CF.chunk_file_name(3, 5)).write_bytes(b"s" * 1000)  # snapshot: not in the ChunkMap
+    ml = scan_copyset_dir(str(lead), 1, 9, chunk_size=chunk, scan_size=sl)
+    mf = scan_copyset_dir(str(foll), 1, 9, chunk_size=chunk, scan_size=sl)
+    assert [m.chunkId for m in ml] == [3] * 5 + [12] * 5 + [40] * 5
+    for cid in (3, 12, 40):
+        want = oracle.scan_slices(raws[cid][:4096], raws[cid][4096:], sl)
+        got = [(m.offset, m.len, m.crc) for m in ml if m.chunkId == cid]
+        assert got == want
+    fails = [(a.chunkId, a.offset) for a, b in zip(ml, mf) if not compare_maps(a, [b, b])[0]]
+    assert fails == [(12, 2 * sl)]
 
 
 def test_scan_files(dev, oracle, tmp_path):
