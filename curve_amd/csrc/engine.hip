@@ -12,9 +12,11 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
@@ -53,6 +55,14 @@ void build_lds_image(uint32_t* img) {
 
 namespace {
 
+// Completion of a staging slot's batch, delivered by a host function enqueued
+// behind the batch: the waiting caller sleeps on a condition variable.
+struct SlotSignal {
+    std::mutex m;
+    std::condition_variable cv;
+    bool fired = true;
+};
+
 struct Staging {
     bool ready = false;
     size_t bytes = 0;            // per slot
@@ -62,6 +72,7 @@ struct Staging {
     uint32_t* hcrc[2] = {nullptr, nullptr};
     hipStream_t stream[2] = {nullptr, nullptr};
     hipEvent_t done[2] = {nullptr, nullptr};
+    SlotSignal sig[2];
 };
 
 struct DevCtx {
@@ -164,6 +175,47 @@ int staging_init(DevCtx* c) {
     return CC_OK;
 }
 
+// Blocking *_host calls come from bthread workers / apply threads (SURVEY
+// §8b) and must not burn the caller's CPU.  hipEventSynchronize spins on this
+// ROCm unless the whole device was put in BlockingSync mode before its context
+// existed (measured: scripts/spin_probe.py), and a sleep-poll loop wakes late
+// and stalls the next batch's submission (-2 % e2e).  So each batch ends with
+// a host function that signals a condition variable: the caller parks in the
+// kernel and is woken as soon as the batch's last copy completes.
+void fire_slot(void* p) {
+    SlotSignal* sg = static_cast<SlotSignal*>(p);
+    {
+        std::lock_guard<std::mutex> lk(sg->m);
+        sg->fired = true;
+    }
+    sg->cv.notify_all();
+}
+
+hipError_t arm_slot(Staging& st, int slot, hipStream_t s) {
+    hipError_t e = hipEventRecord(st.done[slot], s);
+    if (e != hipSuccess) return e;
+    SlotSignal& sg = st.sig[slot];
+    {
+        std::lock_guard<std::mutex> lk(sg.m);
+        sg.fired = false;
+    }
+    e = hipLaunchHostFunc(s, fire_slot, &sg);
+    if (e != hipSuccess) {
+        std::lock_guard<std::mutex> lk(sg.m);
+        sg.fired = true;  // nothing will fire: never leave a waiter hanging
+    }
+    return e;
+}
+
+hipError_t park_slot(Staging& st, int slot) {
+    SlotSignal& sg = st.sig[slot];
+    {
+        std::unique_lock<std::mutex> lk(sg.m);
+        sg.cv.wait(lk, [&] { return sg.fired; });
+    }
+    return hipEventSynchronize(st.done[slot]);  // already complete: returns its status
+}
+
 bool is_pinned(const void* p) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
@@ -182,8 +234,14 @@ void staging_free(Staging& st) {
         if (st.hcrc[i]) hipHostFree(st.hcrc[i]);
         if (st.stream[i]) hipStreamDestroy(st.stream[i]);
         if (st.done[i]) hipEventDestroy(st.done[i]);
+        st.host[i] = st.dev[i] = nullptr;
+        st.dcrc[i] = st.hcrc[i] = nullptr;
+        st.stream[i] = nullptr;
+        st.done[i] = nullptr;
+        st.sig[i].fired = true;
     }
-    st = Staging();
+    st.ready = false;
+    st.bytes = 0;
 }
 
 }  // namespace
@@ -475,7 +533,7 @@ int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
         const uint64_t n = (n_pages - done < per_slot) ? n_pages - done : per_slot;
         // reclaim this slot: wait for its previous batch and copy its CRCs out
         if (pending_n[slot]) {
-            if ((e = hipEventSynchronize(st.done[slot])) != hipSuccess) return map_err(e);
+            if ((e = park_slot(st, slot)) != hipSuccess) return map_err(e);
             memcpy(h_out + pending_first[slot], st.hcrc[slot], pending_n[slot] * 4);
             pending_n[slot] = 0;
         }
@@ -499,7 +557,7 @@ int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
         if ((e = hipMemcpyAsync(st.hcrc[slot], st.dcrc[slot], n * 4, hipMemcpyDeviceToHost, st.stream[slot])) !=
             hipSuccess)
             return map_err(e);
-        if ((e = hipEventRecord(st.done[slot], st.stream[slot])) != hipSuccess) return map_err(e);
+        if ((e = arm_slot(st, slot, st.stream[slot])) != hipSuccess) return map_err(e);
         pending_first[slot] = done;
         pending_n[slot] = n;
         done += n;
@@ -510,7 +568,7 @@ int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
             slot ^= 1;
             continue;
         }
-        if ((e = hipEventSynchronize(st.done[slot])) != hipSuccess) return map_err(e);
+        if ((e = park_slot(st, slot)) != hipSuccess) return map_err(e);
         memcpy(h_out + pending_first[slot], st.hcrc[slot], pending_n[slot] * 4);
         pending_n[slot] = 0;
         slot ^= 1;
@@ -630,7 +688,7 @@ int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_b
     hipError_t e = hipSuccess;
     auto drain = [&](int s) -> int {
         if (!pend_n[s]) return CC_OK;
-        hipError_t ee = hipEventSynchronize(st.done[s]);
+        hipError_t ee = park_slot(st, s);
         if (ee != hipSuccess) return map_err(ee);
         const uint32_t* r = st.hcrc[s];
         const uint64_t nb = pend_n[s], f = pend_first[s];
@@ -714,7 +772,7 @@ int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_b
         if ((e = hipMemcpyAsync(st.hcrc[slot], res, nb * (2 + (uint64_t)slices) * 4, hipMemcpyDeviceToHost, s)) !=
             hipSuccess)
             return map_err(e);
-        if ((e = hipEventRecord(st.done[slot], s)) != hipSuccess) return map_err(e);
+        if ((e = arm_slot(st, slot, s)) != hipSuccess) return map_err(e);
         pend_first[slot] = first;
         pend_n[slot] = nb;
         slot ^= 1;
@@ -781,7 +839,7 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
     uint64_t pend_first[2] = {0, 0}, pend_n[2] = {0, 0};
     auto drain = [&](int s) -> int {
         if (!pend_n[s]) return CC_OK;
-        hipError_t ee = hipEventSynchronize(st.done[s]);
+        hipError_t ee = park_slot(st, s);
         if (ee != hipSuccess) return map_err(ee);
         const uint32_t* r = st.hcrc[s];
         const uint64_t nb = pend_n[s], f = pend_first[s];
@@ -902,7 +960,7 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
         if ((e = hipMemcpyAsync(st.hcrc[slot], res, nb * (2 + (uint64_t)slices) * 4, hipMemcpyDeviceToHost, s)) !=
             hipSuccess)
             return map_err(e);
-        if ((e = hipEventRecord(st.done[slot], s)) != hipSuccess) return map_err(e);
+        if ((e = arm_slot(st, slot, s)) != hipSuccess) return map_err(e);
         pend_first[slot] = first;
         pend_n[slot] = nb;
         slot ^= 1;

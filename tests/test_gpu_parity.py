@@ -271,6 +271,24 @@ def test_host_path_pageable_and_pinned(dev, oracle):
     assert (C.page_crc_host(pinned.numpy(), 4096) == want).all()
 
 
+def test_host_call_blocks_without_spinning(dev):
+    """SURVEY §8b threading rule: a blocking *_host call parks the caller (event
+    waits use hipEventBlockingSync) instead of burning a bthread worker.  With
+    pinned input there is no host copy, so the caller's own CPU time stays a
+    small fraction of the wall time of a PCIe-bound 2 GiB call."""
+    import time
+    from curve_amd import crc as C
+    h = torch.empty(2 << 30, dtype=torch.uint8, pin_memory=True)
+    h[:] = 7
+    a = h.numpy()
+    C.page_crc_host(a[: 1 << 20], 4096)  # warm: staging allocated
+    w0, c0 = time.perf_counter(), time.thread_time()
+    out = C.page_crc_host(a, 4096)
+    wall, cpu = time.perf_counter() - w0, time.thread_time() - c0
+    assert out.size == (2 << 30) // 4096 and (out == out[0]).all()
+    assert cpu < 0.5 * wall, (cpu, wall)
+
+
 def test_large_pool_properties(dev, oracle):
     """Full-size-ish (2 GiB = 128 chunks): every page CRC equals the oracle's
     (multithreaded) and the fold of all page CRCs equals the CRC of the whole buffer."""
