@@ -64,6 +64,28 @@ def build_segment(entries: Sequence[Tuple[int, int, bytes]], meta_page_size: int
     return bytes(meta) + body
 
 
+def append_entries(seg: bytes, entries: Sequence[Tuple[int, int, bytes]], meta_page_size: int = 4096) -> bytes:
+    """CurveSegment::append (curve_segment.cpp:405-440) of more entries at the
+    meta page's used-bytes offset, which then moves past them (_update_meta_page)."""
+    used = struct.unpack_from("<q", seg, 0)[0]
+    body = b"".join(pack_entry(t, ty, d) for t, ty, d in entries)
+    out = bytearray(seg[:used]) + body + bytearray(seg[used + len(body):])
+    out[:8] = struct.pack("<q", used + len(body))
+    return bytes(out)
+
+
+def truncate_segment(seg: bytes, headers: Sequence[EntryHeader], keep: int) -> bytes:
+    """CurveSegment::truncate (curve_segment.cpp:663-717): keep the first `keep`
+    entries; the meta page's used bytes drop to the first dropped entry's offset.
+    The dropped bytes stay in the file (the reference only lseeks) and are
+    ignored by the next load and overwritten by the next append."""
+    if keep >= len(headers):
+        return seg
+    out = bytearray(seg)
+    out[:8] = struct.pack("<q", headers[keep].offset)
+    return bytes(out)
+
+
 def parse_segment(seg, meta_page_size: int = 4096) -> List[EntryHeader]:
     """Header walk of CurveSegment::load (curve_segment.cpp:148-190): stops at a
     truncated tail or the first corrupted header (reported with header_ok=False)."""

@@ -42,3 +42,24 @@ def test_truncated_tail_and_corrupt_header():
     seg[full[2].offset + 3] ^= 1
     hs = wal.parse_segment(bytes(seg))
     assert len(hs) == 3 and not hs[2].header_ok and all(h.header_ok for h in hs[:2])
+
+
+def test_truncate_then_append(oracle):
+    """test_curve_segment.cpp open_segment: append 10 "hello, world: %d"
+    entries, truncate(5), append "HELLO, WORLD: %d" for 5..9; the walk sees the
+    first five old entries then the five new ones, every checksum intact."""
+    old = [(1, wal.ENTRY_TYPE_DATA, (b"hello, world: %d" % i) * 300) for i in range(10)]
+    seg = wal.build_segment(old) + bytes(1 << 16)  # preallocated file (prepare_segment)
+    hs = wal.parse_segment(seg)
+    assert len(hs) == 10
+    seg = wal.truncate_segment(seg, hs, 5)
+    assert len(wal.parse_segment(seg)) == 5
+    new = [(1, wal.ENTRY_TYPE_DATA, (b"HELLO, WORLD: %d" % i) * 7) for i in range(5, 10)]
+    seg = wal.append_entries(seg, new)
+    hs = wal.parse_segment(seg)
+    want = [e[2] for e in old[:5] + new]
+    assert len(hs) == 10 and all(h.header_ok for h in hs)
+    for h, data in zip(hs, want):
+        assert h.data_real_len == len(data)
+        assert seg[h.offset + wal.ENTRY_HEADER_SIZE:h.offset + wal.ENTRY_HEADER_SIZE + len(data)] == data
+        assert h.data_checksum == oracle.crc32c(data)
