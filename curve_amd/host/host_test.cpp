@@ -1,0 +1,287 @@
+// curve_amd/host/host_test.cpp -- parity tests of the C++ host layer
+// (chunkserver_host.h) in the shape of the reference's own gtest cases, run
+// as one binary (no gtest in this image).  TEST ONLY: links the CPU oracle
+// (oracle/crc32c_oracle.c) as the checker.
+//
+//   host_test            run every case; GPU cases are SKIPPED when no device
+//   host_test --gpu      fail if no device (GPU box)
+// Exit status 0 iff every case that ran passed.  Prints one line per case.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <functional>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../include/curve_crc.h"
+#include "chunkserver_host.h"
+
+extern "C" uint32_t oc_crc32c_sse42(uint32_t crc, const void* buf, size_t n);  // oracle (test only)
+
+using namespace cchost;
+
+namespace {
+
+int g_fail = 0;
+#define EXPECT(c)                                                             \
+    do {                                                                      \
+        if (!(c)) {                                                           \
+            fprintf(stderr, "  %s:%d: EXPECT(%s) failed\n", __FILE__, __LINE__, #c); \
+            g_fail++;                                                         \
+        }                                                                     \
+    } while (0)
+
+std::string g_tmp;
+
+std::string MakeDir(const std::string& name) {
+    std::string d = g_tmp + "/" + name;
+    mkdir(d.c_str(), 0755);
+    return d;
+}
+
+void WriteFile(const std::string& path, const std::string& bytes) {
+    FILE* f = fopen(path.c_str(), "wb");
+    if (!f) {
+        perror(path.c_str());
+        abort();
+    }
+    fwrite(bytes.data(), 1, bytes.size(), f);
+    fclose(f);
+}
+
+std::string MetaPage(uint64_t sn, uint8_t version = FORMAT_VERSION_V2, uint32_t page = 4096) {
+    std::string buf(page, '\0');
+    ChunkFileMetaPage m;
+    m.version = version;
+    m.sn = sn;
+    m.encode(&buf[0]);
+    return buf;
+}
+
+uint32_t Oracle(const std::string& s, uint32_t crc = 0) { return oc_crc32c_sse42(crc, s.data(), s.size()); }
+
+// ---- test/common/crc32_test.cpp --------------------------------------------
+void Crc32Vectors() {
+    std::string z(32, '\0'), ff(32, '\xff'), inc(32, 0), dec(32, 0);
+    for (int i = 0; i < 32; i++) {
+        inc[i] = (char)i;
+        dec[i] = (char)(31 - i);
+    }
+    EXPECT(crc32c_value(z.data(), 32) == 0x8a9136aaU);
+    EXPECT(crc32c_value(ff.data(), 32) == 0x62a8ab43U);
+    EXPECT(crc32c_value(inc.data(), 32) == 0x46dd794eU);
+    EXPECT(crc32c_value(dec.data(), 32) == 0x113fdb5cU);
+    EXPECT(crc32c_value("hello world", 11) == crc32c_extend(crc32c_value("hello ", 6), "world", 5));
+    EXPECT(crc32c_value("a", 1) != crc32c_value("foo", 3));
+}
+
+// ---- ChunkFileMetaPage (chunkserver_chunkfile.cpp:64-130) -------------------
+void MetaPageEncodeDecode() {
+    std::string page = MetaPage(7);
+    ChunkFileMetaPage d;
+    EXPECT(d.decode(page.data()) == Success && d.sn == 7 && d.version == FORMAT_VERSION_V2);
+    EXPECT(Oracle(page) == 317729701u);  // residue constant of every non-clone 4 KiB metapage
+    page[3] ^= 1;
+    EXPECT(d.decode(page.data()) == CrcCheckError);
+    EXPECT(d.decode(MetaPage(1, 3).data()) == IncompatibleError);
+    ChunkFileMetaPage clone;
+    clone.sn = 2;
+    clone.location = "curvefs:/f@1";
+    clone.bitmapBits = 20;
+    clone.bitmap = {0xA5, 0x0F, 0x03};
+    std::string cp(4096, '\0');
+    clone.encode(&cp[0]);
+    ChunkFileMetaPage back;
+    EXPECT(back.decode(cp.data()) == Success && back.location == clone.location && back.bitmapBits == 20 &&
+           back.bitmap == clone.bitmap);
+}
+
+// ---- ScanManager::CompareMap (scan_manager_test.cpp shapes) -----------------
+void CompareMapCases() {
+    ScanMap a{1, 2, 3, 10, 100, 0, 4096};
+    std::vector<ScanMap> failed;
+    EXPECT(CompareMap(a, {a, a}, &failed) && failed.empty());
+    ScanMap b = a;
+    b.crc = 200;  // mismatched crc
+    EXPECT(!CompareMap(a, {a, b}, &failed) && failed.size() == 1 && failed[0] == a);
+    ScanMap c = a;
+    c.index = 11;  // index is compared too (MessageDifferencer::Equals)
+    EXPECT(!CompareMap(a, {c, a}, &failed) && failed.size() == 2);
+    EXPECT(!CompareMap(a, {a}, &failed) && failed.size() == 2);  // not three maps: not failed
+}
+
+// ---- CopysetNode::GetHash (copyset_node_test.cpp:811-997) -------------------
+void CopysetHashSmallFiles() {
+    std::string d = MakeDir("cs_small");
+    std::string h;
+    EXPECT(GetCopysetHash(d, 16u << 20, 4096, &h) == 0 && h == "0");  // empty dir
+    WriteFile(d + "/test-1.txt", "wwwww\n");
+    WriteFile(d + "/test-4.txt", "mmmmmmmm\n");
+    WriteFile(d + "/test-5.txt", "eeeeeeeeeee\n");
+    WriteFile(d + "/test-3.txt", std::string(7680, '\0'));
+    WriteFile(d + "/test-2.txt", "abcddddddddd333\n");
+    EXPECT(GetCopysetHash(d, 16u << 20, 4096, &h) == 0 && h == "1355371765");
+    EXPECT(symlink((d + "/gone").c_str(), (d + "/test-6.txt").c_str()) == 0);  // listed, cannot be opened
+    EXPECT(GetCopysetHash(d, 16u << 20, 4096, &h) == -1);
+    EXPECT(GetCopysetHash(d + "/no-such-dir", 16u << 20, 4096, &h) == -1);
+}
+
+// ---- ChunkServiceImpl::GetChunkHash request checks (chunk_service_test.cpp:463-502)
+void ChunkServiceHashRequests() {
+    DataStoreOptions o;
+    o.baseDir = MakeDir("svc");
+    std::string h = "x";
+    EXPECT(ChunkServiceGetChunkHash(o, 100, 0, 4096, &h) == CHUNK_OP_STATUS_SUCCESS && h == "0");  // no chunk
+    EXPECT(ChunkServiceGetChunkHash(o, 100, 3, 4096, &h) == CHUNK_OP_STATUS_INVALID_REQUEST);
+    EXPECT(ChunkServiceGetChunkHash(o, 100, 0, 4097, &h) == CHUNK_OP_STATUS_INVALID_REQUEST);
+    EXPECT(ChunkServiceGetChunkHash(o, 100, (16u << 20) - 4096, 8192, &h) == CHUNK_OP_STATUS_INVALID_REQUEST);
+    // a written chunk, small ranges (CPU primitive): chunk_service_test.cpp:563-578
+    std::string raw = MetaPage(1) + std::string(4096, 'a') + std::string((16u << 20) - 4096, '\0');
+    WriteFile(o.baseDir + "/chunk_1", raw);
+    EXPECT(ChunkServiceGetChunkHash(o, 1, 4096, 4096, &h) == CHUNK_OP_STATUS_SUCCESS && h == "650595490");
+    EXPECT(ChunkServiceGetChunkHash(o, 1, 0, 4096, &h) == CHUNK_OP_STATUS_SUCCESS && h == "317729701");
+}
+
+// ---- GPU cases ----------------------------------------------------------------
+void ChunkHashLongRanges() {  // CSChunkFile::GetHash over long raw ranges (engine path)
+    DataStoreOptions o;
+    o.baseDir = MakeDir("hash_long");
+    std::mt19937_64 rng(11);
+    std::string raw(4096 + (16u << 20), '\0');
+    for (auto& c : raw) c = (char)(rng() & 0xFF);
+    std::string meta = MetaPage(3);
+    raw.replace(0, 4096, meta);
+    WriteFile(o.baseDir + "/chunk_9", raw);
+    std::string h;
+    struct R {
+        off_t off;
+        size_t len;
+    } rs[] = {{0, 16u << 20}, {4096, 16u << 20}, {0, (16u << 20) + 4096}, {12288, 1u << 20}, {5, 200001}};
+    for (const auto& r : rs) {
+        EXPECT(GetChunkHash(o, 9, r.off, r.len, &h) == Success);
+        EXPECT(h == std::to_string(Oracle(raw.substr(r.off, r.len))));
+    }
+    EXPECT(GetChunkHash(o, 9, 4096, (16u << 20) + 1, &h) == InternalError);  // past the end of the file
+    EXPECT(ChunkServiceGetChunkHash(o, 9, 0, 16u << 20, &h) == CHUNK_OP_STATUS_SUCCESS &&
+           h == std::to_string(Oracle(raw.substr(0, 16u << 20))));
+}
+
+void CopysetHashOneChunk() {  // chunkserver_snapshot_test.cpp:339-388
+    std::string d = MakeDir("cs_one");
+    std::string data(16u << 20, '\0');
+    memset(&data[0], 'b', 25 * 4096);
+    WriteFile(d + "/chunk_1", MetaPage(1) + data);
+    std::string h;
+    EXPECT(GetCopysetHash(d, 16u << 20, 4096, &h) == 0 && h == "3049021227");
+}
+
+void CopysetHashMixed() {  // chunk files + a snapshot of other geometry + small files, sorted chain
+    std::string d = MakeDir("cs_mixed");
+    std::mt19937_64 rng(5);
+    std::vector<std::pair<std::string, std::string>> files;
+    for (uint64_t id : {1, 2, 10, 11, 100}) {
+        std::string data(1u << 20, '\0');
+        for (auto& c : data) c = (char)(rng() & 0xFF);
+        files.emplace_back(ChunkFileName(id), MetaPage(id) + data);
+    }
+    files.emplace_back("chunk_2_snap_1", std::string(300000, 's'));
+    files.emplace_back("zz", "tail");
+    for (auto& f : files) WriteFile(d + "/" + f.first, f.second);
+    std::sort(files.begin(), files.end());
+    uint32_t want = 0;
+    for (auto& f : files) want = Oracle(f.second, want);
+    std::string h;
+    EXPECT(GetCopysetHash(d, 1u << 20, 4096, &h) == 0 && h == std::to_string(want));
+}
+
+void ScanCopysetMaps() {  // ScanJobProcess + OnApply over chunk files
+    DataStoreOptions o;
+    o.baseDir = MakeDir("scan");
+    o.chunkSize = 1u << 20;
+    const uint32_t scan = 256u << 10;
+    std::mt19937_64 rng(7);
+    std::vector<std::pair<uint64_t, std::string>> chunks;
+    for (auto idv : std::vector<std::pair<uint64_t, uint8_t>>{{12, 2}, {3, 2}, {7, 1}, {40, 2}}) {
+        std::string data(o.chunkSize, '\0');
+        for (auto& c : data) c = (char)(rng() & 0xFF);
+        std::string raw = MetaPage(idv.first, idv.second) + data;
+        WriteFile(o.baseDir + "/" + ChunkFileName(idv.first), raw);
+        if (idv.second == FORMAT_VERSION_V2) chunks.emplace_back(idv.first, raw);
+    }
+    WriteFile(o.baseDir + "/chunk_3_snap_2", "snapshot");
+    std::sort(chunks.begin(), chunks.end());
+    std::vector<ScanMap> maps;
+    EXPECT(ScanCopyset(o, 1, 9, scan, 100, &maps) == 0);
+    EXPECT(maps.size() == chunks.size() * 5);
+    size_t k = 0;
+    for (auto& c : chunks) {
+        for (int op = 0; op < 5 && k < maps.size(); op++, k++) {
+            const ScanMap& m = maps[k];
+            const uint64_t off = op == 0 ? 0 : (uint64_t)(op - 1) * scan;
+            const uint64_t len = op == 0 ? 4096 : scan;
+            const std::string bytes = op == 0 ? c.second.substr(0, 4096) : c.second.substr(4096 + off, len);
+            EXPECT(m.chunkId == c.first && m.offset == off && m.len == len && m.index == 100 + k &&
+                   m.logicalPoolId == 1 && m.copysetId == 9);
+            EXPECT(m.crc == Oracle(bytes));
+        }
+    }
+    EXPECT(ScanCopyset(o, 1, 9, 3u << 18, 0, &maps) == -1);  // scanSize must divide chunkSize
+}
+
+struct Case {
+    const char* name;
+    bool gpu;
+    std::function<void()> fn;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const bool need_gpu = argc > 1 && strcmp(argv[1], "--gpu") == 0;
+    char tmpl[] = "/tmp/cchost_XXXXXX";
+    const char* t = mkdtemp(tmpl);
+    if (!t) {
+        perror("mkdtemp");
+        return 2;
+    }
+    g_tmp = t;
+    const bool have_gpu = cc_engine_init(nullptr) == CC_OK;
+    if (need_gpu && !have_gpu) {
+        fprintf(stderr, "no usable GPU: %s\n", cc_strerror(cc_engine_init(nullptr)));
+        return 2;
+    }
+    const Case cases[] = {
+        {"Crc32Vectors", false, Crc32Vectors},
+        {"MetaPageEncodeDecode", false, MetaPageEncodeDecode},
+        {"CompareMapCases", false, CompareMapCases},
+        {"CopysetHashSmallFiles", false, CopysetHashSmallFiles},
+        {"ChunkServiceHashRequests", false, ChunkServiceHashRequests},
+        {"ChunkHashLongRanges", true, ChunkHashLongRanges},
+        {"CopysetHashOneChunk", true, CopysetHashOneChunk},
+        {"CopysetHashMixed", true, CopysetHashMixed},
+        {"ScanCopysetMaps", true, ScanCopysetMaps},
+    };
+    int ran = 0, skipped = 0, failed_cases = 0;
+    for (const Case& c : cases) {
+        if (c.gpu && !have_gpu) {
+            printf("[ SKIP ] %s (no GPU)\n", c.name);
+            skipped++;
+            continue;
+        }
+        const int before = g_fail;
+        c.fn();
+        ran++;
+        const bool ok = g_fail == before;
+        failed_cases += !ok;
+        printf("[%s] %s\n", ok ? "  OK  " : " FAIL ", c.name);
+    }
+    printf("%d ran, %d failed, %d skipped\n", ran, failed_cases, skipped);
+    if (have_gpu) cc_engine_fini();
+    std::string rm = "rm -rf " + g_tmp;
+    if (system(rm.c_str()) != 0) fprintf(stderr, "cleanup of %s failed\n", g_tmp.c_str());
+    return failed_cases ? 1 : 0;
+}

@@ -1,0 +1,40 @@
+"""The C++ host layer (curve_amd/host: chunkserver surfaces over the C ABI)
+through its own test binary, whose cases follow the reference's gtest cases.
+CPU: every non-GPU case must pass (GPU cases report SKIP).  GPU: all cases."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOST = os.path.join(ROOT, "curve_amd", "host")
+BIN = os.path.join(HOST, "host_test")
+
+
+@pytest.fixture(scope="module")
+def host_test():
+    if not os.path.exists(os.path.join(ROOT, "curve_amd", "libcurvecrc.so")):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "curve_amd", "csrc")], check=True)
+    subprocess.run(["make", "-s", "-C", HOST], check=True)
+    return BIN
+
+
+def run(binary, *args, timeout=300):
+    p = subprocess.run([binary, *args], capture_output=True, text=True, timeout=timeout)
+    return p.returncode, p.stdout + p.stderr
+
+
+def test_host_layer_cpu_cases(host_test):
+    import torch
+    if torch.cuda.device_count() > 0:  # counting devices does not initialise HIP here
+        pytest.skip("GPU present: covered by test_host_layer_all_cases")
+    rc, out = run(host_test)
+    assert rc == 0, out
+    assert "5 ran, 0 failed, 4 skipped" in out, out
+
+
+@pytest.mark.gpu
+def test_host_layer_all_cases(host_test):
+    rc, out = run(host_test, "--gpu")
+    assert rc == 0, out
+    assert "9 ran, 0 failed, 0 skipped" in out, out
