@@ -20,6 +20,8 @@ CC_ENODEV = -19
 CC_ENOMEM = -12
 CC_EHIP = -5
 CC_ECORRUPT = -74
+CC_ECOMM = -71
+CC_COMM_ID_BYTES = 128
 
 # every symbol include/curve_crc.h declares: (name, restype, argtypes)
 _u32, _u64, _sz, _vp, _int = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int
@@ -35,6 +37,14 @@ class CcFileResult(ctypes.Structure):
 
 class CcChunkSrc(ctypes.Structure):
     _fields_ = [("meta", _vp), ("data", _vp)]
+
+
+class CcPoolShard(ctypes.Structure):  # include/curve_crc.h cc_pool_shard
+    _fields_ = [("d_data", _vp), ("d_meta", _vp), ("n_chunks", _u64), ("chunk_bytes", _u32),
+                ("meta_bytes", _u32), ("page_bytes", _u32), ("slice_bytes", _u32), ("d_after_mult", _vp),
+                ("d_group", _vp), ("n_groups", _u64), ("d_page_crcs", _vp), ("d_meta_crcs", _vp),
+                ("d_slice_crcs", _vp), ("d_file_crcs", _vp), ("d_digest", _vp), ("ev_pages_begin", _vp),
+                ("ev_pages_end", _vp)]
 
 
 SIGNATURES = {
@@ -68,6 +78,13 @@ SIGNATURES = {
     "cc_scan_files": (_int, [ctypes.POINTER(ctypes.c_char_p), _u64, _u32, _u32, _u32, _u32, _u32, _vp,
                               ctypes.POINTER(CcFileResult)]),
     "cc_scan_host": (_int, [ctypes.POINTER(CcChunkSrc), _u64, _u32, _u32, _u32, _u32, _vp, _vp, _vp]),
+    "cc_comm_unique_id": (_int, [_vp, _sz]),
+    "cc_comm_init": (_int, [ctypes.POINTER(_vp), _int, _int, _vp, _sz]),
+    "cc_comm_destroy": (_int, [_vp]),
+    "cc_comm_size": (_int, [_vp]),
+    "cc_comm_rank": (_int, [_vp]),
+    "cc_digest_allreduce_dev": (_int, [_vp, _vp, _u64, _vp]),
+    "cc_pool_scan_dev": (_int, [ctypes.POINTER(CcPoolShard), _vp, _vp]),
 }
 
 _lib = None

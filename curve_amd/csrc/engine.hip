@@ -261,6 +261,7 @@ const char* cc_strerror(int code) {
         case CC_ENOMEM: return "out of memory";
         case CC_EHIP: return "HIP runtime error";
         case CC_ECORRUPT: return "checksum mismatch";
+        case CC_ECOMM: return "RCCL communication error";
         default: return "unknown error";
     }
 }

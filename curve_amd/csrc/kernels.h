@@ -117,4 +117,7 @@ hipError_t launch_combine(const uint32_t* a, const uint32_t* b, uint32_t m_len_b
 hipError_t launch_digest(const uint32_t* crcs, const uint64_t* after_bytes, const uint32_t* group, uint64_t n,
                          uint32_t* digest, hipStream_t s);
 
+// out[i] = XOR_r gathered[r*n + i]  (digest fold after the RCCL all-gather)
+hipError_t launch_xor_fold(const uint32_t* gathered, uint32_t nranks, uint64_t n, uint32_t* out, hipStream_t s);
+
 }  // namespace cc

@@ -638,6 +638,17 @@ __global__ __launch_bounds__(256) void digest_kernel(const uint32_t* __restrict_
     }
 }
 
+// out[i] = XOR over r of gathered[r*n + i]: the local fold after the RCCL
+// all-gather of per-copyset digest partials (XOR is not an RCCL op).
+__global__ void xor_fold_kernel(const uint32_t* __restrict__ gathered, uint32_t nranks, uint64_t n,
+                                uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t v = 0;
+    for (uint32_t r = 0; r < nranks; r++) v ^= gathered[(uint64_t)r * n + i];
+    out[i] = v;
+}
+
 template <int MODE>
 hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
     const dim3 grid(a.blocks), block(kBlockThreads);
@@ -773,6 +784,12 @@ hipError_t launch_combine(const uint32_t* a, const uint32_t* b, uint32_t m_len_b
     if (n == 0) return hipSuccess;
     const uint64_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(combine_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a, b, m_len_b, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_xor_fold(const uint32_t* gathered, uint32_t nranks, uint64_t n, uint32_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(xor_fold_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, gathered, nranks, n, out);
     return hipGetLastError();
 }
 

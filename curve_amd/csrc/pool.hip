@@ -1,0 +1,156 @@
+// curve_amd/csrc/pool.hip -- full-pool integrity scan sharded over the GPUs of
+// a node (BASELINE config 5): one process per GPU, one rank's scan
+// pass as ONE C call, and the per-copyset digest exchange over RCCL (xGMI).
+//
+// Reference: CopysetNode::GetHash (src/chunkserver/copyset_node.cpp:925-975)
+// chains CRC32 over the copyset's files in std::sort name order; the scan
+// hasher (ScanChunkRequest::OnApply, src/chunkserver/op_request.cpp:769-820)
+// produces one ScanMap.crc per metapage / 4 MiB slice op that
+// ScanManager::ScanJobProcess schedules (scan_manager.cpp:210-296).  The
+// reference has no multi-GPU (or multi-process) form of either; the sharding is
+// new and is exact because the chain is linear over GF(2):
+//     V(f1 || .. || fn) = XOR_i shift(V(fi), bytes after fi)
+// so each rank contributes order-free XOR partials for the files it holds and
+// one all-gather of 4 B per copyset per rank completes every digest.  XOR is
+// not an RCCL reduction op (sum/prod/min/max/avg), hence all-gather + a local
+// XOR fold rather than all-reduce; the payload (4 B x copysets x ranks) is
+// latency-bound, far below one xGMI link's bandwidth.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <mutex>
+
+#include "../../include/curve_crc.h"
+#include "kernels.h"
+
+struct cc_comm {
+    ncclComm_t nc = nullptr;
+    int nranks = 0, rank = 0, device = -1;
+    uint32_t* gather = nullptr;  // nranks x cap words of all-gather scratch on `device`
+    uint64_t cap = 0;
+    std::mutex mu;               // guards the scratch (re)allocation
+};
+
+static_assert(CC_COMM_ID_BYTES == sizeof(ncclUniqueId), "RCCL unique id size");
+
+namespace {
+
+int map_hip(hipError_t e) {
+    if (e == hipSuccess) return CC_OK;
+    if (e == hipErrorOutOfMemory) return CC_ENOMEM;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return CC_ENODEV;
+    return CC_EHIP;
+}
+
+int map_nccl(ncclResult_t r) { return r == ncclSuccess ? CC_OK : CC_ECOMM; }
+
+}  // namespace
+
+extern "C" {
+
+int cc_comm_unique_id(void* id, size_t bytes) {
+    if (!id || bytes < sizeof(ncclUniqueId)) return CC_EINVAL;
+    ncclUniqueId u;
+    const int rc = map_nccl(ncclGetUniqueId(&u));
+    if (rc) return rc;
+    memcpy(id, &u, sizeof(u));
+    return CC_OK;
+}
+
+int cc_comm_init(cc_comm** comm, int nranks, int rank, const void* id, size_t bytes) {
+    if (!comm || !id || bytes < sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks) return CC_EINVAL;
+    *comm = nullptr;
+    int dev = -1, n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || hipGetDevice(&dev) != hipSuccess) return CC_ENODEV;
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    cc_comm* c = new cc_comm();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = dev;
+    const int rc = map_nccl(ncclCommInitRank(&c->nc, nranks, u, rank));
+    if (rc) {
+        delete c;
+        return rc;
+    }
+    *comm = c;
+    return CC_OK;
+}
+
+int cc_comm_destroy(cc_comm* comm) {
+    if (!comm) return CC_OK;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(comm->device);
+    if (comm->gather) (void)hipFree(comm->gather);
+    const int rc = comm->nc ? map_nccl(ncclCommDestroy(comm->nc)) : CC_OK;
+    if (cur >= 0) (void)hipSetDevice(cur);
+    delete comm;
+    return rc;
+}
+
+int cc_comm_size(const cc_comm* comm) { return comm ? comm->nranks : 0; }
+int cc_comm_rank(const cc_comm* comm) { return comm ? comm->rank : -1; }
+
+int cc_digest_allreduce_dev(cc_comm* comm, uint32_t* d_digest, uint64_t n, void* stream) {
+    if (!comm || (!d_digest && n)) return CC_EINVAL;
+    if (n == 0) return CC_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    {
+        std::lock_guard<std::mutex> lk(comm->mu);
+        if (n > comm->cap) {  // grows once per layout; the old scratch may still be in use on s
+            if (comm->gather) {
+                hipError_t e = hipStreamSynchronize(s);
+                if (e != hipSuccess) return map_hip(e);
+                (void)hipFree(comm->gather);
+                comm->gather = nullptr;
+                comm->cap = 0;
+            }
+            hipError_t e = hipMalloc(reinterpret_cast<void**>(&comm->gather), (size_t)comm->nranks * n * 4);
+            if (e != hipSuccess) return map_hip(e);
+            comm->cap = n;
+        }
+    }
+    // ring all-gather of the partials into [rank][n], then out = XOR over ranks
+    int rc = map_nccl(ncclAllGather(d_digest, comm->gather, n, ncclUint32, comm->nc, s));
+    if (rc) return rc;
+    return map_hip(cc::launch_xor_fold(comm->gather, (uint32_t)comm->nranks, n, d_digest, s));
+}
+
+int cc_pool_scan_dev(const cc_pool_shard* p, cc_comm* comm, void* stream) {
+    if (!p) return CC_EINVAL;
+    if (p->n_chunks == 0 && !comm) return CC_OK;
+    if (p->page_bytes == 0 || p->slice_bytes == 0 || p->chunk_bytes % p->page_bytes ||
+        p->chunk_bytes % p->slice_bytes || p->slice_bytes % p->page_bytes)
+        return CC_EINVAL;
+    if (p->n_chunks && (!p->d_data || !p->d_meta || !p->d_page_crcs || !p->d_meta_crcs || !p->d_slice_crcs))
+        return CC_EINVAL;
+    const bool dig = p->d_digest != nullptr;
+    if (dig && p->n_chunks && (!p->d_after_mult || !p->d_group)) return CC_EINVAL;
+    if (comm && !dig) return CC_EINVAL;  // nothing to exchange
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint64_t pages = p->n_chunks * (uint64_t)(p->chunk_bytes / p->page_bytes);
+    int rc;
+    hipError_t e;
+    if (p->ev_pages_begin && (e = hipEventRecord(static_cast<hipEvent_t>(p->ev_pages_begin), s)) != hipSuccess)
+        return map_hip(e);
+    // the hot kernel: every 4 KiB data page of the shard
+    if ((rc = cc_page_crc_dev(p->d_data, pages, p->page_bytes, p->d_page_crcs, stream))) return rc;
+    if (p->ev_pages_end && (e = hipEventRecord(static_cast<hipEvent_t>(p->ev_pages_end), s)) != hipSuccess)
+        return map_hip(e);
+    // readMetaPage ops: one "page" of meta_bytes per chunk
+    if ((rc = cc_page_crc_dev(p->d_meta, p->n_chunks, p->meta_bytes, p->d_meta_crcs, stream))) return rc;
+    if (dig && (e = hipMemsetAsync(p->d_digest, 0, p->n_groups * 4, s)) != hipSuccess) return map_hip(e);
+    // slices + file CRCs + digest partials in one launch
+    if ((rc = cc_scan_epilogue_dev(p->d_page_crcs, p->d_meta_crcs, p->n_chunks, p->chunk_bytes / p->page_bytes,
+                                   p->page_bytes, p->slice_bytes / p->page_bytes, p->d_slice_crcs, p->d_file_crcs,
+                                   dig ? p->d_after_mult : nullptr, dig ? p->d_group : nullptr,
+                                   dig ? p->d_digest : nullptr, stream)))
+        return rc;
+    if (comm) return cc_digest_allreduce_dev(comm, p->d_digest, p->n_groups, stream);
+    return CC_OK;
+}
+
+}  // extern "C"

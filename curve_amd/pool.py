@@ -73,3 +73,94 @@ def reduce_digests(partial, dist, group=None):
 def digests_as_hash_strings(digests) -> List[str]:
     """Per-copyset digests -> GetCopysetStatus(queryhash) strings (std::to_string(uint32))."""
     return [str(int(x) & 0xFFFFFFFF) for x in digests.detach().cpu().tolist()]
+
+
+# ---------------------------------------------------------------------------
+# Native path (libcurvecrc): RCCL communicator + one-call shard scan.  This is
+# what a C++ chunkserver binds (include/curve_crc.h cc_comm_* / cc_pool_scan_dev);
+# torch is only the device-memory / stream / rendezvous plumbing here.
+# ---------------------------------------------------------------------------
+class Comm:
+    """An RCCL communicator created and owned by libcurvecrc (cc_comm_init)."""
+
+    def __init__(self, nranks: int, rank: int, uid: bytes):
+        import ctypes
+        from . import _lib
+        if len(uid) != _lib.CC_COMM_ID_BYTES:
+            raise ValueError("unique id must be CC_COMM_ID_BYTES long")
+        self._h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(uid), len(uid))
+        _lib.check(_lib.lib().cc_comm_init(ctypes.byref(self._h), nranks, rank, buf, len(uid)), "cc_comm_init")
+        self.nranks, self.rank = nranks, rank
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes
+        from . import _lib
+        buf = ctypes.create_string_buffer(_lib.CC_COMM_ID_BYTES)
+        _lib.check(_lib.lib().cc_comm_unique_id(buf, _lib.CC_COMM_ID_BYTES), "cc_comm_unique_id")
+        return buf.raw
+
+    @property
+    def handle(self):
+        return self._h
+
+    def allreduce_digest(self, digest, stream=None):
+        """In place: digest[g] <- XOR over ranks (cc_digest_allreduce_dev)."""
+        from . import _lib
+        from .crc import _dev_ptr, _stream_handle
+        _lib.check(_lib.lib().cc_digest_allreduce_dev(self._h, _dev_ptr(digest, "digest"), digest.numel(),
+                                                      _stream_handle(stream)), "cc_digest_allreduce_dev")
+        return digest
+
+    def close(self):
+        from . import _lib
+        if self._h:
+            _lib.check(_lib.lib().cc_comm_destroy(self._h), "cc_comm_destroy")
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_from_dist(dist, group=None) -> Comm:
+    """Rank 0 makes the RCCL unique id, torch.distributed carries its 128 bytes
+    to every rank (as the MDS or any out-of-band channel would), then every
+    rank joins the native communicator on its current device."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    obj = [Comm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return Comm(world, rank, obj[0])
+
+
+def pool_scan(pool, after_mult, group, digest, comm: "Comm" = None, stream=None, events=None):
+    """One integrity scan pass over a DevicePool shard as ONE native call
+    (cc_pool_scan_dev): page CRCs, metapage CRCs, slice/file CRCs, digest
+    partials and -- with a Comm -- the RCCL digest exchange.  `events` =
+    (begin, end) torch.cuda.Event pair recorded around the page kernel (they
+    must already exist: record each once beforehand)."""
+    import ctypes
+    from . import _lib
+    from .crc import _dev_ptr, _stream_handle
+    s = _lib.CcPoolShard()
+    s.d_data = _dev_ptr(pool.data, "data").value
+    s.d_meta = _dev_ptr(pool.meta, "meta").value
+    s.n_chunks = pool.n
+    s.chunk_bytes, s.meta_bytes = pool.chunk_size, pool.meta_size
+    s.page_bytes, s.slice_bytes = pool.page_bytes, pool.scan_size
+    s.d_after_mult = _dev_ptr(after_mult, "after_mult").value if after_mult is not None else None
+    s.d_group = _dev_ptr(group, "group").value if group is not None else None
+    s.n_groups = digest.numel() if digest is not None else 0
+    s.d_page_crcs = _dev_ptr(pool.page_crcs, "page_crcs").value
+    s.d_meta_crcs = _dev_ptr(pool.meta_crcs, "meta_crcs").value
+    s.d_slice_crcs = _dev_ptr(pool.slice_crcs, "slice_crcs").value
+    s.d_file_crcs = _dev_ptr(pool.file_crcs, "file_crcs").value
+    s.d_digest = _dev_ptr(digest, "digest").value if digest is not None else None
+    if events is not None:
+        s.ev_pages_begin, s.ev_pages_end = events[0].cuda_event, events[1].cuda_event
+    _lib.check(_lib.lib().cc_pool_scan_dev(ctypes.byref(s), comm.handle if comm is not None else None,
+                                           _stream_handle(stream)), "cc_pool_scan_dev")
+    return digest

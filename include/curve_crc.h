@@ -257,6 +257,70 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
                   cc_file_result* h_results);
 
 /* ------------------------------------------------------------------------
+ * Full-pool integrity scan sharded over the GPUs of a node (BASELINE config 5,
+ * SURVEY §8e).  One process per GPU; each rank scans the chunk-index range it
+ * owns with no data-path collective.  The only exchange is the per-copyset
+ * digest of CopysetNode::GetHash (copyset_node.cpp:925-975): order-free XOR
+ * partials, all-gathered over RCCL (xGMI) and XOR-folded on the device (XOR is
+ * not an RCCL reduction op).  Per-chunk work is the scan hasher's
+ * (ScanChunkRequest::OnApply, op_request.cpp:769-820, for every op that
+ * ScanManager::ScanJobProcess schedules, scan_manager.cpp:210-296).
+ * ------------------------------------------------------------------------ */
+#define CC_ECOMM (-71) /* an RCCL call failed */
+#define CC_COMM_ID_BYTES 128
+
+typedef struct cc_comm cc_comm; /* opaque: an RCCL communicator + gather scratch */
+
+/* Rank 0 creates the id and hands its CC_COMM_ID_BYTES bytes to every rank
+ * out of band (the MDS, a TCP store, ...). */
+int cc_comm_unique_id(void* id, size_t bytes);
+/* Collective: every rank calls it with the same id, on the HIP device it owns
+ * (the calling thread's current device).  Blocks until all ranks joined. */
+int cc_comm_init(cc_comm** comm, int nranks, int rank, const void* id, size_t bytes);
+int cc_comm_destroy(cc_comm* comm);
+int cc_comm_size(const cc_comm* comm);
+int cc_comm_rank(const cc_comm* comm);
+
+/* d_digest[0..n) <- XOR over all ranks of their d_digest[0..n) (in place;
+ * collective, stream-ordered, enqueue only).  Calls on one communicator must
+ * be issued in the same order on every rank, from one stream at a time. */
+int cc_digest_allreduce_dev(cc_comm* comm, uint32_t* d_digest, uint64_t n, void* stream);
+
+/* One rank's shard of the pool and the outputs of one scan pass over it. */
+typedef struct cc_pool_shard {
+    const void* d_data;       /* n_chunks x chunk_bytes, chunk c's data at c*chunk_bytes */
+    const void* d_meta;       /* n_chunks x meta_bytes metapages (file = metapage || data) */
+    uint64_t n_chunks;
+    uint32_t chunk_bytes;     /* 16 MiB (conf/chunkserver.conf chunksize) */
+    uint32_t meta_bytes;      /* 4 KiB metapage */
+    uint32_t page_bytes;      /* 4 KiB */
+    uint32_t slice_bytes;     /* 4 MiB scan slice (copyset.scan_size_byte) */
+    const uint32_t* d_after_mult; /* [n_chunks] x^(8*bytes after the file in its copyset chain), cc_xpow8_dev */
+    const uint32_t* d_group;      /* [n_chunks] copyset index of each file */
+    uint64_t n_groups;            /* copysets in the WHOLE pool (same on every rank) */
+    /* outputs (device) */
+    uint32_t* d_page_crcs;    /* [n_chunks * chunk_bytes/page_bytes] */
+    uint32_t* d_meta_crcs;    /* [n_chunks]  ScanMap.crc of the readMetaPage op */
+    uint32_t* d_slice_crcs;   /* [n_chunks * chunk_bytes/slice_bytes]  ScanMap.crc of the data ops */
+    uint32_t* d_file_crcs;    /* [n_chunks]  CRC32(metapage || data), may be NULL */
+    uint32_t* d_digest;       /* [n_groups]  full per-copyset digests after the call */
+    /* optional hipEvent_t recorded on `stream` right before / after the page
+     * kernel over the data (NULL = none): lets a bench time the hot kernel
+     * inside the one call */
+    void* ev_pages_begin;
+    void* ev_pages_end;
+} cc_pool_shard;
+
+/* One integrity scan pass over the shard: page CRCs of every data page and
+ * metapage, slice CRCs (ScanMap.crc), file CRCs, digest partials, then (comm
+ * non-NULL) the digest all-reduce, after which d_digest[g] on every rank is
+ * copyset g's CopysetNode::GetHash value over the WHOLE pool
+ * (V(f1||..||fn) = XOR_i shift(V(fi), bytes after fi): exact, no constant).
+ * Enqueue only; comm NULL = single-rank pool.  Needs chunk_bytes = 256*q
+ * pages with slice_bytes = q*2^j pages (the fused epilogue's geometry). */
+int cc_pool_scan_dev(const cc_pool_shard* shard, cc_comm* comm, void* stream);
+
+/* ------------------------------------------------------------------------
  * Diagnostics (new; no reference counterpart)
  * ------------------------------------------------------------------------ */
 /* Copy the 163840-byte LDS image the page kernel loads into every CU (G tables
