@@ -396,7 +396,65 @@ def plan_updates(rec_in, max_batches: int = 1 << 16):
 _work_cache = {}
 
 
+def log_records(dst_off, src_off, lens):
+    """Write log (in write order) as cc_update records (numpy structured array)."""
+    import numpy as np
+    dst_off = np.asarray(dst_off, dtype=np.uint64)
+    rec = np.zeros(dst_off.size, dtype=_update_dtype())
+    rec["dst"], rec["src"], rec["len"] = dst_off, np.asarray(src_off, dtype=np.uint64), np.asarray(lens, np.uint32)
+    return rec
+
+
+_log_work = {}
+
+
+def apply_log(pool, page_crcs, src, d_log, n_updates: int, max_len: int, page_bytes: int = PAGE_SIZE, stream=None):
+    """cc_apply_log_dev: the write log `d_log` (device tensor of n_updates
+    cc_update records, WRITE order, overlaps allowed) applied to `pool` with
+    later writes winning, and the CRC of every touched page recomputed in
+    `page_crcs` -- ordering, apply and rehash all on the device."""
+    torch = _torch()
+    need = int(lib().cc_apply_log_work_bytes(n_updates, max_len, page_bytes))
+    if need == 0:
+        raise CurveCrcError(_lib.CC_EINVAL, "unsupported log geometry")
+    key = pool.device
+    work = _log_work.get(key)
+    if work is None or work.numel() < need:
+        work = torch.empty(need, dtype=torch.uint8, device=pool.device)
+        _log_work[key] = work
+    with torch.cuda.device(pool.device):
+        check(lib().cc_apply_log_dev(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, _dev_ptr(src, "src"),
+                                     _dev_ptr(d_log, "log"), n_updates, max_len, _dev_ptr(page_crcs, "page_crcs"),
+                                     _dev_ptr(work, "work"), work.numel(), _stream_handle(stream)),
+              "cc_apply_log_dev")
+    if stream is not None:
+        work.record_stream(stream)
+    return 1
+
+
 def apply_updates(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int = PAGE_SIZE, stream=None):
+    """Client partial-write path: host-side write log -> device (one copy of the
+    records) -> cc_apply_log_dev.  Returns the number of device calls (1)."""
+    import numpy as np
+    torch = _torch()
+    lens = np.asarray(lens, dtype=np.uint32)
+    dst_off = np.asarray(dst_off, dtype=np.uint64)
+    src_off = np.asarray(src_off, dtype=np.uint64)
+    if not (dst_off.size == src_off.size == lens.size):
+        raise CurveCrcError(_lib.CC_EINVAL, "dst/src/len size mismatch")
+    if lens.size == 0:
+        return 0
+    if (lens == 0).any() or (dst_off + lens > _nbytes(pool)).any() or (src_off + lens > _nbytes(src)).any():
+        raise CurveCrcError(_lib.CC_EINVAL, "update out of range or empty")
+    rec = log_records(dst_off, src_off, lens)
+    d_log = torch.from_numpy(rec.view(np.uint8)).to(pool.device)
+    n = apply_log(pool, page_crcs, src, d_log, rec.size, int(lens.max()), page_bytes, stream)
+    if stream is not None:
+        d_log.record_stream(stream)
+    return n
+
+
+def apply_updates_batched(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int = PAGE_SIZE, stream=None):
     """Client partial-write path on device (cc_apply_updates_dev): write
     src[src_off[i]:+lens[i]] to pool[dst_off[i]:+lens[i]] in order, then
     recompute the CRC of every touched page in `page_crcs` (in place).

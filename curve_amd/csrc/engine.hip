@@ -643,6 +643,76 @@ int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes,
     return map_err(launch_page_list_crc(a, s));
 }
 
+namespace {
+inline bool log_page_ok(uint32_t page_bytes) {
+    const uint32_t m = page_bytes / kWaveBytes;
+    return page_bytes % kWaveBytes == 0 && m >= 1 && m <= 32 && (m & (m - 1)) == 0;
+}
+inline uint32_t log_slots(uint32_t max_len, uint32_t page_bytes) { return (max_len - 1) / page_bytes + 2; }
+inline uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
+}  // namespace
+
+uint64_t cc_apply_log_work_bytes(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes) {
+    if (!log_page_ok(page_bytes) || max_len == 0 || n_updates == 0) return 0;
+    const uint64_t nk = n_updates * log_slots(max_len, page_bytes);
+    if (nk >= (1ull << 31)) return 0;
+    const size_t temp = log_sort_temp_bytes(nk);
+    if (!temp) return 0;
+    return 4 * align256(nk * 4) + align256(temp);
+}
+
+int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
+                     const cc_update* d_log, uint64_t n_updates, uint32_t max_len, uint32_t* d_page_crcs,
+                     void* d_work, uint64_t work_bytes, void* stream) {
+    if (!log_page_ok(page_bytes)) return CC_EINVAL;
+    if (n_updates == 0) return CC_OK;
+    if (!d_pool || !d_src || !d_log || !d_page_crcs || !d_work || max_len == 0) return CC_EINVAL;
+    if (pool_bytes % page_bytes || ((uintptr_t)d_pool & 3u) || ((uintptr_t)d_src & 3u)) return CC_EINVAL;
+    const uint64_t n_pages = pool_bytes / page_bytes;
+    if (n_pages >= kNoPiece) return CC_EINVAL;  // page index must fit a 32-bit key below kNoPiece
+    const uint64_t need = cc_apply_log_work_bytes(n_updates, max_len, page_bytes);
+    if (need == 0 || work_bytes < need) return CC_EINVAL;
+    DevCtx* c = nullptr;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    LogLaunch a = {};
+    a.pool = static_cast<unsigned char*>(d_pool);
+    a.pool_bytes = pool_bytes;
+    a.src = static_cast<const unsigned char*>(d_src);
+    a.upd = reinterpret_cast<const UpdateDesc*>(d_log);
+    a.n_updates = n_updates;
+    a.page_bytes = page_bytes;
+    a.max_len = max_len;
+    a.slots = log_slots(max_len, page_bytes);
+    const uint64_t nk = n_updates * a.slots;
+    unsigned char* w = static_cast<unsigned char*>(d_work);
+    a.keys = reinterpret_cast<uint32_t*>(w);
+    uint32_t* skeys = reinterpret_cast<uint32_t*>(w + align256(nk * 4));
+    a.vals = reinterpret_cast<uint32_t*>(w + 2 * align256(nk * 4));
+    uint32_t* svals = reinterpret_cast<uint32_t*>(w + 3 * align256(nk * 4));
+    void* temp = w + 4 * align256(nk * 4);
+    a.skeys = skeys;
+    a.svals = svals;
+    a.n_keys = nk;
+    a.image = c->image;
+    a.kconst = kconst_for(page_bytes);
+    a.page_crcs = d_page_crcs;
+    // sort only the bits a page index can have, + 1 so kNoPiece sorts last
+    int end_bit = 1;
+    while (end_bit < 32 && (1ull << end_bit) < n_pages) end_bit++;
+    if (end_bit < 32) end_bit++;
+    const uint64_t tiles = (nk + 63) / 64;
+    const uint64_t blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    a.blocks = (int)(blocks < (uint64_t)c->cus ? (blocks ? blocks : 1) : (uint64_t)c->cus);
+    hipError_t e;
+    if ((e = launch_log_expand(a, s)) != hipSuccess) return map_err(e);
+    if ((e = log_sort(temp, work_bytes - 4 * align256(nk * 4), a.keys, skeys, a.vals, svals, nk, end_bit, s)) !=
+        hipSuccess)
+        return map_err(e);
+    return map_err(launch_log_pages(a, s));
+}
+
 // Streaming scan.  Each staging slot holds a batch of whole chunks (data and
 // metapages in separate device regions) plus the per-chunk results; a batch is
 // {H2D data+meta, page kernel over data, page kernel over metapages, fold to

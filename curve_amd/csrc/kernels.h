@@ -84,6 +84,36 @@ struct UpdateLaunch {
 hipError_t launch_apply_updates(const UpdateLaunch& a, hipStream_t s);
 hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s);
 
+// Write-log path (cc_apply_log_dev): every update of an ORDERED log becomes
+// `slots` pieces keyed by the page they touch (0xFFFFFFFF = no piece); a stable
+// sort by page keeps write order inside each page; one wave per touched page
+// then applies its pieces in registers, stores the dirty dwords and rehashes it.
+constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
+struct LogLaunch {
+    unsigned char* pool;
+    uint64_t pool_bytes;
+    const unsigned char* src;
+    const UpdateDesc* upd;
+    uint64_t n_updates;
+    uint32_t page_bytes;
+    uint32_t max_len;
+    uint32_t slots;             // pieces per update: (max_len - 1) / page_bytes + 2
+    uint32_t* keys;             // [n_updates * slots] page of each piece
+    uint32_t* vals;             // [n_updates * slots] update index of each piece
+    const uint32_t* skeys;      // sorted
+    const uint32_t* svals;
+    uint64_t n_keys;
+    const void* image;
+    uint32_t kconst;
+    uint32_t* page_crcs;
+    int blocks;
+};
+hipError_t launch_log_expand(const LogLaunch& a, hipStream_t s);
+hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s);
+size_t log_sort_temp_bytes(uint64_t n);
+hipError_t log_sort(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                    const uint32_t* vals_in, uint32_t* vals_out, uint64_t n, int end_bit, hipStream_t s);
+
 struct RangeDesc {
     uint64_t off, len;
 };

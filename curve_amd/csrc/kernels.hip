@@ -616,6 +616,221 @@ __global__ __launch_bounds__(kBlockThreads) void page_flagged_kernel(UpdateLaunc
     }
 }
 
+// ---------------------------------------------------------------------------
+// Write-log path (cc_apply_log_dev): ordering on the device, no host planning.
+// ---------------------------------------------------------------------------
+// Piece generation: update i -> slots keys (page it touches, or kNoPiece) and
+// values (= i).  Written in write order, so the stable sort keeps it per page.
+// An update that breaks the contract (len 0, len > max_len, beyond the pool)
+// produces no pieces and is not applied at all (never half-applied).
+__global__ void log_expand_kernel(LogLaunch a) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n_updates) return;
+    const UpdateDesc d = a.upd[i];
+    const bool ok = d.len >= 1 && d.len <= a.max_len && d.dst < a.pool_bytes && d.len <= a.pool_bytes - d.dst;
+    const uint64_t p0 = ok ? d.dst / a.page_bytes : 0;
+    const uint64_t p1 = ok ? (d.dst + d.len - 1) / a.page_bytes : 0;
+    for (uint32_t k = 0; k < a.slots; k++) {
+        const bool v = ok && p0 + k <= p1;
+        a.keys[i * a.slots + k] = v ? (uint32_t)(p0 + k) : kNoPiece;
+        a.vals[i * a.slots + k] = (uint32_t)i;
+    }
+}
+
+// The bytes of one update that fall inside one page, page-relative: page bytes
+// [rlo, rhi); the source byte of page byte r is sp[r] (sp is uniform, so every
+// load below is an SGPR base + the lane's 32-bit offset + an immediate).
+struct Piece {
+    uint32_t rlo, rhi;
+    const unsigned char* sp;
+};
+__device__ __forceinline__ Piece piece_in_page(uint64_t pbase, uint32_t page_bytes, uint64_t dst, uint64_t src,
+                                               uint32_t len, const unsigned char* __restrict__ srcbuf) {
+    Piece p;
+    const uint64_t end = dst + len, pend = pbase + page_bytes;
+    p.rlo = (uint32_t)((dst > pbase ? dst : pbase) - pbase);
+    p.rhi = (uint32_t)((end < pend ? end : pend) - pbase);
+    p.sp = srcbuf + (src - dst) + pbase;  // modular: only sp[r], r in [rlo, rhi), is ever dereferenced
+    return p;
+}
+
+// Source bytes of one piece in the layout of the page registers (lane l holds
+// page dwords l + 64j, i.e. page byte r = 4l + 256j).  A dword the piece covers
+// WHOLLY is one unaligned global_load_dword (gfx950 serves unaligned dword
+// loads; all 4 bytes lie in the update's source range).  The at most two
+// partially covered dwords (the piece's first and last) are spliced from the
+// aligned source dwords that hold their needed bytes -- never touching a byte
+// outside the source range -- kept in 4 edge registers, so a page's source can
+// be in flight while the previous page is merged and hashed.
+typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
+
+template <int M>
+struct PieceSrc {
+    uint32_t S[M];
+    uint32_t ea[2], eb[2];  // aligned source dwords holding edge dword k's bytes
+};
+
+// page dword index of the partially covered first / last dword (none = 0xffffffff)
+__device__ __forceinline__ void piece_edges(const Piece& p, uint32_t (&e)[2]) {
+    const uint32_t df = p.rlo >> 2, dl = (p.rhi - 1) >> 2;
+    const bool ff = (p.rlo & 3u) == 0 && 4 * df + 4 <= p.rhi;
+    const bool fl = (p.rhi & 3u) == 0 && 4 * dl >= p.rlo;
+    e[0] = ff ? 0xffffffffu : df;
+    e[1] = (dl != df && !fl) ? dl : 0xffffffffu;
+}
+
+template <int M>
+__device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint32_t lane) {
+    const uint32_t l4 = lane * 4u;
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        const uint32_t b = l4 + 256u * j;
+        const bool full = b >= p.rlo && b + 4 <= p.rhi;
+        r.S[j] = full ? *reinterpret_cast<const u32_unaligned*>(p.sp + b) : 0u;
+    }
+    uint32_t e[2];
+    piece_edges(p, e);
+    const uint32_t sh = (uint32_t)(uintptr_t)p.sp & 3u;  // the same for every dword of the piece
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        r.ea[k] = r.eb[k] = 0u;
+        if (e[k] != 0xffffffffu && lane == (e[k] & 63u)) {
+            const uint32_t b = 4 * e[k];
+            const uint32_t k0 = p.rlo > b ? p.rlo - b : 0u;
+            const uint32_t k1 = p.rhi < b + 4 ? p.rhi - b : 4u;
+            const unsigned char* base = p.sp + b - sh;
+            if (k0 < 4u - sh) r.ea[k] = *reinterpret_cast<const uint32_t*>(base);
+            if (sh && k1 > 4u - sh) r.eb[k] = *reinterpret_cast<const uint32_t*>(base + 4);
+        }
+    }
+}
+
+template <int M>
+__device__ __forceinline__ void merge_piece(uint32_t (&w)[M], uint32_t& dirty, const PieceSrc<M>& r, const Piece& p,
+                                            uint32_t lane) {
+    uint32_t e[2];
+    piece_edges(p, e);
+    const uint32_t sh = (uint32_t)(uintptr_t)p.sp & 3u;
+    const uint32_t v0 = sh ? __builtin_amdgcn_alignbyte(r.eb[0], r.ea[0], sh) : r.ea[0];
+    const uint32_t v1 = sh ? __builtin_amdgcn_alignbyte(r.eb[1], r.ea[1], sh) : r.ea[1];
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        const uint32_t d = lane + 64u * j, b = 4 * d;
+        if (b + 4 <= p.rlo || b >= p.rhi) continue;
+        const uint32_t k0 = p.rlo > b ? p.rlo - b : 0u;
+        const uint32_t k1 = p.rhi < b + 4 ? p.rhi - b : 4u;
+        const uint32_t v = d == e[0] ? v0 : (d == e[1] ? v1 : r.S[j]);
+        const uint32_t mhi = k1 == 4u ? 0xFFFFFFFFu : (1u << (8u * k1)) - 1u;
+        const uint32_t mask = mhi & ~((1u << (8u * k0)) - 1u);
+        w[j] = (v & mask) | (w[j] & ~mask);
+        dirty |= 1u << j;
+    }
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+    // readlane returns int: go through uint32_t so the low half is not sign-extended
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
+}
+
+// One wave per touched page.  Waves walk tiles of 64 sorted pieces; every lane
+// loads its piece's key and update descriptor up front (one latency per tile,
+// not per piece); a lane whose piece starts a new page is a head.  The wave
+// takes its tile's heads in order and software-pipelines them: while page k's
+// pieces are merged, stored and hashed, page k+1's data AND the source bytes
+// of its first piece are already in flight.  A page's further pieces (rare:
+// overlapping / neighbouring writes) are fetched in place, and a page whose
+// pieces run past the tile reads them from the sorted arrays.  Every page is
+// owned by exactly one wave: no write races, no flags, no atomics.
+template <int M>
+__global__ __launch_bounds__(kBlockThreads) void log_pages_kernel(LogLaunch a) {
+    __shared__ uint32_t tab[kLdsBytes / 4];
+    fill_lds(tab, static_cast<const uint4*>(a.image));
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t c0 = lane << 2 & 0x7Cu;
+    const uint32_t c1 = c0 | 0x10000u;
+    const uint32_t cf = kFinBase + (lane << 2);
+    const uint32_t* pages = reinterpret_cast<const uint32_t*>(a.pool) + lane;
+    uint32_t* opages = reinterpret_cast<uint32_t*>(a.pool) + lane;
+    const uint32_t pb = a.page_bytes;
+    const uint64_t n_tiles = (a.n_keys + 63) >> 6;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + wave; t < n_tiles;
+         t += (uint64_t)gridDim.x * kWavesPerBlock) {
+        const uint64_t t0 = t << 6;
+        const uint64_t pos = t0 + lane;
+        const bool valid = pos < a.n_keys;
+        const uint32_t key = valid ? a.skeys[pos] : kNoPiece;
+        uint32_t prev = __shfl_up(key, 1, 64);
+        if (lane == 0) prev = pos > 0 ? a.skeys[pos - 1] : kNoPiece;
+        uint64_t heads = __ballot(key != kNoPiece && (pos == 0 || prev != key));
+        if (!heads) continue;
+        // this lane's piece: its update descriptor (write-log order lives in the sort)
+        uint64_t ddst = 0, dsrc = 0;
+        uint32_t dlen = 0;
+        if (key != kNoPiece) {
+            const UpdateDesc d = a.upd[a.svals[pos]];
+            ddst = d.dst;
+            dsrc = d.src;
+            dlen = d.len;
+        }
+        uint32_t A[M], B[M];
+        PieceSrc<M> S0, S1;
+        uint32_t h = (uint32_t)__builtin_ctzll(heads);
+        heads &= heads - 1;
+        uint32_t page = __builtin_amdgcn_readlane(key, h);
+        Piece p0 = piece_in_page((uint64_t)page * pb, pb, readlane64(ddst, h), readlane64(dsrc, h),
+                                 __builtin_amdgcn_readlane(dlen, h), a.src);
+        load_page<M>(A, pages + (uint64_t)page * (64u * M));
+        fetch_piece<M>(S0, p0, lane);
+        for (;;) {
+            const bool more = heads != 0;
+            const uint32_t hn = more ? (uint32_t)__builtin_ctzll(heads) : h;
+            heads &= heads - 1;
+            const uint32_t npage = __builtin_amdgcn_readlane(key, hn);
+            Piece p1 = p0;
+            if (more) {  // next page + its first piece's source bytes in flight
+                p1 = piece_in_page((uint64_t)npage * pb, pb, readlane64(ddst, hn), readlane64(dsrc, hn),
+                                   __builtin_amdgcn_readlane(dlen, hn), a.src);
+                load_page<M>(B, pages + (uint64_t)npage * (64u * M));
+                fetch_piece<M>(S1, p1, lane);
+            }
+            const uint64_t pbase = (uint64_t)page * pb;
+            uint32_t dirty = 0;
+            merge_piece<M>(A, dirty, S0, p0, lane);
+            // further pieces of this page, in write order
+            for (uint64_t q = t0 + h + 1; q < a.n_keys; q++) {
+                Piece pq;
+                if (q < t0 + 64) {
+                    const uint32_t l = (uint32_t)(q - t0);
+                    if (__builtin_amdgcn_readlane(key, l) != page) break;
+                    pq = piece_in_page(pbase, pb, readlane64(ddst, l), readlane64(dsrc, l),
+                                       __builtin_amdgcn_readlane(dlen, l), a.src);
+                } else {
+                    if (a.skeys[q] != page) break;
+                    const UpdateDesc d = a.upd[a.svals[q]];
+                    pq = piece_in_page(pbase, pb, d.dst, d.src, d.len, a.src);
+                }
+                PieceSrc<M> X;
+                fetch_piece<M>(X, pq, lane);
+                merge_piece<M>(A, dirty, X, pq, lane);
+            }
+#pragma unroll
+            for (int j = 0; j < M; j++)
+                if ((dirty >> j) & 1u) opages[(uint64_t)page * (64u * M) + 64u * j] = A[j];
+            const uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, A, c0, c1), cf)) ^ a.kconst;
+            if (lane == 0) a.page_crcs[page] = crc;
+            if (!more) break;
+#pragma unroll
+            for (int j = 0; j < M; j++) A[j] = B[j];
+            S0 = S1;
+            p0 = p1;
+            h = hn;
+            page = npage;
+        }
+    }
+}
+
 __global__ void combine_kernel(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t m,
                                uint64_t n, uint32_t* __restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -761,6 +976,29 @@ hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s) {
         default: return hipErrorInvalidValue;
     }
 #undef CC_LCASE
+    return hipGetLastError();
+}
+
+hipError_t launch_log_expand(const LogLaunch& a, hipStream_t s) {
+    if (a.n_updates == 0) return hipSuccess;
+    hipLaunchKernelGGL(log_expand_kernel, dim3((uint32_t)((a.n_updates + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s) {
+    if (a.n_keys == 0) return hipSuccess;
+#define CC_GCASE(MM) \
+    case MM: hipLaunchKernelGGL((log_pages_kernel<MM>), dim3(a.blocks), dim3(kBlockThreads), 0, s, a); break;
+    switch (a.page_bytes / kWaveBytes) {
+        CC_GCASE(1)
+        CC_GCASE(2)
+        CC_GCASE(4)
+        CC_GCASE(8)
+        CC_GCASE(16)
+        CC_GCASE(32)
+        default: return hipErrorInvalidValue;
+    }
+#undef CC_GCASE
     return hipGetLastError();
 }
 

@@ -1,0 +1,35 @@
+// curve_amd/csrc/log_sort.hip -- the one library primitive of the write-log
+// path: a stable device radix sort of (page, update index) pieces by page
+// (hipCUB over rocPRIM).  Kept in its own translation unit: the template
+// instantiation is heavy and nothing else here needs it.
+//
+// Stability is what carries the raft-log order (op_request.cpp:429-481 applies
+// writes in log order): pieces are generated in write order, so after a STABLE
+// sort by page the pieces of one page are still in write order and the page
+// kernel applies them front to back (later writes win).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace cc {
+
+size_t log_sort_temp_bytes(uint64_t n) {
+    size_t bytes = 0;
+    // sizing query only (no launch); 32 bits is the widest sort ever requested
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, static_cast<const uint32_t*>(nullptr),
+                                           static_cast<uint32_t*>(nullptr), static_cast<const uint32_t*>(nullptr),
+                                           static_cast<uint32_t*>(nullptr), (int)n, 0, 32) != hipSuccess)
+        return 0;
+    return bytes;
+}
+
+hipError_t log_sort(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                    const uint32_t* vals_in, uint32_t* vals_out, uint64_t n, int end_bit, hipStream_t s) {
+    size_t bytes = temp_bytes;
+    return hipcub::DeviceRadixSort::SortPairs(temp, bytes, keys_in, keys_out, vals_in, vals_out, (int)n, 0, end_bit,
+                                              s);
+}
+
+}  // namespace cc

@@ -213,6 +213,25 @@ int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes,
 int cc_plan_updates(const cc_update* h_in, uint64_t n, cc_update* h_out, uint64_t* h_batch_ends,
                     uint32_t max_batches, uint32_t* n_batches);
 
+/* Client partial-write path with the ordering done on the device (the
+ * drop-in for the write loop of WriteChunkRequest::OnApply -> CSChunkFile::Write,
+ * op_request.cpp:429-481, chunkserver_chunkfile.cpp:287-427, which applies
+ * writes in raft-log order).  d_log[0..n) is the ORDERED write log: entries may
+ * overlap, have any alignment and straddle pages; later entries win.  Every
+ * entry becomes one piece per page it touches, a stable device radix sort by
+ * page keeps write order inside each page, and one wave per touched page
+ * merges that page's pieces in registers, stores the changed dwords and writes
+ * the page's new CRC to d_page_crcs (untouched pages keep theirs).  No host
+ * planning, one sort + 2 kernels.  Contract per entry: 1 <= len <= max_len and
+ * dst + len <= pool_bytes -- an entry that breaks it is skipped whole (never
+ * half-applied); d_src must not alias d_pool.  page_bytes = 256 * 2^k
+ * (k = 0..5).  d_work: >= cc_apply_log_work_bytes(n, max_len, page_bytes) bytes
+ * (0 = unsupported sizes). */
+uint64_t cc_apply_log_work_bytes(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes);
+int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
+                     const cc_update* d_log, uint64_t n_updates, uint32_t max_len, uint32_t* d_page_crcs,
+                     void* d_work, uint64_t work_bytes, void* stream);
+
 /* One chunk file as the datastore holds it: metapage + data
  * (file = metapage || data, chunkserver_chunkfile.cpp:497-536). */
 typedef struct cc_chunk_src {

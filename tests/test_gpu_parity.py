@@ -327,7 +327,29 @@ def test_beyond_4gib_offsets(dev, oracle):
     lens = [70001, 4096, 5000, (1 << 20)]
     got = u32(C.crc_ranges(d, offs, lens))
     assert [int(x) for x in got] == [oracle.crc32c(host[o:o + l].tobytes()) for o, l in zip(offs, lens)]
-    del d, pc
+    # write log with destinations and sources past 2^31 / 2^32 (64-bit offsets in
+    # every lane-to-scalar move of the log kernel), overlapping in log order
+    rng = np.random.default_rng(31)
+    n = 4000
+    lens_u = rng.integers(1, 4097, n).astype(np.uint32)
+    dst = rng.integers(0, nbytes - 4096, n).astype(np.uint64)
+    dst[:1000] = rng.integers((4 << 30) - 8192, (4 << 30) + 8192, 1000)  # pile-up across the 4 GiB line
+    dst[1000:2000] = rng.integers((2 << 30) - 8192, (2 << 30) + 8192, 1000)  # and across 2 GiB
+    src_off = rng.integers(0, nbytes - 4096, n).astype(np.uint64)
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev).random_(0, 256)
+    C.apply_updates(d, pc, src, dst, src_off, lens_u, 4096)
+    src_h = src.cpu().numpy()
+    want = host  # in-order host application (host is d's pre-log copy)
+    for i in range(n):
+        want[dst[i]:dst[i] + lens_u[i]] = src_h[src_off[i]:src_off[i] + lens_u[i]]
+    got_h = d.cpu().numpy()
+    touched = np.unique(np.concatenate([dst // 4096, (dst + lens_u - 1) // 4096])).astype(np.int64)
+    for p in touched:
+        assert (got_h[p * 4096:(p + 1) * 4096] == want[p * 4096:(p + 1) * 4096]).all(), p
+    pcs = u32(pc)
+    for p in touched:
+        assert pcs[p] == oracle.crc32c(want[p * 4096:(p + 1) * 4096].tobytes()), p
+    del d, pc, src
     torch.cuda.empty_cache()
 
 
@@ -396,8 +418,10 @@ def test_scan_host_stream(dev, oracle, pinned):
         assert fc[i] == oracle.crc32c(m.tobytes() + d.tobytes())
 
 
-@pytest.mark.parametrize("page_bytes,n_upd,overlap", [(4096, 3000, False), (4096, 2000, True), (512, 2500, True)])
-def test_partial_writes(dev, oracle, page_bytes, n_upd, overlap):
+@pytest.mark.parametrize("batched", [False, True])
+@pytest.mark.parametrize("page_bytes,n_upd,overlap", [(4096, 3000, False), (4096, 2000, True), (512, 2500, True),
+                                                      (256, 1500, True), (8192, 1000, True)])
+def test_partial_writes(dev, oracle, page_bytes, n_upd, overlap, batched):
     """cc_apply_updates_dev: unaligned sub-page writes (1 B .. >1 page, straddling
     pages, overlapping in order) -> pool bytes == in-order host application and
     every page CRC == oracle on the final bytes (touched pages recomputed,
@@ -415,14 +439,52 @@ def test_partial_writes(dev, oracle, page_bytes, n_upd, overlap):
     dst = rng.integers(0, span, n_upd)
     src_data = rng.integers(0, 256, int(lens.sum()) + 8, dtype=np.uint8)
     src_off = np.concatenate([[0], np.cumsum(lens)[:-1]]) + rng.integers(0, 4, n_upd) * 0
-    nb = C.apply_updates(d_pool, crcs, to_dev(src_data, dev), dst, src_off, lens, page_bytes)
-    assert (nb > 1) == overlap or not overlap
+    apply = C.apply_updates_batched if batched else C.apply_updates
+    nb = apply(d_pool, crcs, to_dev(src_data, dev), dst, src_off, lens, page_bytes)
+    assert nb == 1 or batched
+    assert (nb > 1) == overlap or not overlap or not batched
     want = host.copy()
     for i in range(n_upd):
         want[dst[i]:dst[i] + lens[i]] = src_data[src_off[i]:src_off[i] + lens[i]]
     got = d_pool.cpu().numpy()
     assert (got == want).all()
     assert (u32(crcs) == oracle.page_crcs(want, page_bytes, threads=8)).all()
+
+
+def test_write_log_hot_pages_and_contract(dev, oracle):
+    """cc_apply_log_dev with every write piled on a few pages (long per-page
+    piece lists that cross sort tiles, applied strictly in log order), plus
+    entries that break the contract (len 0, len > max_len, beyond the pool):
+    those are skipped whole, everything else lands as in-order application."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(77)
+    pool_bytes, pb = 1 << 20, 4096
+    host = rng.integers(0, 256, pool_bytes, dtype=np.uint8)
+    d_pool = to_dev(host, dev)
+    crcs = C.page_crc(d_pool, pb)
+    n = 700
+    lens = rng.integers(1, 3000, n).astype(np.uint32)
+    dst = (rng.integers(0, 3 * pb, n) + 5 * pb).astype(np.uint64)  # pages 5..8
+    src_off = rng.integers(0, 1 << 16, n).astype(np.uint64)
+    src_data = rng.integers(0, 256, (1 << 16) + 4096, dtype=np.uint8)
+    bad = [3, 100, 101, 650]
+    lens[3] = 0                       # empty
+    lens[100] = 3500                  # > max_len below
+    dst[101] = pool_bytes - 10        # runs past the pool
+    lens[101] = 20
+    dst[650] = 1 << 40                # far beyond the pool
+    max_len = 3000
+    rec = C.log_records(dst, src_off, lens)
+    d_log = torch.from_numpy(rec.view(np.uint8)).to(dev)
+    C.apply_log(d_pool, crcs, to_dev(src_data, dev), d_log, n, max_len, pb)
+    want = host.copy()
+    for i in range(n):
+        if i in bad:
+            continue
+        want[dst[i]:dst[i] + lens[i]] = src_data[src_off[i]:src_off[i] + lens[i]]
+    got = d_pool.cpu().numpy()
+    assert (got == want).all()
+    assert (u32(crcs) == oracle.page_crcs(want, pb)).all()
 
 
 def test_crc_ranges_arbitrary(dev, oracle):
