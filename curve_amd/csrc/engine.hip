@@ -658,7 +658,7 @@ uint64_t cc_apply_log_work_bytes(uint64_t n_updates, uint32_t max_len, uint32_t 
     if (nk >= (1ull << 31)) return 0;
     const size_t temp = log_sort_temp_bytes(nk);
     if (!temp) return 0;
-    return 4 * align256(nk * 4) + align256(temp);
+    return 5 * align256(nk * 4) + 256 + align256(temp);
 }
 
 int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
@@ -691,7 +691,9 @@ int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, con
     uint32_t* skeys = reinterpret_cast<uint32_t*>(w + align256(nk * 4));
     a.vals = reinterpret_cast<uint32_t*>(w + 2 * align256(nk * 4));
     uint32_t* svals = reinterpret_cast<uint32_t*>(w + 3 * align256(nk * 4));
-    void* temp = w + 4 * align256(nk * 4);
+    a.heads = reinterpret_cast<uint32_t*>(w + 4 * align256(nk * 4));
+    a.head_count = reinterpret_cast<uint32_t*>(w + 5 * align256(nk * 4));
+    void* temp = w + 5 * align256(nk * 4) + 256;
     a.skeys = skeys;
     a.svals = svals;
     a.n_keys = nk;
@@ -702,14 +704,15 @@ int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, con
     int end_bit = 1;
     while (end_bit < 32 && (1ull << end_bit) < n_pages) end_bit++;
     if (end_bit < 32) end_bit++;
-    const uint64_t tiles = (nk + 63) / 64;
-    const uint64_t blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    // at most n_keys page runs: a wave per run up to one 8-wave block per CU
+    const uint64_t blocks = (nk + kWavesPerBlock - 1) / kWavesPerBlock;
     a.blocks = (int)(blocks < (uint64_t)c->cus ? (blocks ? blocks : 1) : (uint64_t)c->cus);
     hipError_t e;
     if ((e = launch_log_expand(a, s)) != hipSuccess) return map_err(e);
-    if ((e = log_sort(temp, work_bytes - 4 * align256(nk * 4), a.keys, skeys, a.vals, svals, nk, end_bit, s)) !=
-        hipSuccess)
+    if ((e = log_sort(temp, work_bytes - 5 * align256(nk * 4) - 256, a.keys, skeys, a.vals, svals, nk, end_bit,
+                      s)) != hipSuccess)
         return map_err(e);
+    if ((e = launch_log_heads(a, s)) != hipSuccess) return map_err(e);
     return map_err(launch_log_pages(a, s));
 }
 

@@ -86,8 +86,9 @@ hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s);
 
 // Write-log path (cc_apply_log_dev): every update of an ORDERED log becomes
 // `slots` pieces keyed by the page they touch (0xFFFFFFFF = no piece); a stable
-// sort by page keeps write order inside each page; one wave per touched page
-// then applies its pieces in registers, stores the dirty dwords and rehashes it.
+// sort by page keeps write order inside each page; the page runs' starts are
+// compacted; one wave per touched page (balanced over the grid) then applies
+// its pieces in registers, stores the changed rows and rehashes it.
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
 struct LogLaunch {
     unsigned char* pool;
@@ -103,12 +104,15 @@ struct LogLaunch {
     const uint32_t* skeys;      // sorted
     const uint32_t* svals;
     uint64_t n_keys;
+    uint32_t* heads;            // [n_keys] sorted positions that start a page run (unordered)
+    uint32_t* head_count;       // number of them (zeroed by the expand kernel)
     const void* image;
     uint32_t kconst;
     uint32_t* page_crcs;
     int blocks;
 };
 hipError_t launch_log_expand(const LogLaunch& a, hipStream_t s);
+hipError_t launch_log_heads(const LogLaunch& a, hipStream_t s);
 hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s);
 size_t log_sort_temp_bytes(uint64_t n);
 hipError_t log_sort(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,

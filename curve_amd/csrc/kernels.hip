@@ -625,6 +625,7 @@ __global__ __launch_bounds__(kBlockThreads) void page_flagged_kernel(UpdateLaunc
 // produces no pieces and is not applied at all (never half-applied).
 __global__ void log_expand_kernel(LogLaunch a) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *a.head_count = 0u;  // for log_heads_kernel, later on the stream
     if (i >= a.n_updates) return;
     const UpdateDesc d = a.upd[i];
     const bool ok = d.len >= 1 && d.len <= a.max_len && d.dst < a.pool_bytes && d.len <= a.pool_bytes - d.dst;
@@ -655,14 +656,18 @@ __device__ __forceinline__ Piece piece_in_page(uint64_t pbase, uint32_t page_byt
 }
 
 // Source bytes of one piece in the layout of the page registers (lane l holds
-// page dwords l + 64j, i.e. page byte r = 4l + 256j).  A dword the piece covers
-// WHOLLY is one unaligned global_load_dword (gfx950 serves unaligned dword
-// loads; all 4 bytes lie in the update's source range).  The at most two
-// partially covered dwords (the piece's first and last) are spliced from the
-// aligned source dwords that hold their needed bytes -- never touching a byte
-// outside the source range -- kept in 4 edge registers, so a page's source can
-// be in flight while the previous page is merged and hashed.
-typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
+// page dwords l + 64j, i.e. page byte r = 4l + 256j), fetched with buffer
+// loads: a lane that needs nothing passes an out-of-range offset, which the
+// buffer unit answers with 0 without touching memory.  So every load is issued
+// unconditionally (no branches around loads: hipcc's vmcnt counts stay exact
+// and the next page's fetch really overlaps this page's merge + hash) and no
+// byte outside the update's source range is ever read.  A dword the piece
+// covers WHOLLY is one unaligned buffer_load_dword (gfx950 serves unaligned
+// dword loads).  The at most two partially covered dwords (the piece's first
+// and last) are spliced from the aligned source dwords holding their needed
+// bytes, kept in 4 edge registers instead of a second [M] array.
+constexpr uint32_t kBufOOB = 0x80000000u;   // offset past num_records: load 0 / store dropped
+constexpr uint32_t kBufFlags = 0x00020000u;  // buffer resource dword 3 for gfx9-family (CDNA)
 
 template <int M>
 struct PieceSrc {
@@ -681,30 +686,37 @@ __device__ __forceinline__ void piece_edges(const Piece& p, uint32_t (&e)[2]) {
 
 template <int M>
 __device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint32_t lane) {
+    const uint32_t sh = (uint32_t)(uintptr_t)p.sp & 3u;  // the same for every dword of the piece
+    // whole dwords: base sp, offset = page byte; edges: aligned base sp - sh
+    const __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(p.sp), 0, 64u * 4u * M + 8u, kBufFlags);
+    const __amdgpu_buffer_rsrc_t re =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(p.sp - sh), 0, 64u * 4u * M + 8u, kBufFlags);
     const uint32_t l4 = lane * 4u;
 #pragma unroll
     for (int j = 0; j < M; j++) {
         const uint32_t b = l4 + 256u * j;
         const bool full = b >= p.rlo && b + 4 <= p.rhi;
-        r.S[j] = full ? *reinterpret_cast<const u32_unaligned*>(p.sp + b) : 0u;
+        r.S[j] = __builtin_amdgcn_raw_buffer_load_b32(rw, full ? b : kBufOOB, 0, 0);
     }
     uint32_t e[2];
     piece_edges(p, e);
-    const uint32_t sh = (uint32_t)(uintptr_t)p.sp & 3u;  // the same for every dword of the piece
 #pragma unroll
     for (int k = 0; k < 2; k++) {
-        r.ea[k] = r.eb[k] = 0u;
-        if (e[k] != 0xffffffffu && lane == (e[k] & 63u)) {
-            const uint32_t b = 4 * e[k];
-            const uint32_t k0 = p.rlo > b ? p.rlo - b : 0u;
-            const uint32_t k1 = p.rhi < b + 4 ? p.rhi - b : 4u;
-            const unsigned char* base = p.sp + b - sh;
-            if (k0 < 4u - sh) r.ea[k] = *reinterpret_cast<const uint32_t*>(base);
-            if (sh && k1 > 4u - sh) r.eb[k] = *reinterpret_cast<const uint32_t*>(base + 4);
-        }
+        const uint32_t b = 4 * (e[k] & 0x3fffffffu);
+        const bool mine = e[k] != 0xffffffffu && lane == (e[k] & 63u);
+        const uint32_t k0 = p.rlo > b ? p.rlo - b : 0u;
+        const uint32_t k1 = p.rhi < b + 4 ? p.rhi - b : 4u;
+        r.ea[k] = __builtin_amdgcn_raw_buffer_load_b32(re, (mine && k0 < 4u - sh) ? b : kBufOOB, 0, 0);
+        r.eb[k] = __builtin_amdgcn_raw_buffer_load_b32(re, (mine && sh && k1 > 4u - sh) ? b + 4 : kBufOOB, 0, 0);
     }
 }
 
+// A piece is one contiguous byte range, so each 256-byte row j of the page
+// (dwords l + 64j of all lanes) is uniformly outside it, wholly inside it (then
+// every lane just takes its source dword), or one of its <= 2 boundary rows:
+// only those run the per-lane byte-mask merge.  `dirty` (rows written) is
+// wave-uniform.
 template <int M>
 __device__ __forceinline__ void merge_piece(uint32_t (&w)[M], uint32_t& dirty, const PieceSrc<M>& r, const Piece& p,
                                             uint32_t lane) {
@@ -713,8 +725,16 @@ __device__ __forceinline__ void merge_piece(uint32_t (&w)[M], uint32_t& dirty, c
     const uint32_t sh = (uint32_t)(uintptr_t)p.sp & 3u;
     const uint32_t v0 = sh ? __builtin_amdgcn_alignbyte(r.eb[0], r.ea[0], sh) : r.ea[0];
     const uint32_t v1 = sh ? __builtin_amdgcn_alignbyte(r.eb[1], r.ea[1], sh) : r.ea[1];
+    const uint32_t row0 = p.rlo >> 8, row1 = (p.rhi - 1) >> 8;  // first / last row touched (uniform)
+    const bool whole0 = (p.rlo & 255u) == 0, whole1 = (p.rhi & 255u) == 0;
 #pragma unroll
     for (int j = 0; j < M; j++) {
+        if ((uint32_t)j < row0 || (uint32_t)j > row1) continue;  // uniform
+        dirty |= 1u << j;
+        if (((uint32_t)j > row0 || whole0) && ((uint32_t)j < row1 || whole1)) {  // whole row
+            w[j] = r.S[j];
+            continue;
+        }
         const uint32_t d = lane + 64u * j, b = 4 * d;
         if (b + 4 <= p.rlo || b >= p.rhi) continue;
         const uint32_t k0 = p.rlo > b ? p.rlo - b : 0u;
@@ -723,7 +743,6 @@ __device__ __forceinline__ void merge_piece(uint32_t (&w)[M], uint32_t& dirty, c
         const uint32_t mhi = k1 == 4u ? 0xFFFFFFFFu : (1u << (8u * k1)) - 1u;
         const uint32_t mask = mhi & ~((1u << (8u * k0)) - 1u);
         w[j] = (v & mask) | (w[j] & ~mask);
-        dirty |= 1u << j;
     }
 }
 
@@ -733,15 +752,41 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
 }
 
-// One wave per touched page.  Waves walk tiles of 64 sorted pieces; every lane
-// loads its piece's key and update descriptor up front (one latency per tile,
-// not per piece); a lane whose piece starts a new page is a head.  The wave
-// takes its tile's heads in order and software-pipelines them: while page k's
-// pieces are merged, stored and hashed, page k+1's data AND the source bytes
-// of its first piece are already in flight.  A page's further pieces (rare:
-// overlapping / neighbouring writes) are fetched in place, and a page whose
-// pieces run past the tile reads them from the sorted arrays.  Every page is
-// owned by exactly one wave: no write races, no flags, no atomics.
+// Page runs of the sorted pieces: position q starts a run (a "head") when its
+// page differs from position q-1's.  Heads are compacted into a.heads (in no
+// particular order: runs are independent) with one atomic per wave; the count
+// was zeroed by log_expand_kernel earlier on the stream.
+__global__ __launch_bounds__(1024) void log_heads_kernel(LogLaunch a) {
+    __shared__ uint32_t wcount[16], bbase;
+    const uint64_t pos = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const bool in = pos < a.n_keys;
+    const uint32_t key = in ? a.skeys[pos] : kNoPiece;
+    const uint32_t prev = (in && pos > 0) ? a.skeys[pos - 1] : kNoPiece;
+    const bool head = key != kNoPiece && key != prev;
+    const uint64_t m = __ballot(head);
+    if (lane == 0) wcount[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // one global atomic per 1024 positions
+        uint32_t tot = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; w++) tot += wcount[w];
+        bbase = tot ? atomicAdd(a.head_count, tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t base = bbase;
+    for (uint32_t w = 0; w < wv; w++) base += wcount[w];
+    if (head) a.heads[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)pos;
+}
+
+// One wave per touched page, balanced: wave w owns heads w, w + W, w + 2W, ...
+// (W = waves in the grid), ~pages/W each.  Its lanes load the metadata of up to
+// 64 of its heads at once (position, page, next position's page, update
+// descriptor: one round trip per 64 pages), then the wave software-pipelines
+// them: while page k's pieces are merged, stored and hashed, page k+1's data
+// AND the source bytes of its first piece are in flight.  A page with more
+// pieces (overlapping / neighbouring writes: rare) reads them from the sorted
+// arrays in place, in write order.  Every page is owned by exactly one wave: no
+// write races, no flags, no atomics on the data.
 template <int M>
 __global__ __launch_bounds__(kBlockThreads) void log_pages_kernel(LogLaunch a) {
     __shared__ uint32_t tab[kLdsBytes / 4];
@@ -752,72 +797,68 @@ __global__ __launch_bounds__(kBlockThreads) void log_pages_kernel(LogLaunch a) {
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
     const uint32_t* pages = reinterpret_cast<const uint32_t*>(a.pool) + lane;
-    uint32_t* opages = reinterpret_cast<uint32_t*>(a.pool) + lane;
     const uint32_t pb = a.page_bytes;
-    const uint64_t n_tiles = (a.n_keys + 63) >> 6;
-    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + wave; t < n_tiles;
-         t += (uint64_t)gridDim.x * kWavesPerBlock) {
-        const uint64_t t0 = t << 6;
-        const uint64_t pos = t0 + lane;
-        const bool valid = pos < a.n_keys;
-        const uint32_t key = valid ? a.skeys[pos] : kNoPiece;
-        uint32_t prev = __shfl_up(key, 1, 64);
-        if (lane == 0) prev = pos > 0 ? a.skeys[pos - 1] : kNoPiece;
-        uint64_t heads = __ballot(key != kNoPiece && (pos == 0 || prev != key));
-        if (!heads) continue;
-        // this lane's piece: its update descriptor (write-log order lives in the sort)
-        uint64_t ddst = 0, dsrc = 0;
-        uint32_t dlen = 0;
-        if (key != kNoPiece) {
-            const UpdateDesc d = a.upd[a.svals[pos]];
-            ddst = d.dst;
-            dsrc = d.src;
-            dlen = d.len;
-        }
+    const uint32_t H = *a.head_count;
+    const uint32_t W = gridDim.x * kWavesPerBlock;
+    for (uint32_t base = blockIdx.x * kWavesPerBlock + wave; base < H; base += 64u * W) {
+        // lane k <- head base + k*W (clamped loads: no branches around them)
+        const uint64_t ih = (uint64_t)base + (uint64_t)lane * W;
+        const bool hv = ih < H;
+        const uint32_t pos = a.heads[hv ? ih : base];
+        const uint32_t key = a.skeys[pos];
+        const uint32_t nkey = a.skeys[pos + 1 < a.n_keys ? pos + 1 : pos];
+        const UpdateDesc d = a.upd[a.svals[pos]];
+        const uint64_t ddst = d.dst, dsrc = d.src;
+        const uint32_t dlen = d.len;
+        const bool single = pos + 1 >= a.n_keys || nkey != key;  // the page's only piece
+        const uint64_t singles = __ballot(single);
+        const uint32_t cnt = (uint32_t)__popcll(__ballot(hv));  // valid lanes are 0 .. cnt-1
+        // two pages in flight: k (being merged + hashed) and k+1.  (A third
+        // buys nothing: a page iteration issues ~53 VMEM instructions -- 16 page
+        // loads, 20 source loads, 17 stores -- and gfx950's 6-bit vmcnt cannot
+        // count two iterations' worth, so the waits stop being exact.)
         uint32_t A[M], B[M];
         PieceSrc<M> S0, S1;
-        uint32_t h = (uint32_t)__builtin_ctzll(heads);
-        heads &= heads - 1;
-        uint32_t page = __builtin_amdgcn_readlane(key, h);
-        Piece p0 = piece_in_page((uint64_t)page * pb, pb, readlane64(ddst, h), readlane64(dsrc, h),
-                                 __builtin_amdgcn_readlane(dlen, h), a.src);
+        auto head_piece = [&](uint32_t k, uint32_t pg) {
+            return piece_in_page((uint64_t)pg * pb, pb, readlane64(ddst, k), readlane64(dsrc, k),
+                                 __builtin_amdgcn_readlane(dlen, k), a.src);
+        };
+        uint32_t h = 0;
+        uint32_t page = __builtin_amdgcn_readlane(key, 0);
+        Piece p0 = head_piece(0, page);
         load_page<M>(A, pages + (uint64_t)page * (64u * M));
         fetch_piece<M>(S0, p0, lane);
         for (;;) {
-            const bool more = heads != 0;
-            const uint32_t hn = more ? (uint32_t)__builtin_ctzll(heads) : h;
-            heads &= heads - 1;
-            const uint32_t npage = __builtin_amdgcn_readlane(key, hn);
-            Piece p1 = p0;
-            if (more) {  // next page + its first piece's source bytes in flight
-                p1 = piece_in_page((uint64_t)npage * pb, pb, readlane64(ddst, hn), readlane64(dsrc, hn),
-                                   __builtin_amdgcn_readlane(dlen, hn), a.src);
-                load_page<M>(B, pages + (uint64_t)npage * (64u * M));
-                fetch_piece<M>(S1, p1, lane);
-            }
+            const bool more = h + 1 < cnt;
+            // page k+1 + its first piece's source bytes in flight (clamped to the
+            // last page: a harmless re-read, so every iteration issues the same
+            // loads and the vmcnt waits stay exact)
+            const uint32_t h1 = more ? h + 1 : h;
+            const uint32_t page1 = __builtin_amdgcn_readlane(key, h1);
+            const Piece p1 = head_piece(h1, page1);
+            load_page<M>(B, pages + (uint64_t)page1 * (64u * M));
+            fetch_piece<M>(S1, p1, lane);
             const uint64_t pbase = (uint64_t)page * pb;
             uint32_t dirty = 0;
             merge_piece<M>(A, dirty, S0, p0, lane);
-            // further pieces of this page, in write order
-            for (uint64_t q = t0 + h + 1; q < a.n_keys; q++) {
-                Piece pq;
-                if (q < t0 + 64) {
-                    const uint32_t l = (uint32_t)(q - t0);
-                    if (__builtin_amdgcn_readlane(key, l) != page) break;
-                    pq = piece_in_page(pbase, pb, readlane64(ddst, l), readlane64(dsrc, l),
-                                       __builtin_amdgcn_readlane(dlen, l), a.src);
-                } else {
+            if (!((singles >> h) & 1ull)) {  // further pieces of this page, in write order
+                for (uint32_t q = __builtin_amdgcn_readlane(pos, h) + 1; q < a.n_keys; q++) {
                     if (a.skeys[q] != page) break;
-                    const UpdateDesc d = a.upd[a.svals[q]];
-                    pq = piece_in_page(pbase, pb, d.dst, d.src, d.len, a.src);
+                    const UpdateDesc dq = a.upd[a.svals[q]];
+                    const Piece pq = piece_in_page(pbase, pb, dq.dst, dq.src, dq.len, a.src);
+                    PieceSrc<M> X;
+                    fetch_piece<M>(X, pq, lane);
+                    merge_piece<M>(A, dirty, X, pq, lane);
                 }
-                PieceSrc<M> X;
-                fetch_piece<M>(X, pq, lane);
-                merge_piece<M>(A, dirty, X, pq, lane);
             }
+            {  // changed rows only; the others get an out-of-range offset and are dropped
+                const __amdgpu_buffer_rsrc_t rp =
+                    __builtin_amdgcn_make_buffer_rsrc(a.pool + pbase, 0, 256u * M, kBufFlags);
 #pragma unroll
-            for (int j = 0; j < M; j++)
-                if ((dirty >> j) & 1u) opages[(uint64_t)page * (64u * M) + 64u * j] = A[j];
+                for (int j = 0; j < M; j++)
+                    __builtin_amdgcn_raw_buffer_store_b32(A[j], rp, ((dirty >> j) & 1u) ? 4u * lane + 256u * j : kBufOOB,
+                                                          0, 0);
+            }
             const uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, A, c0, c1), cf)) ^ a.kconst;
             if (lane == 0) a.page_crcs[page] = crc;
             if (!more) break;
@@ -825,8 +866,8 @@ __global__ __launch_bounds__(kBlockThreads) void log_pages_kernel(LogLaunch a) {
             for (int j = 0; j < M; j++) A[j] = B[j];
             S0 = S1;
             p0 = p1;
-            h = hn;
-            page = npage;
+            page = page1;
+            h = h1;
         }
     }
 }
@@ -982,6 +1023,12 @@ hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s) {
 hipError_t launch_log_expand(const LogLaunch& a, hipStream_t s) {
     if (a.n_updates == 0) return hipSuccess;
     hipLaunchKernelGGL(log_expand_kernel, dim3((uint32_t)((a.n_updates + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_log_heads(const LogLaunch& a, hipStream_t s) {
+    if (a.n_keys == 0) return hipSuccess;
+    hipLaunchKernelGGL(log_heads_kernel, dim3((uint32_t)((a.n_keys + 1023) / 1024)), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 

@@ -17,6 +17,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "../../include/curve_crc.h"
 #include "chunkserver_host.h"
 
@@ -232,6 +234,73 @@ void ScanCopysetMaps() {  // ScanJobProcess + OnApply over chunk files
     EXPECT(ScanCopyset(o, 1, 9, 3u << 18, 0, &maps) == -1);  // scanSize must divide chunkSize
 }
 
+void PoolScanShardRccl() {  // one rank's shard, native RCCL comm (world 1)
+    const uint64_t n = 6;
+    const uint32_t chunk = 1u << 20, meta = 4096, scan = 256u << 10;
+    const uint64_t ids[n] = {3, 1, 12, 7, 40, 2};
+    const uint32_t group[n] = {0, 1, 0, 1, 0, 1};
+    std::mt19937_64 rng(21);
+    std::string data(n * chunk, '\0'), metas(n * meta, '\0');
+    for (auto& c : data) c = (char)(rng() & 0xFF);
+    for (uint64_t i = 0; i < n; i++) metas.replace(i * meta, meta, MetaPage(ids[i]));
+    // copyset chain geometry: files in std::sort name order, bytes after each file
+    std::vector<uint64_t> after(n, 0);
+    for (uint64_t i = 0; i < n; i++)
+        for (uint64_t k = 0; k < n; k++)
+            if (group[k] == group[i] && ChunkFileName(ids[k]) > ChunkFileName(ids[i])) after[i] += chunk + meta;
+    void *d_data, *d_meta, *d_after, *d_mult, *d_group, *d_pc, *d_mc, *d_sc, *d_fc, *d_dig;
+    EXPECT(hipMalloc(&d_data, data.size()) == hipSuccess && hipMalloc(&d_meta, metas.size()) == hipSuccess);
+    EXPECT(hipMalloc(&d_after, n * 8) == hipSuccess && hipMalloc(&d_mult, n * 4) == hipSuccess &&
+           hipMalloc(&d_group, n * 4) == hipSuccess);
+    EXPECT(hipMalloc(&d_pc, n * chunk / 1024) == hipSuccess && hipMalloc(&d_mc, n * 4) == hipSuccess &&
+           hipMalloc(&d_sc, n * 16) == hipSuccess && hipMalloc(&d_fc, n * 4) == hipSuccess &&
+           hipMalloc(&d_dig, 8) == hipSuccess);
+    EXPECT(hipMemcpy(d_data, data.data(), data.size(), hipMemcpyHostToDevice) == hipSuccess);
+    EXPECT(hipMemcpy(d_meta, metas.data(), metas.size(), hipMemcpyHostToDevice) == hipSuccess);
+    EXPECT(hipMemcpy(d_after, after.data(), n * 8, hipMemcpyHostToDevice) == hipSuccess);
+    EXPECT(hipMemcpy(d_group, group, n * 4, hipMemcpyHostToDevice) == hipSuccess);
+    EXPECT(cc_xpow8_dev((const uint64_t*)d_after, n, (uint32_t*)d_mult, nullptr) == CC_OK);
+    char id[CC_COMM_ID_BYTES];
+    cc_comm* comm = nullptr;
+    EXPECT(cc_comm_unique_id(id, sizeof id) == CC_OK);
+    EXPECT(cc_comm_init(&comm, 1, 0, id, sizeof id) == CC_OK && cc_comm_size(comm) == 1);
+    cc_pool_shard s = {};
+    s.d_data = d_data;
+    s.d_meta = d_meta;
+    s.n_chunks = n;
+    s.chunk_bytes = chunk;
+    s.meta_bytes = meta;
+    s.page_bytes = 4096;
+    s.slice_bytes = scan;
+    s.d_after_mult = (const uint32_t*)d_mult;
+    s.d_group = (const uint32_t*)d_group;
+    s.n_groups = 2;
+    s.d_page_crcs = (uint32_t*)d_pc;
+    s.d_meta_crcs = (uint32_t*)d_mc;
+    s.d_slice_crcs = (uint32_t*)d_sc;
+    s.d_file_crcs = (uint32_t*)d_fc;
+    s.d_digest = (uint32_t*)d_dig;
+    EXPECT(cc_pool_scan_dev(&s, comm, nullptr) == CC_OK);
+    EXPECT(hipDeviceSynchronize() == hipSuccess);
+    uint32_t dig[2], sl[n * 4];
+    EXPECT(hipMemcpy(dig, d_dig, 8, hipMemcpyDeviceToHost) == hipSuccess);
+    EXPECT(hipMemcpy(sl, d_sc, sizeof sl, hipMemcpyDeviceToHost) == hipSuccess);
+    for (uint32_t g = 0; g < 2; g++) {  // CopysetNode::GetHash: sorted names, chained CRC from 0
+        std::vector<std::pair<std::string, uint64_t>> files;
+        for (uint64_t i = 0; i < n; i++)
+            if (group[i] == g) files.emplace_back(ChunkFileName(ids[i]), i);
+        std::sort(files.begin(), files.end());
+        uint32_t want = 0;
+        for (auto& f : files)
+            want = Oracle(metas.substr(f.second * meta, meta) + data.substr(f.second * chunk, chunk), want);
+        EXPECT(dig[g] == want);
+    }
+    for (uint64_t i = 0; i < n; i++)
+        for (uint32_t k = 0; k < 4; k++) EXPECT(sl[i * 4 + k] == Oracle(data.substr(i * chunk + k * scan, scan)));
+    EXPECT(cc_comm_destroy(comm) == CC_OK);
+    for (void* p : {d_data, d_meta, d_after, d_mult, d_group, d_pc, d_mc, d_sc, d_fc, d_dig}) EXPECT(hipFree(p) == hipSuccess);
+}
+
 struct Case {
     const char* name;
     bool gpu;
@@ -264,6 +333,7 @@ int main(int argc, char** argv) {
         {"CopysetHashOneChunk", true, CopysetHashOneChunk},
         {"CopysetHashMixed", true, CopysetHashMixed},
         {"ScanCopysetMaps", true, ScanCopysetMaps},
+        {"PoolScanShardRccl", true, PoolScanShardRccl},
     };
     int ran = 0, skipped = 0, failed_cases = 0;
     for (const Case& c : cases) {

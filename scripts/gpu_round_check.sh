@@ -1,7 +1,7 @@
 # quick GPU check used during development: targeted tests + write-log profile
 mkdir -p gpurun_out
 R=$(pwd)
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread -k "beyond_4gib or partial or write_log" > gpurun_out/t3.log 2>&1 || { echo TESTFAIL; tail -40 gpurun_out/t3.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_host_cpp.py tests/test_pool_native.py -m gpu -x -v --timeout 120 --timeout-method thread -k "beyond_4gib or partial or write_log or host_layer or pool" > gpurun_out/t3.log 2>&1 || { echo TESTFAIL; tail -40 gpurun_out/t3.log; exit 1; }
 tail -2 gpurun_out/t3.log
 cd /tmp && export TMPDIR=/tmp
 rm -rf $R/gpurun_out/prof_log
