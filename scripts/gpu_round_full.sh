@@ -1,0 +1,17 @@
+# Round evidence in one GPU call: every -m gpu test, the default bench line,
+# a rocprofv3 kernel-trace/stats profile of the bench, the write-log profile.
+# Each GPU step has its own time limit; the first failure ends the script.
+set -u
+R=$(pwd)
+TAG=${1:-r01}
+mkdir -p $R/gpurun_out
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $R/gpurun_out/gpu_tests_$TAG.log 2>&1 || { echo TESTFAIL; tail -30 $R/gpurun_out/gpu_tests_$TAG.log; exit 1; }
+tail -1 $R/gpurun_out/gpu_tests_$TAG.log
+timeout -k 10 400 python -u bench.py > $R/gpurun_out/bench_$TAG.log 2>&1 || { echo BENCHFAIL; tail -30 $R/gpurun_out/bench_$TAG.log; exit 1; }
+tail -1 $R/gpurun_out/bench_$TAG.log > $R/gpurun_out/bench_$TAG.json
+bash $R/scripts/gpu_profile.sh $TAG 20 || { echo PROFFAIL; exit 1; }
+cd /tmp && export TMPDIR=/tmp
+rm -rf $R/gpurun_out/prof_log_$TAG
+timeout -k 10 150 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_log_$TAG -o run --output-format csv -- python3 $R/scripts/prof_log.py > $R/gpurun_out/prof_log_$TAG.log 2>&1 || { echo LOGPROFFAIL; exit 1; }
+grep "ms per" $R/gpurun_out/prof_log_$TAG.log
+echo done

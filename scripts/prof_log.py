@@ -15,6 +15,7 @@ p = argparse.ArgumentParser()
 p.add_argument("--gib", type=int, default=16)
 p.add_argument("--updates", type=int, default=65536)
 p.add_argument("--reps", type=int, default=5)
+p.add_argument("--align", type=int, default=1, help="round dst/src offsets and lengths down to this")
 a = p.parse_args()
 dev = torch.device("cuda", 0)
 pool = torch.empty(a.gib << 30, dtype=torch.uint8, device=dev).random_(0, 256)
@@ -24,8 +25,9 @@ src = torch.empty(U * 4096, dtype=torch.uint8, device=dev).random_(0, 256)
 rng = np.random.default_rng(1)
 logs = []
 for _ in range(a.reps + 1):
-    rec = C.log_records(rng.integers(0, pool.numel() - 4096, U), rng.integers(0, U * 4096 - 4096, U),
-                        rng.integers(512, 4097, U))
+    al = a.align
+    rec = C.log_records(rng.integers(0, pool.numel() - 4096, U) // al * al,
+                        rng.integers(0, U * 4096 - 4096, U) // al * al, rng.integers(512, 4097, U) // al * al)
     logs.append(torch.from_numpy(rec.view(np.uint8)).to(dev))
 s = torch.cuda.current_stream()
 ms = []
