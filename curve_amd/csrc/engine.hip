@@ -705,7 +705,7 @@ int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, con
     while (end_bit < 32 && (1ull << end_bit) < n_pages) end_bit++;
     if (end_bit < 32) end_bit++;
     // at most n_keys page runs: a wave per run up to one 8-wave block per CU
-    const uint64_t blocks = (nk + kWavesPerBlock - 1) / kWavesPerBlock;
+    const uint64_t blocks = (nk + kLogWaves - 1) / kLogWaves;
     a.blocks = (int)(blocks < (uint64_t)c->cus ? (blocks ? blocks : 1) : (uint64_t)c->cus);
     hipError_t e;
     if ((e = launch_log_expand(a, s)) != hipSuccess) return map_err(e);

@@ -90,6 +90,10 @@ hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s);
 // compacted; one wave per touched page (balanced over the grid) then applies
 // its pieces in registers, stores the changed rows and rehashes it.
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
+#ifndef CC_LOG_WAVES
+#define CC_LOG_WAVES 8  // waves per CU of the write-log page kernel (16 measured equal: HBM-bound)
+#endif
+constexpr int kLogWaves = CC_LOG_WAVES;
 struct LogLaunch {
     unsigned char* pool;
     uint64_t pool_bytes;

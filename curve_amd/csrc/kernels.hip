@@ -91,10 +91,11 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t r) {
            __builtin_amdgcn_readlane(r, 32) ^ __builtin_amdgcn_readlane(r, 48);
 }
 
+template <int THREADS = kBlockThreads>
 __device__ __forceinline__ void fill_lds(uint32_t* tab, const uint4* __restrict__ image) {
     uint4* t4 = reinterpret_cast<uint4*>(tab);
 #pragma unroll 2
-    for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += kBlockThreads) t4[i] = image[i];
+    for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += THREADS) t4[i] = image[i];
     __syncthreads();
 }
 
@@ -684,6 +685,24 @@ __device__ __forceinline__ void piece_edges(const Piece& p, uint32_t (&e)[2]) {
     e[1] = (dl != df && !fl) ? dl : 0xffffffffu;
 }
 
+// Row structure of a piece (wave-uniform).  Row j = page bytes [256j, 256j+256)
+// = dword l + 64j of every lane.  A piece is one contiguous byte range, so it
+// touches rows [row0, row1], wholly covers the rows in `whole` (a bit mask), and
+// only row0 / row1 can be partly covered.
+struct PieceRows {
+    uint32_t row0, row1, whole;
+};
+__device__ __forceinline__ PieceRows piece_rows(const Piece& p) {
+    PieceRows r;
+    r.row0 = p.rlo >> 8;
+    r.row1 = (p.rhi - 1) >> 8;
+    const uint32_t w0 = (p.rlo & 255u) ? r.row0 + 1 : r.row0;
+    const uint32_t w1 = (p.rhi & 255u) ? r.row1 : r.row1 + 1;  // <= 32
+    const uint32_t below1 = w1 >= 32 ? 0xFFFFFFFFu : (1u << w1) - 1u;
+    r.whole = w1 > w0 ? below1 & ~((1u << w0) - 1u) : 0u;
+    return r;
+}
+
 template <int M>
 __device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint32_t lane) {
     const uint32_t sh = (uint32_t)(uintptr_t)p.sp & 3u;  // the same for every dword of the piece
@@ -693,11 +712,15 @@ __device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint
     const __amdgpu_buffer_rsrc_t re =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(p.sp - sh), 0, 64u * 4u * M + 8u, kBufFlags);
     const uint32_t l4 = lane * 4u;
+    const PieceRows pr = piece_rows(p);
+    // per-lane whole-dword test only for the two boundary rows; every other
+    // row is uniformly all-or-nothing
+    const uint32_t b0 = l4 + 256u * pr.row0, b1 = l4 + 256u * pr.row1;
+    const bool f0 = b0 >= p.rlo && b0 + 4 <= p.rhi, f1 = b1 >= p.rlo && b1 + 4 <= p.rhi;
 #pragma unroll
     for (int j = 0; j < M; j++) {
-        const uint32_t b = l4 + 256u * j;
-        const bool full = b >= p.rlo && b + 4 <= p.rhi;
-        r.S[j] = __builtin_amdgcn_raw_buffer_load_b32(rw, full ? b : kBufOOB, 0, 0);
+        const bool full = ((pr.whole >> j) & 1u) || ((uint32_t)j == pr.row0 && f0) || ((uint32_t)j == pr.row1 && f1);
+        r.S[j] = __builtin_amdgcn_raw_buffer_load_b32(rw, (full ? l4 : kBufOOB) + 256u * j, 0, 0);
     }
     uint32_t e[2];
     piece_edges(p, e);
@@ -712,11 +735,33 @@ __device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint
     }
 }
 
-// A piece is one contiguous byte range, so each 256-byte row j of the page
-// (dwords l + 64j of all lanes) is uniformly outside it, wholly inside it (then
-// every lane just takes its source dword), or one of its <= 2 boundary rows:
-// only those run the per-lane byte-mask merge.  `dirty` (rows written) is
-// wave-uniform.
+// Whole rows: every lane takes its source dword (one v_cndmask per row on a
+// uniform mask, no branches).  The <= 2 boundary rows run the per-lane
+// byte-mask merge, addressed by a uniform row index (selects instead of a
+// branch per row: more instructions than branching on each unrolled row, but
+// 186 -> 139 VGPRs at 4 KiB pages and no spills at 8 KiB; the kernel is
+// HBM-bound either way, measured equal).  `dirty` (rows written) is uniform.
+template <int M>
+__device__ __forceinline__ void merge_row(uint32_t (&w)[M], const PieceSrc<M>& r, const Piece& p, uint32_t row,
+                                          uint32_t lane, const uint32_t (&e)[2], uint32_t v0, uint32_t v1) {
+    const uint32_t d = lane + 64u * row, b = 4 * d;
+    const bool covered = b + 4 > p.rlo && b < p.rhi;
+    const uint32_t k0 = p.rlo > b ? p.rlo - b : 0u;
+    const uint32_t k1 = p.rhi < b + 4 ? p.rhi - b : 4u;
+    uint32_t old = w[0], s = r.S[0];
+#pragma unroll
+    for (int j = 1; j < M; j++) {  // uniform row select
+        old = (uint32_t)j == row ? w[j] : old;
+        s = (uint32_t)j == row ? r.S[j] : s;
+    }
+    const uint32_t v = d == e[0] ? v0 : (d == e[1] ? v1 : s);
+    const uint32_t mhi = k1 == 4u ? 0xFFFFFFFFu : (1u << (8u * k1)) - 1u;
+    const uint32_t mask = covered ? mhi & ~((1u << (8u * k0)) - 1u) : 0u;
+    const uint32_t nv = (v & mask) | (old & ~mask);
+#pragma unroll
+    for (int j = 0; j < M; j++) w[j] = (uint32_t)j == row ? nv : w[j];
+}
+
 template <int M>
 __device__ __forceinline__ void merge_piece(uint32_t (&w)[M], uint32_t& dirty, const PieceSrc<M>& r, const Piece& p,
                                             uint32_t lane) {
@@ -725,25 +770,13 @@ __device__ __forceinline__ void merge_piece(uint32_t (&w)[M], uint32_t& dirty, c
     const uint32_t sh = (uint32_t)(uintptr_t)p.sp & 3u;
     const uint32_t v0 = sh ? __builtin_amdgcn_alignbyte(r.eb[0], r.ea[0], sh) : r.ea[0];
     const uint32_t v1 = sh ? __builtin_amdgcn_alignbyte(r.eb[1], r.ea[1], sh) : r.ea[1];
-    const uint32_t row0 = p.rlo >> 8, row1 = (p.rhi - 1) >> 8;  // first / last row touched (uniform)
-    const bool whole0 = (p.rlo & 255u) == 0, whole1 = (p.rhi & 255u) == 0;
+    const PieceRows pr = piece_rows(p);
 #pragma unroll
-    for (int j = 0; j < M; j++) {
-        if ((uint32_t)j < row0 || (uint32_t)j > row1) continue;  // uniform
-        dirty |= 1u << j;
-        if (((uint32_t)j > row0 || whole0) && ((uint32_t)j < row1 || whole1)) {  // whole row
-            w[j] = r.S[j];
-            continue;
-        }
-        const uint32_t d = lane + 64u * j, b = 4 * d;
-        if (b + 4 <= p.rlo || b >= p.rhi) continue;
-        const uint32_t k0 = p.rlo > b ? p.rlo - b : 0u;
-        const uint32_t k1 = p.rhi < b + 4 ? p.rhi - b : 4u;
-        const uint32_t v = d == e[0] ? v0 : (d == e[1] ? v1 : r.S[j]);
-        const uint32_t mhi = k1 == 4u ? 0xFFFFFFFFu : (1u << (8u * k1)) - 1u;
-        const uint32_t mask = mhi & ~((1u << (8u * k0)) - 1u);
-        w[j] = (v & mask) | (w[j] & ~mask);
-    }
+    for (int j = 0; j < M; j++) w[j] = ((pr.whole >> j) & 1u) ? r.S[j] : w[j];
+    if (!((pr.whole >> pr.row0) & 1u)) merge_row<M>(w, r, p, pr.row0, lane, e, v0, v1);
+    if (pr.row1 != pr.row0 && !((pr.whole >> pr.row1) & 1u)) merge_row<M>(w, r, p, pr.row1, lane, e, v0, v1);
+    const uint32_t top = pr.row1 >= 31 ? 0xFFFFFFFFu : (2u << pr.row1) - 1u;
+    dirty |= top & ~((1u << pr.row0) - 1u);
 }
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
@@ -787,10 +820,15 @@ __global__ __launch_bounds__(1024) void log_heads_kernel(LogLaunch a) {
 // pieces (overlapping / neighbouring writes: rare) reads them from the sorted
 // arrays in place, in write order.  Every page is owned by exactly one wave: no
 // write races, no flags, no atomics on the data.
+#if CC_LOG_WAVES == 16
+#define CC_LOG_ATTR __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 4)))
+#else
+#define CC_LOG_ATTR __launch_bounds__(64 * CC_LOG_WAVES)
+#endif
 template <int M>
-__global__ __launch_bounds__(kBlockThreads) void log_pages_kernel(LogLaunch a) {
+__global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
     __shared__ uint32_t tab[kLdsBytes / 4];
-    fill_lds(tab, static_cast<const uint4*>(a.image));
+    fill_lds<64 * kLogWaves>(tab, static_cast<const uint4*>(a.image));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t c0 = lane << 2 & 0x7Cu;
@@ -799,8 +837,8 @@ __global__ __launch_bounds__(kBlockThreads) void log_pages_kernel(LogLaunch a) {
     const uint32_t* pages = reinterpret_cast<const uint32_t*>(a.pool) + lane;
     const uint32_t pb = a.page_bytes;
     const uint32_t H = *a.head_count;
-    const uint32_t W = gridDim.x * kWavesPerBlock;
-    for (uint32_t base = blockIdx.x * kWavesPerBlock + wave; base < H; base += 64u * W) {
+    const uint32_t W = gridDim.x * kLogWaves;
+    for (uint32_t base = blockIdx.x * kLogWaves + wave; base < H; base += 64u * W) {
         // lane k <- head base + k*W (clamped loads: no branches around them)
         const uint64_t ih = (uint64_t)base + (uint64_t)lane * W;
         const bool hv = ih < H;
@@ -823,32 +861,29 @@ __global__ __launch_bounds__(kBlockThreads) void log_pages_kernel(LogLaunch a) {
             return piece_in_page((uint64_t)pg * pb, pb, readlane64(ddst, k), readlane64(dsrc, k),
                                  __builtin_amdgcn_readlane(dlen, k), a.src);
         };
-        uint32_t h = 0;
-        uint32_t page = __builtin_amdgcn_readlane(key, 0);
-        Piece p0 = head_piece(0, page);
-        load_page<M>(A, pages + (uint64_t)page * (64u * M));
-        fetch_piece<M>(S0, p0, lane);
-        for (;;) {
-            const bool more = h + 1 < cnt;
-            // page k+1 + its first piece's source bytes in flight (clamped to the
-            // last page: a harmless re-read, so every iteration issues the same
-            // loads and the vmcnt waits stay exact)
-            const uint32_t h1 = more ? h + 1 : h;
-            const uint32_t page1 = __builtin_amdgcn_readlane(key, h1);
-            const Piece p1 = head_piece(h1, page1);
-            load_page<M>(B, pages + (uint64_t)page1 * (64u * M));
-            fetch_piece<M>(S1, p1, lane);
-            const uint64_t pbase = (uint64_t)page * pb;
+        // one page step: merge + store + rehash page `pg` from (X, SX, px) while
+        // the loads of the next page go into (Y, SY); false after the last page
+        auto step = [&](uint32_t (&X)[M], PieceSrc<M>& SX, const Piece& px, uint32_t pg, uint32_t hh,
+                        uint32_t (&Y)[M], PieceSrc<M>& SY, Piece& py, uint32_t& pgy) {
+            const bool more = hh + 1 < cnt;
+            // next page + its first piece's source bytes in flight (clamped to the
+            // last page: a harmless re-read, so every step issues the same loads
+            // and the vmcnt waits stay exact)
+            const uint32_t h1 = more ? hh + 1 : hh;
+            pgy = __builtin_amdgcn_readlane(key, h1);
+            py = head_piece(h1, pgy);
+            load_page<M>(Y, pages + (uint64_t)pgy * (64u * M));
+            fetch_piece<M>(SY, py, lane);
+            const uint64_t pbase = (uint64_t)pg * pb;
             uint32_t dirty = 0;
-            merge_piece<M>(A, dirty, S0, p0, lane);
-            if (!((singles >> h) & 1ull)) {  // further pieces of this page, in write order
-                for (uint32_t q = __builtin_amdgcn_readlane(pos, h) + 1; q < a.n_keys; q++) {
-                    if (a.skeys[q] != page) break;
+            merge_piece<M>(X, dirty, SX, px, lane);
+            if (!((singles >> hh) & 1ull)) {  // further pieces of this page, in write order
+                for (uint32_t q = __builtin_amdgcn_readlane(pos, hh) + 1; q < a.n_keys; q++) {
+                    if (a.skeys[q] != pg) break;
                     const UpdateDesc dq = a.upd[a.svals[q]];
                     const Piece pq = piece_in_page(pbase, pb, dq.dst, dq.src, dq.len, a.src);
-                    PieceSrc<M> X;
-                    fetch_piece<M>(X, pq, lane);
-                    merge_piece<M>(A, dirty, X, pq, lane);
+                    fetch_piece<M>(SX, pq, lane);  // SX is consumed: reuse its registers
+                    merge_piece<M>(X, dirty, SX, pq, lane);
                 }
             }
             {  // changed rows only; the others get an out-of-range offset and are dropped
@@ -856,18 +891,22 @@ __global__ __launch_bounds__(kBlockThreads) void log_pages_kernel(LogLaunch a) {
                     __builtin_amdgcn_make_buffer_rsrc(a.pool + pbase, 0, 256u * M, kBufFlags);
 #pragma unroll
                 for (int j = 0; j < M; j++)
-                    __builtin_amdgcn_raw_buffer_store_b32(A[j], rp, ((dirty >> j) & 1u) ? 4u * lane + 256u * j : kBufOOB,
+                    __builtin_amdgcn_raw_buffer_store_b32(X[j], rp, (((dirty >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j,
                                                           0, 0);
             }
-            const uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, A, c0, c1), cf)) ^ a.kconst;
-            if (lane == 0) a.page_crcs[page] = crc;
-            if (!more) break;
-#pragma unroll
-            for (int j = 0; j < M; j++) A[j] = B[j];
-            S0 = S1;
-            p0 = p1;
-            page = page1;
-            h = h1;
+            const uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
+            if (lane == 0) a.page_crcs[pg] = crc;
+            return more;
+        };
+        // the two register sets alternate (no copies): page k in one while page
+        // k+1's loads land in the other
+        uint32_t pgA = __builtin_amdgcn_readlane(key, 0), pgB = pgA;
+        Piece pA = head_piece(0, pgA), pB = pA;
+        load_page<M>(A, pages + (uint64_t)pgA * (64u * M));
+        fetch_piece<M>(S0, pA, lane);
+        for (uint32_t h = 0;; h += 2) {
+            if (!step(A, S0, pA, pgA, h, B, S1, pB, pgB)) break;
+            if (!step(B, S1, pB, pgB, h + 1, A, S0, pA, pgA)) break;
         }
     }
 }
@@ -1035,7 +1074,7 @@ hipError_t launch_log_heads(const LogLaunch& a, hipStream_t s) {
 hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s) {
     if (a.n_keys == 0) return hipSuccess;
 #define CC_GCASE(MM) \
-    case MM: hipLaunchKernelGGL((log_pages_kernel<MM>), dim3(a.blocks), dim3(kBlockThreads), 0, s, a); break;
+    case MM: hipLaunchKernelGGL((log_pages_kernel<MM>), dim3(a.blocks), dim3(64 * kLogWaves), 0, s, a); break;
     switch (a.page_bytes / kWaveBytes) {
         CC_GCASE(1)
         CC_GCASE(2)

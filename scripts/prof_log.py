@@ -15,8 +15,12 @@ p = argparse.ArgumentParser()
 p.add_argument("--gib", type=int, default=16)
 p.add_argument("--updates", type=int, default=65536)
 p.add_argument("--reps", type=int, default=5)
+p.add_argument("--lib", default=None, help="libcurvecrc variant to load instead of the in-tree one")
 p.add_argument("--align", type=int, default=1, help="round dst/src offsets and lengths down to this")
 a = p.parse_args()
+if a.lib:
+    from curve_amd import _lib
+    _lib.LIB_PATH = os.path.abspath(a.lib)
 dev = torch.device("cuda", 0)
 pool = torch.empty(a.gib << 30, dtype=torch.uint8, device=dev).random_(0, 256)
 crcs = C.page_crc(pool, 4096)
@@ -39,4 +43,6 @@ for k, d_log in enumerate(logs):
     torch.cuda.synchronize()
     if k:
         ms.append(e0.elapsed_time(e1))
-print("apply_log ms per batch:", [round(x, 4) for x in ms])
+ok = bool(torch.equal(crcs, C.page_crc(pool, 4096)))  # page CRCs consistent with the final bytes
+print("apply_log ms per batch:", [round(x, 4) for x in ms], "median", round(sorted(ms)[len(ms) // 2], 4),
+      "crcs_consistent", ok)
