@@ -62,15 +62,23 @@ class ChunkFileMetaPage:
     @classmethod
     def decode(cls, buf: bytes) -> Tuple[int, Optional["ChunkFileMetaPage"]]:
         """(CSErrorCode, metapage) like ChunkFileMetaPage::decode."""
+        if len(buf) < 29:
+            return CSErrorCode.CrcCheckError, None
         version, sn, csn, loc_size = struct.unpack_from("<BQQQ", buf, 0)
         n = 25
         m = cls(version, sn, csn)
         if loc_size > 0:
+            # lengths that overrun the page cannot carry a valid CRC (the
+            # reference would read past its buffer here)
+            if loc_size > len(buf) - n - 8:
+                return CSErrorCode.CrcCheckError, None
             m.location = bytes(buf[n:n + loc_size])
             n += loc_size
             (m.bitmap_bits,) = struct.unpack_from("<I", buf, n)
             n += 4
             nb = (m.bitmap_bits + 7) >> 3
+            if nb > len(buf) - n - 4:
+                return CSErrorCode.CrcCheckError, None
             m.bitmap = bytes(buf[n:n + nb])
             n += nb
         (rec,) = struct.unpack_from("<I", buf, n)

@@ -101,7 +101,8 @@ void ChunkFileMetaPage::encode(char* buf) const {
     memcpy(buf + len, &crc, sizeof(crc));
 }
 
-CSErrorCode ChunkFileMetaPage::decode(const char* buf) {
+CSErrorCode ChunkFileMetaPage::decode(const char* buf, size_t size) {
+    if (size < 25 + sizeof(uint32_t)) return CrcCheckError;
     size_t len = 0;
     auto get = [&](void* p, size_t n) {
         memcpy(p, buf + len, n);
@@ -116,10 +117,16 @@ CSErrorCode ChunkFileMetaPage::decode(const char* buf) {
     bitmap.clear();
     bitmapBits = 0;
     if (loc_size > 0) {
+        // a header that claims more bytes than the page holds cannot carry a
+        // valid CRC: report it as one instead of reading past the page (the
+        // reference trusts loc_size / bitmap bits here)
+        if (loc_size > size - len || size - len - loc_size < sizeof(bitmapBits) + sizeof(uint32_t))
+            return CrcCheckError;
         location.assign(buf + len, loc_size);
         len += loc_size;
         get(&bitmapBits, sizeof(bitmapBits));
-        const size_t nb = (bitmapBits + 7) >> 3;
+        const size_t nb = ((size_t)bitmapBits + 7) >> 3;
+        if (nb > size - len - sizeof(uint32_t)) return CrcCheckError;
         bitmap.assign(buf + len, buf + len + nb);
         len += nb;
     }

@@ -60,7 +60,9 @@ struct ChunkFileMetaPage {
     // metapage long); layout as the reference: version u8 | sn u64 |
     // correctedSn u64 | loc_size size_t [| location | bits u32 | bitmap] | crc u32
     void encode(char* buf) const;
-    CSErrorCode decode(const char* buf);
+    // size = bytes readable at buf (the metapage); a header that does not fit
+    // in it is CrcCheckError
+    CSErrorCode decode(const char* buf, size_t size = 4096);
 };
 
 struct DataStoreOptions {

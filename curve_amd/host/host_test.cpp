@@ -100,6 +100,17 @@ void MetaPageEncodeDecode() {
     ChunkFileMetaPage back;
     EXPECT(back.decode(cp.data()) == Success && back.location == clone.location && back.bitmapBits == 20 &&
            back.bitmap == clone.bitmap);
+    // corrupt lengths: a loc_size or bitmap that overruns the page is a CRC
+    // error, never a read past the buffer
+    std::string huge = cp;
+    const uint64_t big = 1ull << 40;
+    memcpy(&huge[17], &big, 8);
+    EXPECT(back.decode(huge.data(), huge.size()) == CrcCheckError);
+    std::string bits = cp;
+    const uint32_t many = 0xFFFFFFFFu;
+    memcpy(&bits[25 + clone.location.size()], &many, 4);
+    EXPECT(back.decode(bits.data(), bits.size()) == CrcCheckError);
+    EXPECT(back.decode(cp.data(), 20) == CrcCheckError);  // shorter than a header
 }
 
 // ---- ScanManager::CompareMap (scan_manager_test.cpp shapes) -----------------

@@ -29,6 +29,15 @@ def test_metapage_clone_and_errors(oracle):
     assert CF.ChunkFileMetaPage.decode(bytes(page))[0] == CF.CSErrorCode.CrcCheckError
     bad = CF.ChunkFileMetaPage(version=3).encode()
     assert CF.ChunkFileMetaPage.decode(bad)[0] == CF.CSErrorCode.IncompatibleError
+    # lengths that overrun the page: CrcCheckError, never an exception / overread
+    good = bytearray(m.encode())
+    huge = bytearray(good)
+    huge[17:25] = struct.pack("<Q", 1 << 40)
+    assert CF.ChunkFileMetaPage.decode(bytes(huge))[0] == CF.CSErrorCode.CrcCheckError
+    bits = bytearray(good)
+    bits[25 + len(m.location):29 + len(m.location)] = struct.pack("<I", 0xFFFFFFFF)
+    assert CF.ChunkFileMetaPage.decode(bytes(bits))[0] == CF.CSErrorCode.CrcCheckError
+    assert CF.ChunkFileMetaPage.decode(bytes(good[:20]))[0] == CF.CSErrorCode.CrcCheckError
 
 
 def test_metapage_crc_is_the_residue_constant(oracle, golden):
