@@ -306,6 +306,49 @@ def test_large_pool_properties(dev, oracle):
     assert int(cnt[0]) == 0
 
 
+def test_write_log_full_size_config3(dev, oracle):
+    """BASELINE config 3 at full size: a 16 GiB pool (1024 chunks), 65,536 random
+    512 B-4 KiB writes in one log (unaligned, straddling, some overlapping).
+    Size-independent properties: every page CRC still verifies against the
+    final bytes (all 4M pages), and 300 sampled touched pages equal their host
+    rebuild -- the original page with every log entry touching it applied in
+    log order -- byte for byte, with the oracle's CRC."""
+    from curve_amd import crc as C
+    n_chunks, pb, U = 1024, 4096, 65536
+    pool = torch.empty(n_chunks << 24, dtype=torch.uint8, device=dev).random_(0, 256)
+    pcs = C.page_crc(pool, pb)
+    src = torch.empty(U * 4096, dtype=torch.uint8, device=dev).random_(0, 256)
+    rng = np.random.default_rng(0xC3)
+    lens = rng.integers(512, 4097, U).astype(np.uint64)
+    dst = rng.integers(0, pool.numel() - 4096, U).astype(np.uint64)
+    dst[:64] = np.minimum(dst[64:128] + rng.integers(0, 2048, 64).astype(np.uint64),
+                          pool.numel() - 4097)  # guaranteed overlaps
+    src_off = rng.integers(0, U * 4096 - 4096, U).astype(np.uint64)
+    p0, p1 = dst // pb, (dst + lens - 1) // pb
+    touched = np.unique(np.concatenate([p0, p1]))
+    sample = rng.choice(touched, 300, replace=False)
+    sample = np.unique(np.concatenate([sample, p0[:64]]))  # include overlapped pages
+    before = {int(p): pool[int(p) * pb:(int(p) + 1) * pb].cpu().numpy().copy() for p in sample}
+    C.apply_updates(pool, pcs, src, dst, src_off, lens, pb)
+    cnt = C.page_verify(pool, pcs, pb)
+    torch.cuda.synchronize()
+    assert int(cnt[0]) == 0  # every page's CRC matches its final bytes
+    src_h = src.cpu().numpy()
+    pcs_h = u32(pcs)
+    for p in sample:
+        p = int(p)
+        page = before[p]
+        lo, hi = p * pb, (p + 1) * pb
+        for i in np.flatnonzero((dst < hi) & (dst + lens > lo)):  # log order
+            a, b = max(int(dst[i]), lo), min(int(dst[i] + lens[i]), hi)
+            s = int(src_off[i]) + (a - int(dst[i]))
+            page[a - lo:b - lo] = src_h[s:s + (b - a)]
+        assert (pool[lo:hi].cpu().numpy() == page).all(), p
+        assert pcs_h[p] == oracle.crc32c(page.tobytes()), p
+    del pool, src, pcs
+    torch.cuda.empty_cache()
+
+
 def test_beyond_4gib_offsets(dev, oracle):
     """Maximum-size addressing: a 4.25 GiB buffer (byte offsets past 2^32):
     every page CRC, verify finding a page past 4 GiB, and ranges at offsets
