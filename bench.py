@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--e2e-gib", type=float, default=1.0, help="pinned host buffer for the e2e leg")
     p.add_argument("--updates", type=int, default=65536, help="config-3 updates per batch")
     p.add_argument("--update-batches", type=int, default=5)
+    p.add_argument("--reads", type=int, default=65536, help="verify-on-read leg: reads per batch (0 = skip)")
     p.add_argument("--stream-chunks", type=int, default=10000, help="config-4 stream leg (0 = skip)")
     p.add_argument("--file-chunks", type=int, default=128, help="datastore read-path leg (0 = skip)")
     p.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/traffic_*.json)")
@@ -253,6 +254,40 @@ def partial_write_leg(pool, args):
             "note": "alg bytes = 2*update bytes + 4100*touched pages; log + data resident in HBM"}
 
 
+def read_verify_leg(pool, args):
+    """Verify-on-read (the datastore read path, CSChunkFile::Read): batches of
+    `--reads` random client reads of 4 KiB-128 KiB at page-aligned offsets
+    (CheckRequestOffsetAndLength) over the resident pool; every touched page is
+    rehashed and compared with its stored CRC (cc_verify_reads_dev).  Reads and
+    CRC table resident in HBM; HIP events on the launch stream."""
+    from curve_amd import crc as C
+    dev = pool.data.device
+    n, pb = args.reads, args.page_bytes
+    flat = pool.data.view(-1)
+    n_pages = flat.numel() // pb
+    rng = np.random.default_rng(0xEAD)
+    stream = torch.cuda.current_stream()
+    ms, pages = [], 0
+    for it in range(4):
+        npg = rng.integers(1, 33, n)
+        first = rng.integers(0, n_pages - 32, n)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        bad, total = C.verify_reads(flat, pool.page_crcs, first * pb, npg * pb, pb)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        assert int(total.item()) == 0, "clean pool flagged"
+        if it:
+            ms.append(e0.elapsed_time(e1))
+            pages += int(npg.sum())
+    t = float(np.mean(ms))
+    per = pages / len(ms)
+    return {"reads_per_batch": n, "pages_per_batch": int(per), "ms_per_batch": round(t, 4),
+            "GiBps_verified": round(per * pb / GiB / (t * 1e-3), 1),
+            "alg_frac_of_hbm_peak": round(per * (pb + 4) / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "note": "one launch per batch; alg bytes = 4100 per touched page"}
+
+
 def load_traffic(args):
     path = args.traffic_json
     if path is None:
@@ -425,6 +460,8 @@ def main():
         out["digest_exchange"] = {"path": comm_note, "matches_torch_distributed": digest_check}
     if rank == 0 and world == 1 and args.updates:
         out["partial_write"] = partial_write_leg(pool, args)
+    if rank == 0 and world == 1 and args.reads:
+        out["read_verify"] = read_verify_leg(pool, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pool, args, rank)
     if rank == 0 and world == 1 and not args.no_e2e:

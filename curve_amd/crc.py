@@ -493,6 +493,35 @@ def apply_updates_batched(pool, page_crcs, src, dst_off, src_off, lens, page_byt
     return nb
 
 
+def verify_reads(pool, page_crcs, offsets, lengths, page_bytes: int = PAGE_SIZE, stream=None):
+    """cc_verify_reads_dev: verify-on-read for a batch of reads of the pool.
+    Returns (bad pages per read: int32 device tensor, -1 = read past the pool;
+    total bad pages: int64 device tensor [1]).  No host sync."""
+    import numpy as np
+    torch = _torch()
+    off = np.asarray(offsets, dtype=np.uint64)
+    ln = np.asarray(lengths, dtype=np.uint64)
+    if off.size != ln.size:
+        raise CurveCrcError(_lib.CC_EINVAL, "offsets/lengths size mismatch")
+    n = off.size
+    bad = torch.zeros(max(n, 1), dtype=torch.int32, device=pool.device)
+    total = torch.zeros(1, dtype=torch.int64, device=pool.device)
+    if n == 0:
+        return bad[:0], total
+    rng = torch.from_numpy(np.stack([off, ln], axis=1).reshape(-1).view(np.int64)).to(pool.device)
+    need = int(lib().cc_verify_reads_work_bytes(n))
+    work = torch.empty(need, dtype=torch.uint8, device=pool.device)
+    with torch.cuda.device(pool.device):
+        check(lib().cc_verify_reads_dev(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, _dev_ptr(rng, "reads"), n,
+                                        _dev_ptr(page_crcs, "page_crcs"), _dev_ptr(bad, "bad"),
+                                        _dev_ptr(total, "total"), _dev_ptr(work, "work"), need,
+                                        _stream_handle(stream)), "cc_verify_reads_dev")
+    if stream is not None:
+        for t in (rng, work):
+            t.record_stream(stream)
+    return bad, total
+
+
 def scan_files(paths, chunk_bytes: int = CHUNK_SIZE, meta_bytes: int = META_PAGE_SIZE,
                page_bytes: int = PAGE_SIZE, slice_bytes: int = SCAN_SIZE, io_threads: int = 8):
     """cc_scan_files: native pread + scan of chunk files.

@@ -716,6 +716,50 @@ int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, con
     return map_err(launch_log_pages(a, s));
 }
 
+uint64_t cc_verify_reads_work_bytes(uint64_t n_reads) {
+    if (n_reads == 0 || n_reads >= (1ull << 31)) return 0;
+    const size_t temp = scan_temp_bytes(n_reads);
+    if (!temp) return 0;
+    return 2 * align256(n_reads * 8) + align256(temp);
+}
+
+int cc_verify_reads_dev(const void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const cc_range* d_reads,
+                        uint64_t n_reads, const uint32_t* d_page_crcs, uint32_t* d_bad_per_read, uint64_t* d_bad_total,
+                        void* d_work, uint64_t work_bytes, void* stream) {
+    if (!log_page_ok(page_bytes)) return CC_EINVAL;
+    if (n_reads == 0) return CC_OK;
+    if (!d_pool || !d_reads || !d_page_crcs || !d_bad_per_read || !d_bad_total || !d_work) return CC_EINVAL;
+    if (pool_bytes % page_bytes || ((uintptr_t)d_pool & 3u)) return CC_EINVAL;
+    const uint64_t need = cc_verify_reads_work_bytes(n_reads);
+    if (need == 0 || work_bytes < need) return CC_EINVAL;
+    DevCtx* c = nullptr;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    unsigned char* w = static_cast<unsigned char*>(d_work);
+    ReadVerifyLaunch a = {};
+    a.pool = static_cast<const uint32_t*>(d_pool);
+    a.pool_bytes = pool_bytes;
+    a.page_bytes = page_bytes;
+    a.reads = reinterpret_cast<const RangeDesc*>(d_reads);
+    a.n_reads = n_reads;
+    a.counts = reinterpret_cast<uint64_t*>(w);
+    a.start = reinterpret_cast<uint64_t*>(w + align256(n_reads * 8));
+    void* temp = w + 2 * align256(n_reads * 8);
+    a.page_crcs = d_page_crcs;
+    a.bad_per_read = d_bad_per_read;
+    a.bad_total = reinterpret_cast<unsigned long long*>(d_bad_total);
+    a.image = c->image;
+    a.kconst = kconst_for(page_bytes);
+    a.blocks = c->cus;  // every wave takes an equal share of the (device-computed) page slots
+    hipError_t e;
+    if ((e = launch_read_counts(a, s)) != hipSuccess) return map_err(e);
+    if ((e = exclusive_scan_u64(temp, work_bytes - 2 * align256(n_reads * 8), a.counts, a.start, n_reads, s)) !=
+        hipSuccess)
+        return map_err(e);
+    return map_err(launch_read_verify(a, s));
+}
+
 // Streaming scan.  Each staging slot holds a batch of whole chunks (data and
 // metapages in separate device regions) plus the per-chunk results; a batch is
 // {H2D data+meta, page kernel over data, page kernel over metapages, fold to

@@ -125,6 +125,31 @@ hipError_t log_sort(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint
 struct RangeDesc {
     uint64_t off, len;
 };
+
+// Verify-on-read for a batch of reads (cc_verify_reads_dev): every page a read
+// touches is a "slot"; slots of read i start at start[i] (exclusive scan of the
+// per-read page counts); each wave rehashes the reads starting in an equal
+// share of the slots.
+struct ReadVerifyLaunch {
+    const uint32_t* pool;
+    uint64_t pool_bytes;
+    uint32_t page_bytes;
+    const RangeDesc* reads;
+    uint64_t n_reads;
+    uint64_t* counts;           // [n_reads] pages per read
+    uint64_t* start;            // [n_reads] exclusive scan of counts
+    const uint32_t* page_crcs;  // stored CRC per pool page
+    uint32_t* bad_per_read;     // [n_reads] += mismatching pages; UINT32_MAX for a read beyond the pool
+    unsigned long long* bad_total;
+    const void* image;
+    uint32_t kconst;
+    int blocks;
+};
+hipError_t launch_read_counts(const ReadVerifyLaunch& a, hipStream_t s);
+size_t scan_temp_bytes(uint64_t n);
+hipError_t exclusive_scan_u64(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
+                              hipStream_t s);
+hipError_t launch_read_verify(const ReadVerifyLaunch& a, hipStream_t s);
 // CRC32C (butil Value) of arbitrary byte ranges of one device buffer.
 hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, const void* image,
                             uint32_t* out, int blocks, hipStream_t s);

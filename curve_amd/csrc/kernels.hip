@@ -911,6 +911,124 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Verify-on-read for a batch of datastore reads (cc_verify_reads_dev)
+// ---------------------------------------------------------------------------
+// Pages each read touches (a read past the pool touches none and is marked).
+__global__ void read_counts_kernel(ReadVerifyLaunch a) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n_reads) return;
+    const RangeDesc r = a.reads[i];
+    uint64_t c = 0;
+    if (r.off >= a.pool_bytes || r.len > a.pool_bytes - r.off) {
+        if (r.len) a.bad_per_read[i] = 0xFFFFFFFFu;
+    } else if (r.len) {
+        c = (r.off + r.len - 1) / a.page_bytes - r.off / a.page_bytes + 1;
+    }
+    a.counts[i] = c;
+}
+
+// Every page a read touches is one slot; read i owns slots start[i] ..
+// start[i] + counts[i] - 1 (start = exclusive scan of counts).  Wave w owns
+// the reads whose first slot lies in [T*w/W, T*(w+1)/W): balanced to within
+// one read whatever the read sizes, found with two 64-ary searches over
+// start[] (lanes probe 64 entries per round trip).  It takes its reads 64 at a
+// time (lane j <- one read: first page, page count) and lays their pages out
+// as one stream with a wave prefix sum: page k of the stream belongs to the
+// first lane whose running count exceeds k (a ballot), so the stream is walked
+// with uniform scalar math only -- no loads in the per-page path -- hashed with
+// the next two pages' loads in flight (three register sets rotating).  The
+// stored CRCs come in with VECTOR loads (an opaque zero in the address) so
+// they never share lgkmcnt with the chain's LDS lookups.  A mismatch is
+// counted on its read (rare: atomics).
+template <int M>
+__global__ __launch_bounds__(kBlockThreads) void read_verify_kernel(ReadVerifyLaunch a) {
+    __shared__ uint32_t tab[kLdsBytes / 4];
+    fill_lds(tab, static_cast<const uint4*>(a.image));
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t c0 = lane << 2 & 0x7Cu;
+    const uint32_t c1 = c0 | 0x10000u;
+    const uint32_t cf = kFinBase + (lane << 2);
+    const uint32_t* pages = a.pool + lane;
+    const uint64_t n = a.n_reads;
+    const uint64_t T = a.start[n - 1] + a.counts[n - 1];
+    const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+    uint32_t vz = 0;
+    asm volatile("" : "+v"(vz));  // opaque zero: keeps uniform-address loads on the vector path
+    // first read whose first slot is >= target (n if none): 64-ary search
+    auto lower_bound = [&](uint64_t target) -> uint64_t {
+        uint64_t lo = 0, hi = n;  // answer in [lo, hi]
+        while (lo < hi) {
+            const uint64_t step = (hi - lo + 63) / 64;
+            const uint64_t idx = lo + (uint64_t)lane * step;
+            const bool probe = idx < hi;
+            const uint64_t st = a.start[(probe ? idx : lo) + vz];
+            const uint64_t lt = __ballot(probe && st < target);  // a prefix of the probes
+            if (!lt) {
+                hi = lo;
+                break;
+            }
+            const uint32_t j = 63u - (uint32_t)__builtin_clzll(lt);
+            lo = lo + (uint64_t)j * step + 1;
+            const uint64_t nh = lo - 1 + step;
+            hi = nh < hi ? nh : hi;
+        }
+        return lo;
+    };
+    const uint64_t rb = lower_bound(T * w / W), re = lower_bound(T * (w + 1) / W);
+    auto stored_crc = [&](uint64_t g) { return a.page_crcs[g + vz]; };
+    for (uint64_t base = rb; base < re; base += 64) {
+        const uint64_t ri = base + lane;
+        const bool valid = ri < re;
+        const RangeDesc r = a.reads[(valid ? ri : base) + vz];
+        const uint32_t cnt = valid ? (uint32_t)a.counts[ri] : 0u;  // 0 also for reads past the pool
+        const uint64_t p0 = r.off / a.page_bytes;
+        uint32_t cum = cnt;  // inclusive prefix sum over the lanes
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(cum, d, 64);
+            if (lane >= (uint32_t)d) cum += o;
+        }
+        const uint32_t P = __builtin_amdgcn_readlane(cum, 63);
+        if (P == 0) continue;
+        auto page_at = [&](uint32_t k, uint32_t& owner) -> uint64_t {
+            owner = (uint32_t)__builtin_ctzll(__ballot(cum > k));
+            const uint32_t before = owner ? (uint32_t)__builtin_amdgcn_readlane(cum, owner - 1) : 0u;
+            const uint64_t first = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(p0 >> 32), owner) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((uint32_t)p0, owner);
+            return first + (k - before);
+        };
+        uint32_t A[M], B[M], Cq[M];
+        uint32_t oA, oB, oC;
+        uint64_t gA = page_at(0, oA), gB = page_at(P > 1 ? 1 : 0, oB), gC = gB;
+        oC = oB;
+        uint32_t sA = stored_crc(gA), sB = stored_crc(gB), sC = sB;
+        load_page<M>(A, pages + gA * (64u * M));
+        load_page<M>(B, pages + gB * (64u * M));
+        // hash X (page k: stored CRC sx, owner lane ox); page k+2's loads go into Y
+        auto step = [&](uint32_t (&X)[M], uint32_t sx, uint32_t ox, uint32_t k, uint32_t (&Y)[M], uint64_t& gy,
+                        uint32_t& sy, uint32_t& oy) {
+            const bool more = k + 1 < P;
+            gy = page_at(k + 2 < P ? k + 2 : P - 1, oy);  // clamped: same loads every step
+            sy = stored_crc(gy);
+            load_page<M>(Y, pages + gy * (64u * M));
+            const uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
+            if (crc != sx && lane == 0) {
+                atomicAdd(a.bad_per_read + base + ox, 1u);
+                atomicAdd(a.bad_total, 1ull);
+            }
+            return more;
+        };
+        for (uint32_t k = 0;; k += 3) {
+            if (!step(A, sA, oA, k, Cq, gC, sC, oC)) break;
+            if (!step(B, sB, oB, k + 1, A, gA, sA, oA)) break;
+            if (!step(Cq, sC, oC, k + 2, B, gB, sB, oB)) break;
+        }
+    }
+}
+
 __global__ void combine_kernel(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t m,
                                uint64_t n, uint32_t* __restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1085,6 +1203,29 @@ hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s) {
         default: return hipErrorInvalidValue;
     }
 #undef CC_GCASE
+    return hipGetLastError();
+}
+
+hipError_t launch_read_counts(const ReadVerifyLaunch& a, hipStream_t s) {
+    if (a.n_reads == 0) return hipSuccess;
+    hipLaunchKernelGGL(read_counts_kernel, dim3((uint32_t)((a.n_reads + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_read_verify(const ReadVerifyLaunch& a, hipStream_t s) {
+    if (a.n_reads == 0) return hipSuccess;
+#define CC_RCASE(MM) \
+    case MM: hipLaunchKernelGGL((read_verify_kernel<MM>), dim3(a.blocks), dim3(kBlockThreads), 0, s, a); break;
+    switch (a.page_bytes / kWaveBytes) {
+        CC_RCASE(1)
+        CC_RCASE(2)
+        CC_RCASE(4)
+        CC_RCASE(8)
+        CC_RCASE(16)
+        CC_RCASE(32)
+        default: return hipErrorInvalidValue;
+    }
+#undef CC_RCASE
     return hipGetLastError();
 }
 

@@ -1,7 +1,8 @@
-// curve_amd/csrc/log_sort.hip -- the one library primitive of the write-log
-// path: a stable device radix sort of (page, update index) pieces by page
-// (hipCUB over rocPRIM).  Kept in its own translation unit: the template
-// instantiation is heavy and nothing else here needs it.
+// curve_amd/csrc/log_sort.hip -- the library primitives of the batched paths
+// (hipCUB over rocPRIM): the stable device radix sort of the write log's
+// (page, update index) pieces, and the exclusive scan that lays out the page
+// slots of a batch of reads.  Kept in their own translation unit: the template
+// instantiations are heavy and nothing else here needs them.
 //
 // Stability is what carries the raft-log order (op_request.cpp:429-481 applies
 // writes in log order): pieces are generated in write order, so after a STABLE
@@ -30,6 +31,20 @@ hipError_t log_sort(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint
     size_t bytes = temp_bytes;
     return hipcub::DeviceRadixSort::SortPairs(temp, bytes, keys_in, keys_out, vals_in, vals_out, (int)n, 0, end_bit,
                                               s);
+}
+
+size_t scan_temp_bytes(uint64_t n) {
+    size_t bytes = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, static_cast<const uint64_t*>(nullptr),
+                                         static_cast<uint64_t*>(nullptr), (int)n) != hipSuccess)
+        return 0;
+    return bytes;
+}
+
+hipError_t exclusive_scan_u64(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
+                              hipStream_t s) {
+    size_t bytes = temp_bytes;
+    return hipcub::DeviceScan::ExclusiveSum(temp, bytes, in, out, (int)n, s);
 }
 
 }  // namespace cc

@@ -232,6 +232,21 @@ int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, con
                      const cc_update* d_log, uint64_t n_updates, uint32_t max_len, uint32_t* d_page_crcs,
                      void* d_work, uint64_t work_bytes, void* stream);
 
+/* Verify-on-read for a batch of datastore reads (the read path of
+ * CSChunkFile::Read, chunkserver_chunkfile.cpp:497-536, which today returns the
+ * bytes unchecked): every page that read i = d_reads[i] (pool byte range, any
+ * offset/length; a partly covered page is verified whole) touches is rehashed
+ * and compared with its stored CRC in d_page_crcs.  d_bad_per_read[i] += the
+ * mismatching pages of read i (caller zeroes it; UINT32_MAX marks a read that
+ * runs past the pool); *d_bad_total += all mismatches.  Every touched page is
+ * one work slot and the slots are split evenly over the device, so reads of
+ * any size mix freely.  page_bytes = 256 * 2^k (k = 0..5).
+ * d_work >= cc_verify_reads_work_bytes(n_reads) bytes of device scratch. */
+uint64_t cc_verify_reads_work_bytes(uint64_t n_reads);
+int cc_verify_reads_dev(const void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const cc_range* d_reads,
+                        uint64_t n_reads, const uint32_t* d_page_crcs, uint32_t* d_bad_per_read,
+                        uint64_t* d_bad_total, void* d_work, uint64_t work_bytes, void* stream);
+
 /* One chunk file as the datastore holds it: metapage + data
  * (file = metapage || data, chunkserver_chunkfile.cpp:497-536). */
 typedef struct cc_chunk_src {

@@ -1,6 +1,6 @@
 # write-log correctness (GPU tests) + A/B of kernel variants (build/variants/libcurvecrc_*.so)
 set -u
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "beyond_4gib or partial or write_log or full_size" > gpurun_out/tv.log 2>&1 || { echo TESTFAIL; tail -30 gpurun_out/tv.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "beyond_4gib or partial or write_log or full_size or verify_reads" > gpurun_out/tv.log 2>&1 || { echo TESTFAIL; tail -30 gpurun_out/tv.log; exit 1; }
 tail -1 gpurun_out/tv.log
 for lib in curve_amd/libcurvecrc.so; do
   echo "$lib"

@@ -349,6 +349,43 @@ def test_write_log_full_size_config3(dev, oracle):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("page_bytes", [4096, 512])
+def test_verify_reads_batch(dev, oracle, page_bytes):
+    """cc_verify_reads_dev: a batch of reads of every shape (page-aligned as
+    CheckRequestOffsetAndLength demands, 512 B blocks, unaligned, empty, one
+    spanning the whole pool, one past the end) against a pool with corrupted
+    pages: each read reports exactly the corrupted pages it touches."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(page_bytes)
+    n_pages = 3000
+    host = rng.integers(0, 256, n_pages * page_bytes, dtype=np.uint8)
+    stored = to_dev(oracle.page_crcs(host, page_bytes).view(np.int32), dev)
+    pool = to_dev(host, dev)
+    bad_pages = {0, 7, 64, 65, 1999, n_pages - 1}
+    for p in bad_pages:
+        pool[p * page_bytes + int(rng.integers(0, page_bytes))] ^= 0x10
+    total_bytes = n_pages * page_bytes
+    reads = [(0, page_bytes), (7 * page_bytes, 3 * page_bytes), (512, 4096), (100, 1), (5 * page_bytes, 0),
+             (63 * page_bytes + 17, 2 * page_bytes), (0, total_bytes), (total_bytes - 10, 10),
+             (total_bytes - 10, 11), (1500 * page_bytes, 400 * page_bytes)]
+    for _ in range(300):
+        o = int(rng.integers(0, total_bytes - 1))
+        reads.append((o, int(rng.integers(0, min(64 * page_bytes, total_bytes - o) + 1))))
+    off, ln = zip(*reads)
+    bad, total = C.verify_reads(pool, stored, off, ln, page_bytes)
+    got = bad.cpu().numpy()
+    want_total = 0
+    for i, (o, n) in enumerate(reads):
+        if o + n > total_bytes:
+            assert got[i] == -1, i
+            continue
+        touched = set(range(o // page_bytes, (o + n - 1) // page_bytes + 1)) if n else set()
+        want = len(touched & bad_pages)
+        want_total += want
+        assert got[i] == want, (i, o, n)
+    assert int(total.item()) == want_total
+
+
 def test_beyond_4gib_offsets(dev, oracle):
     """Maximum-size addressing: a 4.25 GiB buffer (byte offsets past 2^32):
     every page CRC, verify finding a page past 4 GiB, and ranges at offsets
