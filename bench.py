@@ -47,6 +47,7 @@ def parse():
     p.add_argument("--update-batches", type=int, default=5)
     p.add_argument("--reads", type=int, default=65536, help="verify-on-read leg: reads per batch (0 = skip)")
     p.add_argument("--stream-chunks", type=int, default=10000, help="config-4 stream leg (0 = skip)")
+    p.add_argument("--stream-chunks-per-rank", type=int, default=2000, help="N>1: streamed chunks per rank")
     p.add_argument("--file-chunks", type=int, default=128, help="datastore read-path leg (0 = skip)")
     p.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/traffic_*.json)")
     return p.parse_args()
@@ -160,6 +161,47 @@ def stream_leg(args):
     return {"chunks": n, "GiBps_e2e": round(n * (C.CHUNK_SIZE + C.META_PAGE_SIZE) / GiB / el, 2),
             "seconds": round(el, 3), "with_digest_seconds": round(el_all, 3), "copysets": lay.n_groups,
             "scan_maps": int(sc.size + mc.size), "source": "pinned host pool of 64 chunk files, re-referenced"}
+
+
+def stream_all_ranks_leg(args, rank, world, dev):
+    """Config 5 end to end: each rank streams `--stream-chunks-per-rank` chunk
+    files (a pinned pool of 64 distinct files, re-referenced) through
+    cc_scan_host on its own GPU, computes its copysets' digest partials from the
+    file CRCs and joins the digest exchange; aggregate = all ranks' bytes / the
+    slowest rank's time (barrier on both sides)."""
+    from curve_amd import crc as C
+    from curve_amd.pool import copyset_layout, reduce_digests
+    n = args.stream_chunks_per_rank
+    pool_n = 64
+    data = torch.empty((pool_n, C.CHUNK_SIZE), dtype=torch.uint8, pin_memory=True)
+    data.random_(0, 256)
+    meta = torch.zeros((pool_n, C.META_PAGE_SIZE), dtype=torch.uint8, pin_memory=True)
+    meta[:, 0] = 2
+    dn, mn = data.numpy(), meta.numpy()
+    chunks = [(mn[i % pool_n], dn[i % pool_n]) for i in range(n)]
+    total = n * world
+    per = 100  # chunks per copyset, over the whole pool
+    lay = copyset_layout(list(range(total)), [i // per for i in range(total)],
+                         [C.CHUNK_SIZE + C.META_PAGE_SIZE] * total)
+    C.scan_host(chunks[:4])  # warm
+    dist.barrier()
+    t0 = time.perf_counter()
+    _, _, fc = C.scan_host(chunks)
+    part = np.zeros(lay.n_groups, dtype=np.uint32)
+    lo = rank * n
+    for i in range(n):
+        part[lay.group[lo + i]] ^= C.shift(int(fc[i]), lay.after_bytes[lo + i])
+    dig = reduce_digests(torch.from_numpy(part.view(np.int32)).to(dev), dist)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64,
+                     device="cpu" if dist.get_backend() == "gloo" else dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    return {"chunks_per_rank": n, "ranks": world, "seconds_max_rank": round(el, 3),
+            "GiBps_e2e_aggregate": round(total * (C.CHUNK_SIZE + C.META_PAGE_SIZE) / GiB / el, 2),
+            "copysets": lay.n_groups, "digests": int(dig.numel()),
+            "source": "pinned host pool of 64 chunk files per rank, re-referenced; cc_scan_host per rank"}
 
 
 def files_leg(args):
@@ -464,6 +506,13 @@ def main():
         out["read_verify"] = read_verify_leg(pool, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pool, args, rank)
+    if world > 1 and not args.no_e2e and args.stream_chunks:
+        # BASELINE config 5 streamed end to end: every rank scans its own chunk
+        # files from pinned host memory through its own PCIe link
+        try:
+            out["stream_all_ranks"] = stream_all_ranks_leg(args, rank, world, dev)
+        except Exception as e:  # report, never lose the main line
+            out["stream_all_ranks"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_e2e:
         out["e2e_pinned_GiBps"] = e2e_leg(args, dev)
         if args.stream_chunks:
