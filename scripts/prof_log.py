@@ -17,6 +17,7 @@ p.add_argument("--updates", type=int, default=65536)
 p.add_argument("--reps", type=int, default=5)
 p.add_argument("--lib", default=None, help="libcurvecrc variant to load instead of the in-tree one")
 p.add_argument("--align", type=int, default=1, help="round dst/src offsets and lengths down to this")
+p.add_argument("--delta", action="store_true", help="cc_apply_log_delta_dev (stored CRCs updated by linearity)")
 a = p.parse_args()
 if a.lib:
     from curve_amd import _lib
@@ -38,11 +39,11 @@ ms = []
 for k, d_log in enumerate(logs):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
-    C.apply_log(pool, crcs, src, d_log, U, 4096, 4096)
+    C.apply_log(pool, crcs, src, d_log, U, 4096, 4096, delta=a.delta)
     e1.record(s)
     torch.cuda.synchronize()
     if k:
         ms.append(e0.elapsed_time(e1))
 ok = bool(torch.equal(crcs, C.page_crc(pool, 4096)))  # page CRCs consistent with the final bytes
-print("apply_log ms per batch:", [round(x, 4) for x in ms], "median", round(sorted(ms)[len(ms) // 2], 4),
+print("apply_log%s ms per batch:" % (" delta" if a.delta else ""), [round(x, 4) for x in ms], "median", round(sorted(ms)[len(ms) // 2], 4),
       "crcs_consistent", ok)
