@@ -80,6 +80,7 @@ SIGNATURES = {
     "cc_scan_host": (_int, [ctypes.POINTER(CcChunkSrc), _u64, _u32, _u32, _u32, _u32, _vp, _vp, _vp]),
     "cc_apply_log_work_bytes": (_u64, [_u64, _u32, _u32]),
     "cc_apply_log_dev": (_int, [_vp, _u64, _u32, _vp, _vp, _u64, _u32, _vp, _vp, _u64, _vp]),
+    "cc_apply_log_delta_dev": (_int, [_vp, _u64, _u32, _vp, _vp, _u64, _u32, _vp, _vp, _u64, _vp]),
     "cc_verify_reads_work_bytes": (_u64, [_u64]),
     "cc_verify_reads_dev": (_int, [_vp, _u64, _u32, _vp, _u64, _vp, _vp, _vp, _vp, _u64, _vp]),
     "cc_comm_unique_id": (_int, [_vp, _sz]),

@@ -408,11 +408,15 @@ def log_records(dst_off, src_off, lens):
 _log_work = {}
 
 
-def apply_log(pool, page_crcs, src, d_log, n_updates: int, max_len: int, page_bytes: int = PAGE_SIZE, stream=None):
+def apply_log(pool, page_crcs, src, d_log, n_updates: int, max_len: int, page_bytes: int = PAGE_SIZE, stream=None,
+              delta: bool = False):
     """cc_apply_log_dev: the write log `d_log` (device tensor of n_updates
     cc_update records, WRITE order, overlaps allowed) applied to `pool` with
     later writes winning, and the CRC of every touched page recomputed in
-    `page_crcs` -- ordering, apply and rehash all on the device."""
+    `page_crcs` -- ordering, apply and rehash all on the device.
+    delta=True -> cc_apply_log_delta_dev: `page_crcs` must hold the CRCs of the
+    pages before the batch; they are updated by linearity from the touched rows
+    only (a stale CRC stays stale instead of being refreshed)."""
     torch = _torch()
     need = int(lib().cc_apply_log_work_bytes(n_updates, max_len, page_bytes))
     if need == 0:
@@ -423,18 +427,20 @@ def apply_log(pool, page_crcs, src, d_log, n_updates: int, max_len: int, page_by
         work = torch.empty(need, dtype=torch.uint8, device=pool.device)
         _log_work[key] = work
     with torch.cuda.device(pool.device):
-        check(lib().cc_apply_log_dev(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, _dev_ptr(src, "src"),
-                                     _dev_ptr(d_log, "log"), n_updates, max_len, _dev_ptr(page_crcs, "page_crcs"),
-                                     _dev_ptr(work, "work"), work.numel(), _stream_handle(stream)),
-              "cc_apply_log_dev")
+        fn = "cc_apply_log_delta_dev" if delta else "cc_apply_log_dev"
+        check(getattr(lib(), fn)(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, _dev_ptr(src, "src"),
+                                 _dev_ptr(d_log, "log"), n_updates, max_len, _dev_ptr(page_crcs, "page_crcs"),
+                                 _dev_ptr(work, "work"), work.numel(), _stream_handle(stream)), fn)
     if stream is not None:
         work.record_stream(stream)
     return 1
 
 
-def apply_updates(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int = PAGE_SIZE, stream=None):
+def apply_updates(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int = PAGE_SIZE, stream=None,
+                  delta: bool = False):
     """Client partial-write path: host-side write log -> device (one copy of the
-    records) -> cc_apply_log_dev.  Returns the number of device calls (1)."""
+    records) -> cc_apply_log_dev (cc_apply_log_delta_dev with delta=True).
+    Returns the number of device calls (1)."""
     import numpy as np
     torch = _torch()
     lens = np.asarray(lens, dtype=np.uint32)
@@ -448,7 +454,7 @@ def apply_updates(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int 
         raise CurveCrcError(_lib.CC_EINVAL, "update out of range or empty")
     rec = log_records(dst_off, src_off, lens)
     d_log = torch.from_numpy(rec.view(np.uint8)).to(pool.device)
-    n = apply_log(pool, page_crcs, src, d_log, rec.size, int(lens.max()), page_bytes, stream)
+    n = apply_log(pool, page_crcs, src, d_log, rec.size, int(lens.max()), page_bytes, stream, delta)
     if stream is not None:
         d_log.record_stream(stream)
     return n

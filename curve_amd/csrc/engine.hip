@@ -661,9 +661,10 @@ uint64_t cc_apply_log_work_bytes(uint64_t n_updates, uint32_t max_len, uint32_t 
     return 5 * align256(nk * 4) + 256 + align256(temp);
 }
 
-int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
-                     const cc_update* d_log, uint64_t n_updates, uint32_t max_len, uint32_t* d_page_crcs,
-                     void* d_work, uint64_t work_bytes, void* stream) {
+namespace {
+int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src, const cc_update* d_log,
+              uint64_t n_updates, uint32_t max_len, uint32_t* d_page_crcs, void* d_work, uint64_t work_bytes,
+              void* stream, int delta) {
     if (!log_page_ok(page_bytes)) return CC_EINVAL;
     if (n_updates == 0) return CC_OK;
     if (!d_pool || !d_src || !d_log || !d_page_crcs || !d_work || max_len == 0) return CC_EINVAL;
@@ -700,6 +701,7 @@ int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, con
     a.image = c->image;
     a.kconst = kconst_for(page_bytes);
     a.page_crcs = d_page_crcs;
+    a.delta = delta;
     // sort only the bits a page index can have, + 1 so kNoPiece sorts last
     int end_bit = 1;
     while (end_bit < 32 && (1ull << end_bit) < n_pages) end_bit++;
@@ -714,6 +716,21 @@ int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, con
         return map_err(e);
     if ((e = launch_log_heads(a, s)) != hipSuccess) return map_err(e);
     return map_err(launch_log_pages(a, s));
+}
+}  // namespace
+
+int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
+                     const cc_update* d_log, uint64_t n_updates, uint32_t max_len, uint32_t* d_page_crcs,
+                     void* d_work, uint64_t work_bytes, void* stream) {
+    return apply_log(d_pool, pool_bytes, page_bytes, d_src, d_log, n_updates, max_len, d_page_crcs, d_work,
+                     work_bytes, stream, 0);
+}
+
+int cc_apply_log_delta_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
+                           const cc_update* d_log, uint64_t n_updates, uint32_t max_len, uint32_t* d_page_crcs,
+                           void* d_work, uint64_t work_bytes, void* stream) {
+    return apply_log(d_pool, pool_bytes, page_bytes, d_src, d_log, n_updates, max_len, d_page_crcs, d_work,
+                     work_bytes, stream, 1);
 }
 
 uint64_t cc_verify_reads_work_bytes(uint64_t n_reads) {

@@ -112,8 +112,9 @@ struct LogLaunch {
     uint32_t* head_count;       // number of them (zeroed by the expand kernel)
     const void* image;
     uint32_t kconst;
-    uint32_t* page_crcs;
+    uint32_t* page_crcs;        // out; in delta mode also in (the CRCs before the batch)
     int blocks;
+    int delta;                  // 1: update the stored CRCs through linearity (reads touched rows only)
 };
 hipError_t launch_log_expand(const LogLaunch& a, hipStream_t s);
 hipError_t launch_log_heads(const LogLaunch& a, hipStream_t s);

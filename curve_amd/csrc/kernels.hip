@@ -667,6 +667,9 @@ __device__ __forceinline__ Piece piece_in_page(uint64_t pbase, uint32_t page_byt
 // dword loads).  The at most two partially covered dwords (the piece's first
 // and last) are spliced from the aligned source dwords holding their needed
 // bytes, kept in 4 edge registers instead of a second [M] array.
+#ifndef CC_LOG_ABLATE
+#define CC_LOG_ABLATE 0  // timing ablations of log_pages_kernel (wrong results): 1 no stores, 2 no source loads, 3 no page loads, 4 no CRC chain, 5 no loads/stores of data
+#endif
 constexpr uint32_t kBufOOB = 0x80000000u;   // offset past num_records: load 0 / store dropped
 constexpr uint32_t kBufFlags = 0x00020000u;  // buffer resource dword 3 for gfx9-family (CDNA)
 
@@ -720,7 +723,7 @@ __device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint
 #pragma unroll
     for (int j = 0; j < M; j++) {
         const bool full = ((pr.whole >> j) & 1u) || ((uint32_t)j == pr.row0 && f0) || ((uint32_t)j == pr.row1 && f1);
-        r.S[j] = __builtin_amdgcn_raw_buffer_load_b32(rw, (full ? l4 : kBufOOB) + 256u * j, 0, 0);
+        r.S[j] = __builtin_amdgcn_raw_buffer_load_b32(rw, (full && CC_LOG_ABLATE != 2 && CC_LOG_ABLATE != 5 ? l4 : kBufOOB) + 256u * j, 0, 0);
     }
     uint32_t e[2];
     piece_edges(p, e);
@@ -825,7 +828,25 @@ __global__ __launch_bounds__(1024) void log_heads_kernel(LogLaunch a) {
 #else
 #define CC_LOG_ATTR __launch_bounds__(64 * CC_LOG_WAVES)
 #endif
+// Delta mode (cc_apply_log_delta_dev): the stored CRC of each touched page is
+// taken as the CRC of its bytes before the batch and updated through
+// linearity, V(new) = V(old) ^ raw0(old ^ new) (equal lengths: the init and
+// xorout terms cancel), so only the rows the page's pieces touch are read --
+// untouched rows get an out-of-range buffer offset (0, no memory traffic) and
+// contribute 0 to old ^ new.  A page with several pieces reads all rows.
+// Bit-identical to the full rehash whenever the stored CRC matched the page;
+// if it did not (latent corruption), the mismatch survives the write instead
+// of being laundered into a fresh CRC.
 template <int M>
+__device__ __forceinline__ void load_rows(uint32_t (&w)[M], const unsigned char* page, uint32_t rows, uint32_t lane) {
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(page), 0, 256u * M,
+                                                                         kBufFlags);
+#pragma unroll
+    for (int j = 0; j < M; j++)
+        w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, (((rows >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j, 0, 2);
+}
+
+template <int M, bool Delta>
 __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
     __shared__ uint32_t tab[kLdsBytes / 4];
     fill_lds<64 * kLogWaves>(tab, static_cast<const uint4*>(a.image));
@@ -863,8 +884,26 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
         };
         // one page step: merge + store + rehash page `pg` from (X, SX, px) while
         // the loads of the next page go into (Y, SY); false after the last page
-        auto step = [&](uint32_t (&X)[M], PieceSrc<M>& SX, const Piece& px, uint32_t pg, uint32_t hh,
-                        uint32_t (&Y)[M], PieceSrc<M>& SY, Piece& py, uint32_t& pgy) {
+        // delta mode: rows of page h to read (the head piece's if it is the
+        // page's only piece) and the page's stored CRC (a vector load: a scalar
+        // one would share lgkmcnt with the chain's LDS lookups)
+        auto load_next = [&](uint32_t (&Y)[M], const Piece& py, uint32_t pgy, uint32_t h, uint32_t& ocy) {
+            if constexpr (Delta) {
+                const PieceRows r = piece_rows(py);
+                const uint32_t top = r.row1 >= 31 ? 0xFFFFFFFFu : (2u << r.row1) - 1u;
+                const uint32_t rows = ((singles >> h) & 1ull) ? top & ~((1u << r.row0) - 1u) : 0xFFFFFFFFu;
+                load_rows<M>(Y, a.pool + (uint64_t)pgy * pb, rows, lane);
+                uint32_t vz = 0;
+                asm volatile("" : "+v"(vz));
+                ocy = a.page_crcs[pgy + vz];
+            } else if constexpr (CC_LOG_ABLATE == 3 || CC_LOG_ABLATE == 5) {
+                load_rows<M>(Y, a.pool + (uint64_t)pgy * pb, 0u, lane);  // timing ablation: no page reads
+            } else {
+                load_page<M>(Y, pages + (uint64_t)pgy * (64u * M));
+            }
+        };
+        auto step = [&](uint32_t (&X)[M], PieceSrc<M>& SX, const Piece& px, uint32_t pg, uint32_t hh, uint32_t ocx,
+                        uint32_t (&Y)[M], PieceSrc<M>& SY, Piece& py, uint32_t& pgy, uint32_t& ocy) {
             const bool more = hh + 1 < cnt;
             // next page + its first piece's source bytes in flight (clamped to the
             // last page: a harmless re-read, so every step issues the same loads
@@ -872,10 +911,15 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
             const uint32_t h1 = more ? hh + 1 : hh;
             pgy = __builtin_amdgcn_readlane(key, h1);
             py = head_piece(h1, pgy);
-            load_page<M>(Y, pages + (uint64_t)pgy * (64u * M));
+            load_next(Y, py, pgy, h1, ocy);
             fetch_piece<M>(SY, py, lane);
             const uint64_t pbase = (uint64_t)pg * pb;
             uint32_t dirty = 0;
+            uint32_t O[Delta ? M : 1];
+            if constexpr (Delta) {
+#pragma unroll
+                for (int j = 0; j < M; j++) O[j] = X[j];
+            }
             merge_piece<M>(X, dirty, SX, px, lane);
             if (!((singles >> hh) & 1ull)) {  // further pieces of this page, in write order
                 for (uint32_t q = __builtin_amdgcn_readlane(pos, hh) + 1; q < a.n_keys; q++) {
@@ -891,22 +935,39 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
                     __builtin_amdgcn_make_buffer_rsrc(a.pool + pbase, 0, 256u * M, kBufFlags);
 #pragma unroll
                 for (int j = 0; j < M; j++)
-                    __builtin_amdgcn_raw_buffer_store_b32(X[j], rp, (((dirty >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j,
+                    __builtin_amdgcn_raw_buffer_store_b32(X[j], rp,
+                                                          (((dirty >> j) & 1u) && CC_LOG_ABLATE != 1 && CC_LOG_ABLATE != 5
+                                                               ? 4u * lane
+                                                               : kBufOOB) +
+                                                              256u * j,
                                                           0, 0);
             }
-            const uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
+            uint32_t crc;
+            if constexpr (Delta) {
+#pragma unroll
+                for (int j = 0; j < M; j++) O[j] ^= X[j];  // old ^ new: 0 outside the changed bytes
+                crc = wave_xor(apply_fin(tab, chain<M>(tab, O, c0, c1), cf)) ^ ocx;
+            } else if constexpr (CC_LOG_ABLATE == 4) {
+                uint32_t x = 0;  // timing ablation: no chain
+#pragma unroll
+                for (int j = 0; j < M; j++) x ^= X[j];
+                crc = wave_xor(x);
+            } else {
+                crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
+            }
             if (lane == 0) a.page_crcs[pg] = crc;
             return more;
         };
         // the two register sets alternate (no copies): page k in one while page
         // k+1's loads land in the other
         uint32_t pgA = __builtin_amdgcn_readlane(key, 0), pgB = pgA;
+        uint32_t ocA = 0, ocB = 0;
         Piece pA = head_piece(0, pgA), pB = pA;
-        load_page<M>(A, pages + (uint64_t)pgA * (64u * M));
+        load_next(A, pA, pgA, 0, ocA);
         fetch_piece<M>(S0, pA, lane);
         for (uint32_t h = 0;; h += 2) {
-            if (!step(A, S0, pA, pgA, h, B, S1, pB, pgB)) break;
-            if (!step(B, S1, pB, pgB, h + 1, A, S0, pA, pgA)) break;
+            if (!step(A, S0, pA, pgA, h, ocA, B, S1, pB, pgB, ocB)) break;
+            if (!step(B, S1, pB, pgB, h + 1, ocB, A, S0, pA, pgA, ocA)) break;
         }
     }
 }
@@ -1191,8 +1252,13 @@ hipError_t launch_log_heads(const LogLaunch& a, hipStream_t s) {
 
 hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s) {
     if (a.n_keys == 0) return hipSuccess;
-#define CC_GCASE(MM) \
-    case MM: hipLaunchKernelGGL((log_pages_kernel<MM>), dim3(a.blocks), dim3(64 * kLogWaves), 0, s, a); break;
+#define CC_GCASE(MM)                                                                                        \
+    case MM:                                                                                                \
+        if (a.delta)                                                                                        \
+            hipLaunchKernelGGL((log_pages_kernel<MM, true>), dim3(a.blocks), dim3(64 * kLogWaves), 0, s, a);  \
+        else                                                                                                \
+            hipLaunchKernelGGL((log_pages_kernel<MM, false>), dim3(a.blocks), dim3(64 * kLogWaves), 0, s, a); \
+        break;
     switch (a.page_bytes / kWaveBytes) {
         CC_GCASE(1)
         CC_GCASE(2)

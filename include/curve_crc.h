@@ -232,6 +232,18 @@ int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, con
                      const cc_update* d_log, uint64_t n_updates, uint32_t max_len, uint32_t* d_page_crcs,
                      void* d_work, uint64_t work_bytes, void* stream);
 
+/* The same write log, with d_page_crcs[p] taken as the CRC of page p BEFORE
+ * the batch and updated incrementally: V(new) = V(old) ^ raw(old ^ new) for
+ * equal-length pages, so only the 256-byte rows the writes touch are read
+ * (a page with several writes reads whole).  Identical output to
+ * cc_apply_log_dev whenever the stored CRCs matched the pages; a page whose
+ * stored CRC did not match (latent corruption) keeps mismatching after the
+ * write instead of receiving a fresh CRC over the corrupt bytes.  Same
+ * contract and work size as cc_apply_log_dev. */
+int cc_apply_log_delta_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
+                           const cc_update* d_log, uint64_t n_updates, uint32_t max_len, uint32_t* d_page_crcs,
+                           void* d_work, uint64_t work_bytes, void* stream);
+
 /* Verify-on-read for a batch of datastore reads (the read path of
  * CSChunkFile::Read, chunkserver_chunkfile.cpp:497-536, which today returns the
  * bytes unchecked): every page that read i = d_reads[i] (pool byte range, any

@@ -498,14 +498,16 @@ def test_scan_host_stream(dev, oracle, pinned):
         assert fc[i] == oracle.crc32c(m.tobytes() + d.tobytes())
 
 
-@pytest.mark.parametrize("batched", [False, True])
+@pytest.mark.parametrize("mode", ["log", "delta", "batched"])
 @pytest.mark.parametrize("page_bytes,n_upd,overlap", [(4096, 3000, False), (4096, 2000, True), (512, 2500, True),
                                                       (256, 1500, True), (8192, 1000, True)])
-def test_partial_writes(dev, oracle, page_bytes, n_upd, overlap, batched):
-    """cc_apply_updates_dev: unaligned sub-page writes (1 B .. >1 page, straddling
-    pages, overlapping in order) -> pool bytes == in-order host application and
-    every page CRC == oracle on the final bytes (touched pages recomputed,
+def test_partial_writes(dev, oracle, page_bytes, n_upd, overlap, mode):
+    """cc_apply_log_dev / cc_apply_log_delta_dev / cc_apply_updates_dev:
+    unaligned sub-page writes (1 B .. >1 page, straddling pages, overlapping in
+    order) -> pool bytes == in-order host application and every page CRC ==
+    oracle on the final bytes (touched pages recomputed or delta-updated,
     untouched ones kept)."""
+    batched = mode == "batched"
     from curve_amd import crc as C
     rng = np.random.default_rng(n_upd + overlap + page_bytes)
     pool_bytes = 8 << 20
@@ -519,8 +521,11 @@ def test_partial_writes(dev, oracle, page_bytes, n_upd, overlap, batched):
     dst = rng.integers(0, span, n_upd)
     src_data = rng.integers(0, 256, int(lens.sum()) + 8, dtype=np.uint8)
     src_off = np.concatenate([[0], np.cumsum(lens)[:-1]]) + rng.integers(0, 4, n_upd) * 0
-    apply = C.apply_updates_batched if batched else C.apply_updates
-    nb = apply(d_pool, crcs, to_dev(src_data, dev), dst, src_off, lens, page_bytes)
+    if batched:
+        nb = C.apply_updates_batched(d_pool, crcs, to_dev(src_data, dev), dst, src_off, lens, page_bytes)
+    else:
+        nb = C.apply_updates(d_pool, crcs, to_dev(src_data, dev), dst, src_off, lens, page_bytes,
+                             delta=mode == "delta")
     assert nb == 1 or batched
     assert (nb > 1) == overlap or not overlap or not batched
     want = host.copy()
@@ -531,7 +536,8 @@ def test_partial_writes(dev, oracle, page_bytes, n_upd, overlap, batched):
     assert (u32(crcs) == oracle.page_crcs(want, page_bytes, threads=8)).all()
 
 
-def test_write_log_hot_pages_and_contract(dev, oracle):
+@pytest.mark.parametrize("delta", [False, True])
+def test_write_log_hot_pages_and_contract(dev, oracle, delta):
     """cc_apply_log_dev with every write piled on a few pages (long per-page
     piece lists that cross sort tiles, applied strictly in log order), plus
     entries that break the contract (len 0, len > max_len, beyond the pool):
@@ -556,7 +562,7 @@ def test_write_log_hot_pages_and_contract(dev, oracle):
     max_len = 3000
     rec = C.log_records(dst, src_off, lens)
     d_log = torch.from_numpy(rec.view(np.uint8)).to(dev)
-    C.apply_log(d_pool, crcs, to_dev(src_data, dev), d_log, n, max_len, pb)
+    C.apply_log(d_pool, crcs, to_dev(src_data, dev), d_log, n, max_len, pb, delta=delta)
     want = host.copy()
     for i in range(n):
         if i in bad:
@@ -565,6 +571,44 @@ def test_write_log_hot_pages_and_contract(dev, oracle):
     got = d_pool.cpu().numpy()
     assert (got == want).all()
     assert (u32(crcs) == oracle.page_crcs(want, pb)).all()
+
+
+@pytest.mark.parametrize("page_bytes", [4096, 512])
+def test_write_log_delta_keeps_latent_corruption(dev, oracle, page_bytes):
+    """cc_apply_log_delta_dev on a pool where some pages were corrupted after
+    their CRC was stored: the full rehash (cc_apply_log_dev) would hand those
+    pages a fresh CRC over the corrupt bytes; the delta update keeps the
+    mismatch, stored' = stored ^ V(old bytes) ^ V(new bytes), so verify still
+    flags exactly the corrupted pages after the write, clean pages match the
+    oracle, and the pool bytes equal in-order application either way."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(page_bytes + 5)
+    n_pages = 2048
+    pool_bytes = n_pages * page_bytes
+    host = rng.integers(0, 256, pool_bytes, dtype=np.uint8)
+    stored = oracle.page_crcs(host, page_bytes).copy()
+    rotten = sorted({1, 2, 500, 1023, n_pages - 1} | set(rng.integers(0, n_pages, 20).tolist()))
+    for p in rotten:  # bit rot after the CRC was written
+        host[p * page_bytes + int(rng.integers(0, page_bytes))] ^= 0x08
+    d_pool = to_dev(host, dev)
+    crcs = to_dev(stored.view(np.int32), dev)
+    n = 3000
+    lens = rng.integers(1, page_bytes + 300, n).astype(np.uint32)
+    dst = rng.integers(0, pool_bytes - page_bytes - 300, n).astype(np.uint64)
+    dst[:len(rotten)] = np.array(rotten, dtype=np.uint64) * page_bytes + 3  # write into every rotten page
+    dst[:len(rotten)] = np.minimum(dst[:len(rotten)], pool_bytes - page_bytes - 300)
+    src_data = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    src_off = rng.integers(0, (1 << 20) - page_bytes - 300, n).astype(np.uint64)
+    C.apply_updates(d_pool, crcs, to_dev(src_data, dev), dst, src_off, lens, page_bytes, delta=True)
+    want = host.copy()
+    for i in range(n):
+        want[dst[i]:dst[i] + lens[i]] = src_data[src_off[i]:src_off[i] + lens[i]]
+    assert (d_pool.cpu().numpy() == want).all()
+    got = u32(crcs)
+    old_c = oracle.page_crcs(host, page_bytes)
+    new_c = oracle.page_crcs(want, page_bytes)
+    assert (got == (stored ^ old_c ^ new_c)).all()
+    assert np.flatnonzero(got != new_c).tolist() == rotten  # exactly the rotten pages still fail
 
 
 def test_crc_ranges_arbitrary(dev, oracle):
