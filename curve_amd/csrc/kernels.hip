@@ -706,6 +706,19 @@ __device__ __forceinline__ PieceRows piece_rows(const Piece& p) {
     return r;
 }
 
+// Per-lane position of a piece: x_j = (page byte of the lane's row-j dword) -
+// rlo, in wrapping 32-bit arithmetic, so "dword wholly inside the piece" is ONE
+// unsigned compare per row, x_j < len - 3 (a dword below rlo wraps to >= 2^31),
+// on the vector unit: no per-row scalar masks or uniform row selects.
+struct PieceLane {
+    uint32_t o;   // 4 * lane - rlo (wrapping)
+    uint32_t l3;  // len - 3 if len >= 4, else 0 (no whole dword)
+};
+__device__ __forceinline__ PieceLane piece_lane(const Piece& p, uint32_t lane) {
+    const uint32_t len = p.rhi - p.rlo;
+    return {lane * 4u - p.rlo, len >= 4u ? len - 3u : 0u};
+}
+
 template <int M>
 __device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint32_t lane) {
     const uint32_t sh = (uint32_t)(uintptr_t)p.sp & 3u;  // the same for every dword of the piece
@@ -715,15 +728,12 @@ __device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint
     const __amdgpu_buffer_rsrc_t re =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(p.sp - sh), 0, 64u * 4u * M + 8u, kBufFlags);
     const uint32_t l4 = lane * 4u;
-    const PieceRows pr = piece_rows(p);
-    // per-lane whole-dword test only for the two boundary rows; every other
-    // row is uniformly all-or-nothing
-    const uint32_t b0 = l4 + 256u * pr.row0, b1 = l4 + 256u * pr.row1;
-    const bool f0 = b0 >= p.rlo && b0 + 4 <= p.rhi, f1 = b1 >= p.rlo && b1 + 4 <= p.rhi;
+    const PieceLane pl = piece_lane(p, lane);
 #pragma unroll
     for (int j = 0; j < M; j++) {
-        const bool full = ((pr.whole >> j) & 1u) || ((uint32_t)j == pr.row0 && f0) || ((uint32_t)j == pr.row1 && f1);
-        r.S[j] = __builtin_amdgcn_raw_buffer_load_b32(rw, (full && CC_LOG_ABLATE != 2 && CC_LOG_ABLATE != 5 ? l4 : kBufOOB) + 256u * j, 0, 0);
+        const bool full = pl.o + 256u * j < pl.l3;
+        r.S[j] = __builtin_amdgcn_raw_buffer_load_b32(
+            rw, (full && CC_LOG_ABLATE != 2 && CC_LOG_ABLATE != 5 ? l4 : kBufOOB) + 256u * j, 0, 0);
     }
     uint32_t e[2];
     piece_edges(p, e);
@@ -738,46 +748,35 @@ __device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint
     }
 }
 
-// Whole rows: every lane takes its source dword (one v_cndmask per row on a
-// uniform mask, no branches).  The <= 2 boundary rows run the per-lane
-// byte-mask merge, addressed by a uniform row index (selects instead of a
-// branch per row: more instructions than branching on each unrolled row, but
-// 186 -> 139 VGPRs at 4 KiB pages and no spills at 8 KiB; the kernel is
-// HBM-bound either way, measured equal).  `dirty` (rows written) is uniform.
-template <int M>
-__device__ __forceinline__ void merge_row(uint32_t (&w)[M], const PieceSrc<M>& r, const Piece& p, uint32_t row,
-                                          uint32_t lane, const uint32_t (&e)[2], uint32_t v0, uint32_t v1) {
-    const uint32_t d = lane + 64u * row, b = 4 * d;
-    const bool covered = b + 4 > p.rlo && b < p.rhi;
-    const uint32_t k0 = p.rlo > b ? p.rlo - b : 0u;
-    const uint32_t k1 = p.rhi < b + 4 ? p.rhi - b : 4u;
-    uint32_t old = w[0], s = r.S[0];
-#pragma unroll
-    for (int j = 1; j < M; j++) {  // uniform row select
-        old = (uint32_t)j == row ? w[j] : old;
-        s = (uint32_t)j == row ? r.S[j] : s;
-    }
-    const uint32_t v = d == e[0] ? v0 : (d == e[1] ? v1 : s);
-    const uint32_t mhi = k1 == 4u ? 0xFFFFFFFFu : (1u << (8u * k1)) - 1u;
-    const uint32_t mask = covered ? mhi & ~((1u << (8u * k0)) - 1u) : 0u;
-    const uint32_t nv = (v & mask) | (old & ~mask);
-#pragma unroll
-    for (int j = 0; j < M; j++) w[j] = (uint32_t)j == row ? nv : w[j];
-}
-
+// Whole dwords: one compare + select per row, on the vector unit.  The <= 2
+// partially covered dwords (the piece's first and last: each is one lane in
+// one row) are spliced under their byte mask; the owning lane carries the row
+// index, so each row costs a compare + select and there are no lane or row
+// branches.  `dirty` (rows written) is uniform.
 template <int M>
 __device__ __forceinline__ void merge_piece(uint32_t (&w)[M], uint32_t& dirty, const PieceSrc<M>& r, const Piece& p,
                                             uint32_t lane) {
+    const PieceLane pl = piece_lane(p, lane);
+#pragma unroll
+    for (int j = 0; j < M; j++) w[j] = pl.o + 256u * j < pl.l3 ? r.S[j] : w[j];
     uint32_t e[2];
     piece_edges(p, e);
     const uint32_t sh = (uint32_t)(uintptr_t)p.sp & 3u;
-    const uint32_t v0 = sh ? __builtin_amdgcn_alignbyte(r.eb[0], r.ea[0], sh) : r.ea[0];
-    const uint32_t v1 = sh ? __builtin_amdgcn_alignbyte(r.eb[1], r.ea[1], sh) : r.ea[1];
-    const PieceRows pr = piece_rows(p);
 #pragma unroll
-    for (int j = 0; j < M; j++) w[j] = ((pr.whole >> j) & 1u) ? r.S[j] : w[j];
-    if (!((pr.whole >> pr.row0) & 1u)) merge_row<M>(w, r, p, pr.row0, lane, e, v0, v1);
-    if (pr.row1 != pr.row0 && !((pr.whole >> pr.row1) & 1u)) merge_row<M>(w, r, p, pr.row1, lane, e, v0, v1);
+    for (int k = 0; k < 2; k++) {
+        const uint32_t v = sh ? __builtin_amdgcn_alignbyte(r.eb[k], r.ea[k], sh) : r.ea[k];
+        const uint32_t b = 4 * (e[k] & 0x3fffffffu);
+        const uint32_t k0 = p.rlo > b ? p.rlo - b : 0u;
+        const uint32_t k1 = p.rhi < b + 4 ? p.rhi - b : 4u;
+        const uint32_t mhi = k1 >= 4u ? 0xFFFFFFFFu : (1u << (8u * k1)) - 1u;
+        const uint32_t mask = mhi & ~((1u << (8u * (k0 & 3u))) - 1u);  // uniform
+        // row of edge k on its lane; no row elsewhere (or when there is no edge k)
+        uint32_t row = (e[k] != 0xffffffffu && lane == (e[k] & 63u)) ? e[k] >> 6 : 0xFFFFu;
+        asm volatile("" : "+v"(row));  // keep the per-row test one vector compare (not a scalar compare + mask)
+#pragma unroll
+        for (int j = 0; j < M; j++) w[j] = row == (uint32_t)j ? (v & mask) | (w[j] & ~mask) : w[j];
+    }
+    const PieceRows pr = piece_rows(p);
     const uint32_t top = pr.row1 >= 31 ? 0xFFFFFFFFu : (2u << pr.row1) - 1u;
     dirty |= top & ~((1u << pr.row0) - 1u);
 }
