@@ -91,7 +91,7 @@ hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s);
 // its pieces in registers, stores the changed rows and rehashes it.
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
 #ifndef CC_LOG_WAVES
-#define CC_LOG_WAVES 8  // waves per CU of the write-log page kernel (16 measured equal: HBM-bound)
+#define CC_LOG_WAVES 12  // waves per CU of the write-log page kernel (A/B: 12 beats 8 by ~6 %; 16 forces <= 128 VGPRs and spills in delta mode)
 #endif
 constexpr int kLogWaves = CC_LOG_WAVES;
 struct LogLaunch {
