@@ -499,6 +499,32 @@ def apply_updates_batched(pool, page_crcs, src, dst_off, src_off, lens, page_byt
     return nb
 
 
+_reads_work = {}
+
+
+def verify_read_records(pool, page_crcs, d_reads, n_reads: int, bad, total, page_bytes: int = PAGE_SIZE,
+                        stream=None):
+    """cc_verify_reads_dev on a batch already resident on the device: `d_reads`
+    = int64 device tensor of n_reads (offset, length) pairs; mismatches are
+    ADDED to `bad` (int32 [n_reads], -1 marks a read past the pool) and
+    `total` (int64 [1]).  Work buffer cached per device.  No host sync."""
+    torch = _torch()
+    need = int(lib().cc_verify_reads_work_bytes(n_reads))
+    if need == 0:
+        raise CurveCrcError(_lib.CC_EINVAL, "unsupported read batch")
+    work = _reads_work.get(pool.device)
+    if work is None or work.numel() < need:
+        work = torch.empty(need, dtype=torch.uint8, device=pool.device)
+        _reads_work[pool.device] = work
+    with torch.cuda.device(pool.device):
+        check(lib().cc_verify_reads_dev(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, _dev_ptr(d_reads, "reads"),
+                                        n_reads, _dev_ptr(page_crcs, "page_crcs"), _dev_ptr(bad, "bad"),
+                                        _dev_ptr(total, "total"), _dev_ptr(work, "work"), work.numel(),
+                                        _stream_handle(stream)), "cc_verify_reads_dev")
+    if stream is not None:
+        work.record_stream(stream)
+
+
 def verify_reads(pool, page_crcs, offsets, lengths, page_bytes: int = PAGE_SIZE, stream=None):
     """cc_verify_reads_dev: verify-on-read for a batch of reads of the pool.
     Returns (bad pages per read: int32 device tensor, -1 = read past the pool;

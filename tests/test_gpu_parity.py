@@ -384,6 +384,13 @@ def test_verify_reads_batch(dev, oracle, page_bytes):
         want_total += want
         assert got[i] == want, (i, o, n)
     assert int(total.item()) == want_total
+    # the device-resident entry point (records already in HBM) agrees
+    d_reads = to_dev(np.stack([np.array(off, dtype=np.uint64), np.array(ln, dtype=np.uint64)], axis=1)
+                     .reshape(-1).view(np.int64), dev)
+    bad2 = torch.zeros(len(reads), dtype=torch.int32, device=dev)
+    total2 = torch.zeros(1, dtype=torch.int64, device=dev)
+    C.verify_read_records(pool, stored, d_reads, len(reads), bad2, total2, page_bytes)
+    assert (bad2.cpu().numpy() == got).all() and int(total2.item()) == want_total
 
 
 def test_beyond_4gib_offsets(dev, oracle):
