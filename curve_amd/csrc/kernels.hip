@@ -1001,10 +1001,14 @@ __global__ void read_counts_kernel(ReadVerifyLaunch a) {
 // stored CRCs come in with VECTOR loads (an opaque zero in the address) so
 // they never share lgkmcnt with the chain's LDS lookups.  A mismatch is
 // counted on its read (rare: atomics).
+#ifndef CC_RV_WAVES
+#define CC_RV_WAVES 8  // waves per CU of the verify-on-read kernel
+#endif
+constexpr int kRvWaves = CC_RV_WAVES;
 template <int M>
-__global__ __launch_bounds__(kBlockThreads) void read_verify_kernel(ReadVerifyLaunch a) {
+__global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLaunch a) {
     __shared__ uint32_t tab[kLdsBytes / 4];
-    fill_lds(tab, static_cast<const uint4*>(a.image));
+    fill_lds<64 * kRvWaves>(tab, static_cast<const uint4*>(a.image));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t c0 = lane << 2 & 0x7Cu;
@@ -1013,8 +1017,8 @@ __global__ __launch_bounds__(kBlockThreads) void read_verify_kernel(ReadVerifyLa
     const uint32_t* pages = a.pool + lane;
     const uint64_t n = a.n_reads;
     const uint64_t T = a.start[n - 1] + a.counts[n - 1];
-    const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wave;
+    const uint64_t W = (uint64_t)gridDim.x * kRvWaves;
+    const uint64_t w = (uint64_t)blockIdx.x * kRvWaves + wave;
     uint32_t vz = 0;
     asm volatile("" : "+v"(vz));  // opaque zero: keeps uniform-address loads on the vector path
     // first read whose first slot is >= target (n if none): 64-ary search
@@ -1280,7 +1284,7 @@ hipError_t launch_read_counts(const ReadVerifyLaunch& a, hipStream_t s) {
 hipError_t launch_read_verify(const ReadVerifyLaunch& a, hipStream_t s) {
     if (a.n_reads == 0) return hipSuccess;
 #define CC_RCASE(MM) \
-    case MM: hipLaunchKernelGGL((read_verify_kernel<MM>), dim3(a.blocks), dim3(kBlockThreads), 0, s, a); break;
+    case MM: hipLaunchKernelGGL((read_verify_kernel<MM>), dim3(a.blocks), dim3(64 * kRvWaves), 0, s, a); break;
     switch (a.page_bytes / kWaveBytes) {
         CC_RCASE(1)
         CC_RCASE(2)
