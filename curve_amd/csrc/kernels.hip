@@ -690,20 +690,12 @@ __device__ __forceinline__ void piece_edges(const Piece& p, uint32_t (&e)[2]) {
 
 // Row structure of a piece (wave-uniform).  Row j = page bytes [256j, 256j+256)
 // = dword l + 64j of every lane.  A piece is one contiguous byte range, so it
-// touches rows [row0, row1], wholly covers the rows in `whole` (a bit mask), and
-// only row0 / row1 can be partly covered.
+// touches rows [row0, row1] (the rows it dirties; in delta mode the rows read).
 struct PieceRows {
-    uint32_t row0, row1, whole;
+    uint32_t row0, row1;
 };
 __device__ __forceinline__ PieceRows piece_rows(const Piece& p) {
-    PieceRows r;
-    r.row0 = p.rlo >> 8;
-    r.row1 = (p.rhi - 1) >> 8;
-    const uint32_t w0 = (p.rlo & 255u) ? r.row0 + 1 : r.row0;
-    const uint32_t w1 = (p.rhi & 255u) ? r.row1 : r.row1 + 1;  // <= 32
-    const uint32_t below1 = w1 >= 32 ? 0xFFFFFFFFu : (1u << w1) - 1u;
-    r.whole = w1 > w0 ? below1 & ~((1u << w0) - 1u) : 0u;
-    return r;
+    return {p.rlo >> 8, (p.rhi - 1) >> 8};
 }
 
 // Per-lane position of a piece: x_j = (page byte of the lane's row-j dword) -

@@ -50,6 +50,24 @@ def test_combine_shift_zeros(oracle):
     assert C.zeros(0) == 0
 
 
+def test_delta_update_identity(oracle):
+    """The identity cc_apply_log_delta_dev relies on, on the oracle: for equal
+    lengths V(new) = V(old) ^ raw(old ^ new), raw = zero init, no xorout
+    (= V(x) ^ V(0^n)); zero bytes outside the changed range add nothing, so the
+    rows a write does not touch need not be read."""
+    rng = np.random.default_rng(11)
+    for n, lo, hi in [(4096, 0, 1), (4096, 17, 3000), (4096, 4095, 4096), (512, 3, 509), (8192, 0, 8192)]:
+        old = rng.integers(0, 256, n, dtype=np.uint8)
+        new = old.copy()
+        new[lo:hi] = rng.integers(0, 256, hi - lo, dtype=np.uint8)
+        delta = (old ^ new).tobytes()
+        raw = oracle.crc32c(delta) ^ oracle.crc32c(bytes(n))
+        assert oracle.crc32c(new.tobytes()) == oracle.crc32c(old.tobytes()) ^ raw
+        # a stale stored CRC stays exactly as stale after the update
+        stale = oracle.crc32c(old.tobytes()) ^ 0x10
+        assert (stale ^ raw) ^ oracle.crc32c(new.tobytes()) == 0x10
+
+
 def test_fold_host(oracle, golden):
     s = golden["seeded_pages"]
     pages = oracle.splitmix64_bytes(s["seed"], s["n_pages"] * s["page_bytes"])
