@@ -1,6 +1,7 @@
 # PMC passes over the write-log path (scripts/prof_log.py): HBM bytes (FETCH_SIZE,
 # WRITE_SIZE: one pass each) and the SQ instruction mix, each in its own pass
-# usage: gpu_pmc_log.sh [SUFFIX [prof_log.py args...]]  (e.g. "delta --delta")
+# usage: gpu_pmc_log.sh [SUFFIX [driver args...]]  (e.g. "delta --delta")
+# PMC_DRIVER=scripts/prof_reads.py profiles the verify-on-read path instead
 set -u
 R=$(pwd)
 SUF=${1:-}
@@ -11,6 +12,6 @@ cd /tmp && export TMPDIR=/tmp
 IFS='|' read -ra PL <<< "$PASSES"
 for pass in "${PL[@]}"; do
   name=$(echo "$pass" | cut -d' ' -f1)$SUF
-  timeout -s KILL 90 rocprofv3 --pmc $pass -d $R/gpurun_out/pmc_log_$name -o run --output-format csv -- python3 $R/scripts/prof_log.py --reps 2 "$@" > $R/gpurun_out/pmc_log_$name.log 2>&1 || { echo "pass $name failed"; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $pass -d $R/gpurun_out/pmc_log_$name -o run --output-format csv -- python3 $R/${PMC_DRIVER:-scripts/prof_log.py} --reps 2 "$@" > $R/gpurun_out/pmc_log_$name.log 2>&1 || { echo "pass $name failed"; exit 1; }
 done
 echo pmc done
