@@ -312,6 +312,47 @@ void PoolScanShardRccl() {  // one rank's shard, native RCCL 
     for (void* p : {d_data, d_meta, d_after, d_mult, d_group, d_pc, d_mc, d_sc, d_fc, d_dig}) EXPECT(hipFree(p) == hipSuccess);
 }
 
+void WriteLogBothModes() {  // an ordered write log from plain C++, both CRC modes
+    const uint32_t pb = 4096, max_len = 5000;
+    const uint64_t pool_bytes = 1 << 20, src_bytes = 1 << 16, n = 600;
+    std::mt19937_64 rng(33);
+    std::string pool(pool_bytes, '\0'), src(src_bytes, '\0');
+    for (auto& c : pool) c = (char)(rng() & 0xFF);
+    for (auto& c : src) c = (char)(rng() & 0xFF);
+    std::vector<cc_update> log(n);
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t len = 1 + (uint32_t)(rng() % max_len);
+        const uint64_t dst = i < 200 ? 5 * pb + rng() % (3 * pb) : rng() % (pool_bytes - len);  // overlaps first
+        log[i] = {dst < pool_bytes - len ? dst : pool_bytes - len, rng() % (src_bytes - len), len, 0};
+    }
+    std::string want = pool;  // in-order application: later writes win
+    for (const cc_update& u : log) want.replace(u.dst, u.len, src.substr(u.src, u.len));
+    void *d_src, *d_log, *d_work;
+    EXPECT(hipMalloc(&d_src, src_bytes) == hipSuccess && hipMalloc(&d_log, n * sizeof(cc_update)) == hipSuccess);
+    EXPECT(hipMemcpy(d_src, src.data(), src_bytes, hipMemcpyHostToDevice) == hipSuccess);
+    EXPECT(hipMemcpy(d_log, log.data(), n * sizeof(cc_update), hipMemcpyHostToDevice) == hipSuccess);
+    const uint64_t work = cc_apply_log_work_bytes(n, max_len, pb);
+    EXPECT(work > 0 && hipMalloc(&d_work, work) == hipSuccess);
+    for (int delta = 0; delta < 2; delta++) {
+        void *d_pool, *d_pc;
+        EXPECT(hipMalloc(&d_pool, pool_bytes) == hipSuccess && hipMalloc(&d_pc, pool_bytes / pb * 4) == hipSuccess);
+        EXPECT(hipMemcpy(d_pool, pool.data(), pool_bytes, hipMemcpyHostToDevice) == hipSuccess);
+        EXPECT(cc_page_crc_dev(d_pool, pool_bytes / pb, pb, (uint32_t*)d_pc, nullptr) == CC_OK);
+        auto apply = delta ? cc_apply_log_delta_dev : cc_apply_log_dev;
+        EXPECT(apply(d_pool, pool_bytes, pb, d_src, (const cc_update*)d_log, n, max_len, (uint32_t*)d_pc, d_work, work,
+                     nullptr) == CC_OK);
+        EXPECT(hipDeviceSynchronize() == hipSuccess);
+        std::string got(pool_bytes, '\0');
+        std::vector<uint32_t> pc(pool_bytes / pb);
+        EXPECT(hipMemcpy(&got[0], d_pool, pool_bytes, hipMemcpyDeviceToHost) == hipSuccess);
+        EXPECT(hipMemcpy(pc.data(), d_pc, pc.size() * 4, hipMemcpyDeviceToHost) == hipSuccess);
+        EXPECT(got == want);
+        for (uint64_t p = 0; p < pc.size(); p++) EXPECT(pc[p] == Oracle(want.substr(p * pb, pb)));
+        for (void* q : {d_pool, d_pc}) EXPECT(hipFree(q) == hipSuccess);
+    }
+    for (void* q : {d_src, d_log, d_work}) EXPECT(hipFree(q) == hipSuccess);
+}
+
 struct Case {
     const char* name;
     bool gpu;
@@ -345,6 +386,7 @@ int main(int argc, char** argv) {
         {"CopysetHashMixed", true, CopysetHashMixed},
         {"ScanCopysetMaps", true, ScanCopysetMaps},
         {"PoolScanShardRccl", true, PoolScanShardRccl},
+        {"WriteLogBothModes", true, WriteLogBothModes},
     };
     int ran = 0, skipped = 0, failed_cases = 0;
     for (const Case& c : cases) {
