@@ -49,6 +49,7 @@ def parse():
     p.add_argument("--stream-chunks", type=int, default=10000, help="config-4 stream leg (0 = skip)")
     p.add_argument("--stream-chunks-per-rank", type=int, default=2000, help="N>1: streamed chunks per rank")
     p.add_argument("--file-chunks", type=int, default=128, help="datastore read-path leg (0 = skip)")
+    p.add_argument("--wal-entries", type=int, default=65536, help="WAL replay leg: entries per batch (0 = skip)")
     p.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/traffic_*.json)")
     return p.parse_args()
 
@@ -360,6 +361,56 @@ def read_verify_leg(pool, args):
                     "(count, scan, verify); alg bytes = 4100 per touched page"}
 
 
+def wal_replay_leg(pool, args):
+    """SURVEY §8f row 3, the raft WAL's data checksums on replay
+    (CurveSegment::_load_entry, raftlog/curve_segment.cpp:307-371): entries laid
+    out as CurveSegment::append writes them (28-byte header + data, padded to
+    4 KiB, walAlignSize) back to back in HBM; data_real_len uniform in
+    [1 KiB, 128 KiB] (client writes).  One cc_crc_ranges_dev call verifies the
+    data CRC of every entry; the header walk stays on the host (curve_amd/wal.py).
+    The synthetic segments are the resident pool's bytes (random), so the
+    ranges are arbitrary-alignment views of HBM, as the WAL's are."""
+    from curve_amd import crc as C
+    dev = pool.data.device
+    flat = pool.data.view(-1)
+    n = args.wal_entries
+    rng = np.random.default_rng(0x3A1)
+    real = rng.integers(1024, (128 << 10) + 1, n).astype(np.uint64)
+    slot = (28 + real + 4095) // 4096 * 4096          # header + data, padded to walAlignSize
+    start = np.concatenate([[0], np.cumsum(slot)[:-1]]).astype(np.uint64) + 4096  # after the meta page
+    if int(start[-1] + slot[-1]) > flat.numel():
+        return {"skipped": "pool too small for the WAL batch"}
+    offs = start + 28
+    rec = np.empty((n, 2), dtype=np.uint64)
+    rec[:, 0], rec[:, 1] = offs, real
+    d_rec = torch.from_numpy(rec.view(np.uint8).reshape(-1)).to(dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+    L = C.lib()
+    ms = []
+    for it in range(6):
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        C.check(L.cc_crc_ranges_dev(flat.data_ptr(), d_rec.data_ptr(), n, out.data_ptr(),
+                                    C._stream_handle(stream)), "cc_crc_ranges_dev")
+        e1.record(stream)
+        torch.cuda.synchronize()
+        if it:
+            ms.append(e0.elapsed_time(e1))
+    # spot check against the CPU primitive (crc32c_value, the product's own)
+    got = C.as_u32(out)
+    host = {int(i): flat[int(offs[i]):int(offs[i] + real[i])].cpu().numpy().tobytes() for i in (0, n // 2, n - 1)}
+    spot = all(int(got[i]) == C.CRC32(b) for i, b in host.items())
+    t = float(np.mean(ms))
+    data = float(real.sum())
+    return {"entries_per_batch": n, "data_bytes_per_batch": int(data), "ms_per_batch": round(t, 4),
+            "entries_per_s": round(n / (t * 1e-3), 1), "GBps": round(data / (t * 1e-3) / 1e9, 1),
+            "alg_frac_of_hbm_peak": round((data + 4 * n) / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "spot_check_vs_cpu_primitive": spot,
+            "note": "entry records resident in HBM; alg bytes = data bytes read + 4 B CRC written per entry"}
+
+
 def load_traffic(args):
     path = args.traffic_json
     if path is None:
@@ -534,6 +585,8 @@ def main():
         out["partial_write"] = partial_write_leg(pool, args)
     if rank == 0 and world == 1 and args.reads:
         out["read_verify"] = read_verify_leg(pool, args)
+    if rank == 0 and world == 1 and args.wal_entries:
+        out["wal_replay"] = wal_replay_leg(pool, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pool, args, rank)
     if world > 1 and not args.no_e2e and args.stream_chunks:

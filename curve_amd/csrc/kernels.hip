@@ -327,6 +327,18 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
     }
 }
 
+#ifndef CC_LOG_ABLATE
+#define CC_LOG_ABLATE 0  // timing ablations of log_pages_kernel (wrong results): 1 no stores, 2 no source loads, 3 no page loads, 4 no CRC chain, 5 no loads/stores of data
+#endif
+constexpr uint32_t kBufOOB = 0x80000000u;   // offset past num_records: load 0 / store dropped
+constexpr uint32_t kBufFlags = 0x00020000u;  // buffer resource dword 3 for gfx9-family (CDNA)
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+    // readlane returns int: go through uint32_t so the low half is not sign-extended
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
+}
+
 // ---------------------------------------------------------------------------
 // GF(2) helpers for the fold / shift kernels (tiny volume: 4 B per page).
 // ---------------------------------------------------------------------------
@@ -368,14 +380,76 @@ __device__ __forceinline__ uint32_t xpow_wave(uint64_t n, uint32_t lane) {
 
 // ---------------------------------------------------------------------------
 // CRC32C of arbitrary byte ranges (WAL entries on replay, raw-file hashes).
-// One wave per range.  The range [off, off+len) is viewed as R whole 256-byte
-// rows starting at the 4-byte-aligned address a = off & ~3: bytes before off
-// and at/after off+len are masked to zero.  Leading zeros do not change a
-// zero-init (raw) CRC, so the page-kernel chain yields raw(data || 0^t) =
-// shift(raw(data), t) with t = 256R - (off - a) - len; multiplying by
-// x^(-8t) undoes the trailing pad, and K(len) = ~shift(~0, len) converts to
-// butil's Value.
+// The range [off, off+len) is viewed as whole 256-byte rows starting at the
+// 4-byte-aligned address a = off & ~3, bytes before off and at/after off+len
+// masked to zero.  Leading zeros do not change a zero-init (raw) CRC, so the
+// page-kernel chain yields raw(data' || 0^t) = x^(8t) raw(data'), t = pad after
+// the range in its last row; multiplying by x^(-8t) removes the pad.  butil's
+// init is folded into the data (len >= 4): for a reflected CRC, Value(M) =
+// raw(M ^ (~0 || 0...)) ^ ~0, so the first four bytes of the range are XORed
+// with 0xFF as they are loaded.  (len < 4: K(len) = ~shift(~0, len) instead.)
+//
+// Schedule: wave w owns ranges w, w+W, ... (W = waves in the grid); its lanes
+// load 64 range descriptors at once, and the wave walks their 4 KiB blocks (16
+// rows) as one stream: block k+1 -- of the same range or the next one -- is
+// loaded while block k is masked and chained, so a range of any length keeps
+// a block of loads in flight.  Loads are buffer loads with an out-of-range
+// offset for rows past the range (no branches around them: exact vmcnt waits).
 // ---------------------------------------------------------------------------
+struct RangeGeo {
+    uint64_t a;      // 4-byte-aligned start
+    uint64_t lim;    // bytes from a to the range's end
+    uint64_t len;
+    uint32_t head;   // off - a
+    uint32_t rows;   // 256-byte rows from a
+    uint32_t nb;     // 4 KiB blocks from a
+};
+__device__ __forceinline__ RangeGeo range_geo(uint64_t off, uint64_t len) {
+    RangeGeo g;
+    g.a = off & ~3ull;
+    g.head = (uint32_t)(off - g.a);
+    g.len = len;
+    g.lim = len + g.head;
+    g.rows = (uint32_t)((g.lim + 255) >> 8);
+    g.nb = (g.rows + 15) >> 4;
+    return g;
+}
+
+// Block k of range g (16 rows, lane l holds dwords l + 64j of the block).
+__device__ __forceinline__ void load_range_block(uint32_t (&w)[16], const unsigned char* buf, const RangeGeo& g,
+                                                 uint32_t k, uint32_t lane) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(buf + g.a + ((uint64_t)k << 12)), 0, 4096u,
+                                          kBufFlags);
+    const uint64_t rem = g.lim - ((uint64_t)k << 12);  // > 0 for every block of the range
+    const uint32_t remc = rem > 4096u ? 4096u : (uint32_t)rem;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint32_t o = 256u * j + 4u * lane;
+        w[j] = __builtin_amdgcn_raw_buffer_load_b32(r, o < remc ? o : kBufOOB, 0, 2);
+    }
+}
+
+// Zero the bytes outside the range (first / last dword) and fold butil's init
+// into the first four bytes.  Block k; the row/lane tests are per-lane compares.
+__device__ __forceinline__ void mask_range_block(uint32_t (&w)[16], const RangeGeo& g, uint32_t k, uint32_t lane) {
+    const uint64_t last = g.lim - 1;  // byte offset (from a) of the range's last byte
+    const uint32_t tail = (uint32_t)(g.lim & 3u);
+    const uint32_t mhi = tail ? 0xFFFFFFFFu >> (8u * (4u - tail)) : 0xFFFFFFFFu;
+    const uint64_t lrow = last >> 8;
+    uint32_t rl = (lane == (uint32_t)((last >> 2) & 63u) && (lrow >> 4) == k) ? (uint32_t)(lrow & 15u) : 0xFFFFu;
+    asm volatile("" : "+v"(rl));
+#pragma unroll
+    for (int j = 0; j < 16; j++) w[j] = rl == (uint32_t)j ? w[j] & mhi : w[j];
+    if (k == 0) {  // uniform
+        uint32_t lo = lane == 0 ? 0xFFFFFFFFu << (8u * g.head) : 0xFFFFFFFFu;
+        uint32_t init = 0u;
+        if (g.len >= 4) init = lane == 0 ? 0xFFFFFFFFu << (8u * g.head)
+                                         : (lane == 1 && g.head ? 0xFFFFFFFFu >> (8u * (4u - g.head)) : 0u);
+        w[0] = (w[0] & lo) ^ init;
+    }
+}
+
 __global__ __launch_bounds__(kBlockThreads) void range_crc_kernel(const unsigned char* __restrict__ buf,
                                                                   const RangeDesc* __restrict__ ranges, uint64_t n,
                                                                   const uint4* __restrict__ image,
@@ -387,29 +461,63 @@ __global__ __launch_bounds__(kBlockThreads) void range_crc_kernel(const unsigned
     const uint32_t c0 = lane << 2 & 0x7Cu;
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
-    for (uint64_t r = (uint64_t)blockIdx.x * kWavesPerBlock + wave; r < n; r += (uint64_t)gridDim.x * kWavesPerBlock) {
-        const uint64_t off = ranges[r].off, len = ranges[r].len;
-        if (len == 0) {
-            if (lane == 0) out[r] = 0u;
-            continue;
-        }
-        const uint64_t a = off & ~3ull, end = off + len;
-        const uint64_t rows = (len + (off - a) + 255) >> 8;
-        const uint32_t t = (uint32_t)((rows << 8) - (off - a) - len);
-        auto word = [&](uint64_t j) -> uint32_t {
-            const uint64_t addr = a + (j << 8) + 4ull * lane;
-            if (addr >= end) return 0u;
-            uint32_t w = *reinterpret_cast<const uint32_t*>(buf + addr);
-            if (addr < off) w &= 0xFFFFFFFFu << (8u * (uint32_t)(off - addr));  // bytes before the range
-            if (addr + 4 > end) w &= 0xFFFFFFFFu >> (8u * (uint32_t)(addr + 4 - end));  // bytes after it
-            return w;
+    const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t base = (uint64_t)blockIdx.x * kWavesPerBlock + wave; base < n; base += 64u * W) {
+        const uint64_t ri = base + (uint64_t)lane * W;
+        const bool valid = ri < n;
+        const RangeDesc rd = ranges[valid ? ri : base];
+        if (valid && rd.len == 0) out[ri] = 0u;  // V(empty) = 0
+        uint64_t bits = __ballot(valid && rd.len != 0);
+        if (!bits) continue;
+        auto geo = [&](uint32_t h) {
+            return range_geo(readlane64(rd.off, h), readlane64(rd.len, h));
         };
-        uint32_t s = word(0);
-        for (uint64_t j = 1; j < rows; j++) s = apply_g_xor(tab, s, word(j), c0, c1);
-        const uint32_t raw_pad = wave_xor(apply_fin(tab, s, cf));
-        const uint32_t kz = ~mulmod_dev(xpow_wave(len << 3, lane), 0xFFFFFFFFu);
-        const uint32_t v = mulmod_dev(c_xinv.t[t], raw_pad) ^ kz;
-        if (lane == 0) out[r] = v;
+        uint32_t A[16], B[16];
+        uint32_t hA = (uint32_t)__builtin_ctzll(bits), hB = hA;
+        bits &= bits - 1;
+        RangeGeo gA = geo(hA), gB = gA;
+        uint32_t kA = 0, kB = 0;
+        uint32_t s = 0;
+        load_range_block(A, buf, gA, 0, lane);
+        // consume block (X: range gx slot hx, block kx) while the successor's
+        // loads go into Y; false after the wave's last block
+        auto step = [&](uint32_t (&X)[16], const RangeGeo& gx, uint32_t hx, uint32_t kx, uint32_t (&Y)[16],
+                        RangeGeo& gy, uint32_t& hy, uint32_t& ky) {
+            bool any = true;
+            if (kx + 1 < gx.nb) {
+                gy = gx, hy = hx, ky = kx + 1;
+            } else if (bits) {
+                hy = (uint32_t)__builtin_ctzll(bits);
+                bits &= bits - 1;
+                gy = geo(hy), ky = 0;
+            } else {
+                any = false;  // clamped: re-read the current block (same loads every step)
+                gy = gx, hy = hx, ky = kx;
+            }
+            load_range_block(Y, buf, gy, ky, lane);
+            mask_range_block(X, gx, kx, lane);
+            const uint32_t rib = gx.rows - 16u * kx;  // rows of this block inside the range (>= 1)
+            s = kx == 0 ? X[0] : apply_g_xor(tab, s, X[0], c0, c1);
+#pragma unroll
+            for (int j = 1; j < 16; j++)
+                if ((uint32_t)j < rib) s = apply_g_xor(tab, s, X[j], c0, c1);
+            if (kx + 1 == gx.nb) {  // range done
+                const uint32_t raw_pad = wave_xor(apply_fin(tab, s, cf));
+                const uint32_t t = (uint32_t)(((uint64_t)gx.rows << 8) - gx.lim);  // zero pad in the last row
+                uint32_t v = mulmod_dev(c_xinv.t[t], raw_pad);
+                if (gx.len >= 4) {
+                    v ^= 0xFFFFFFFFu;
+                } else {
+                    v ^= ~mulmod_dev(xpow_wave(gx.len << 3, lane), 0xFFFFFFFFu);
+                }
+                if (lane == 0) out[base + (uint64_t)hx * W] = v;
+            }
+            return any;
+        };
+        for (;;) {
+            if (!step(A, gA, hA, kA, B, gB, hB, kB)) break;
+            if (!step(B, gB, hB, kB, A, gA, hA, kA)) break;
+        }
     }
 }
 
@@ -667,11 +775,6 @@ __device__ __forceinline__ Piece piece_in_page(uint64_t pbase, uint32_t page_byt
 // dword loads).  The at most two partially covered dwords (the piece's first
 // and last) are spliced from the aligned source dwords holding their needed
 // bytes, kept in 4 edge registers instead of a second [M] array.
-#ifndef CC_LOG_ABLATE
-#define CC_LOG_ABLATE 0  // timing ablations of log_pages_kernel (wrong results): 1 no stores, 2 no source loads, 3 no page loads, 4 no CRC chain, 5 no loads/stores of data
-#endif
-constexpr uint32_t kBufOOB = 0x80000000u;   // offset past num_records: load 0 / store dropped
-constexpr uint32_t kBufFlags = 0x00020000u;  // buffer resource dword 3 for gfx9-family (CDNA)
 
 template <int M>
 struct PieceSrc {
@@ -773,11 +876,6 @@ __device__ __forceinline__ void merge_piece(uint32_t (&w)[M], uint32_t& dirty, c
     dirty |= top & ~((1u << pr.row0) - 1u);
 }
 
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
-    // readlane returns int: go through uint32_t so the low half is not sign-extended
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
-           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
-}
 
 // Page runs of the sorted pieces: position q starts a run (a "head") when its
 // page differs from position q-1's.  Heads are compacted into a.heads (in no
