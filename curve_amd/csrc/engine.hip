@@ -121,8 +121,9 @@ int get_ctx(DevCtx** out) {
         if (e != hipSuccess) return map_err(e);
         e = upload_x2k(x2k().t);
         if (e != hipSuccess) return map_err(e);
-        uint32_t xinv[260];
-        for (uint32_t t = 0; t < 260; t++) xinv[t] = xinv_bytes(t);
+        static uint32_t xinv[kXinvEntries];
+        uint32_t r = xinv_bytes(0);
+        for (uint32_t t = 0; t < kXinvEntries; t++, r = div_x8(r)) xinv[t] = r;  // x^(-8t)
         e = upload_xinv(xinv);
         if (e != hipSuccess) return map_err(e);
         c->ready = true;
@@ -403,8 +404,12 @@ int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, u
     DevCtx* c = nullptr;
     int rc = get_ctx(&c);
     if (rc) return rc;
+#ifndef CC_RANGE_GRID_MULT
+#define CC_RANGE_GRID_MULT 1  // workgroups per CU launched for a range batch (> 1: hardware re-balances waves)
+#endif
     const uint64_t need = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-    const int blocks = (int)(need < (uint64_t)c->cus ? need : (uint64_t)c->cus);
+    const uint64_t cap = (uint64_t)c->cus * CC_RANGE_GRID_MULT;
+    const int blocks = (int)(need < cap ? need : cap);
     return map_err(launch_range_crc(static_cast<const unsigned char*>(d_buf),
                                     reinterpret_cast<const RangeDesc*>(d_ranges), n, c->image, d_out, blocks,
                                     static_cast<hipStream_t>(stream)));

@@ -30,6 +30,10 @@ inline uint32_t div_x(uint32_t b) {
 }
 
 // x^(-8t) mod P.
+inline uint32_t div_x8(uint32_t r) {  // r * x^-8
+    for (int i = 0; i < 8; i++) r = div_x(r);
+    return r;
+}
 inline uint32_t xinv_bytes(uint32_t t) {
     uint32_t r = kOne;
     for (uint32_t i = 0; i < 8 * t; i++) r = div_x(r);

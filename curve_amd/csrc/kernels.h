@@ -155,7 +155,8 @@ hipError_t launch_read_verify(const ReadVerifyLaunch& a, hipStream_t s);
 hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, const void* image,
                             uint32_t* out, int blocks, hipStream_t s);
 // x^(-8t) mod P for t = 0..259 (undoing a row's trailing zero padding)
-hipError_t upload_xinv(const uint32_t* t260);
+constexpr uint32_t kXinvEntries = 4100;  // x^(-8t), t < 4096 + 4: the zero pad after a range in its last 4 KiB block
+hipError_t upload_xinv(const uint32_t* table);
 
 // Fused scan epilogue: one 256-thread block per chunk.
 struct EpilogueLaunch {

@@ -365,9 +365,9 @@ __device__ __forceinline__ uint32_t xpow_dev(uint64_t n) {
 }
 
 struct XInv {
-    uint32_t t[260];
+    uint32_t t[kXinvEntries];
 };
-__constant__ XInv c_xinv;  // x^(-8t) mod P, t = 0..259
+__constant__ XInv c_xinv;  // x^(-8t) mod P, t = 0 .. kXinvEntries-1
 
 // Product over the wave of per-lane GF(2)[x]/P factors (lane k: x^(2^k) if bit k
 // of n is set, else 1) = x^n mod P; result in every lane.
@@ -384,7 +384,7 @@ __device__ __forceinline__ uint32_t xpow_wave(uint64_t n, uint32_t lane) {
 // 4-byte-aligned address a = off & ~3, bytes before off and at/after off+len
 // masked to zero.  Leading zeros do not change a zero-init (raw) CRC, so the
 // page-kernel chain yields raw(data' || 0^t) = x^(8t) raw(data'), t = pad after
-// the range in its last row; multiplying by x^(-8t) removes the pad.  butil's
+// the range in its last 4 KiB block; multiplying by x^(-8t) removes the pad.  butil's
 // init is folded into the data (len >= 4): for a reflected CRC, Value(M) =
 // raw(M ^ (~0 || 0...)) ^ ~0, so the first four bytes of the range are XORed
 // with 0xFF as they are loaded.  (len < 4: K(len) = ~shift(~0, len) instead.)
@@ -472,51 +472,74 @@ __global__ __launch_bounds__(kBlockThreads) void range_crc_kernel(const unsigned
         auto geo = [&](uint32_t h) {
             return range_geo(readlane64(rd.off, h), readlane64(rd.len, h));
         };
-        uint32_t A[16], B[16];
-        uint32_t hA = (uint32_t)__builtin_ctzll(bits), hB = hA;
-        bits &= bits - 1;
-        RangeGeo gA = geo(hA), gB = gA;
-        uint32_t kA = 0, kB = 0;
-        uint32_t s = 0;
-        load_range_block(A, buf, gA, 0, lane);
-        // consume block (X: range gx slot hx, block kx) while the successor's
-        // loads go into Y; false after the wave's last block
-        auto step = [&](uint32_t (&X)[16], const RangeGeo& gx, uint32_t hx, uint32_t kx, uint32_t (&Y)[16],
-                        RangeGeo& gy, uint32_t& hy, uint32_t& ky) {
-            bool any = true;
-            if (kx + 1 < gx.nb) {
-                gy = gx, hy = hx, ky = kx + 1;
-            } else if (bits) {
-                hy = (uint32_t)__builtin_ctzll(bits);
+        // stream position: block k of the range in lane slot h; `real` false
+        // once the wave's blocks are exhausted (then the last block is re-read:
+        // every step issues the same loads, so the vmcnt waits stay exact)
+        struct Pos {
+            RangeGeo g;
+            uint32_t h, k;
+            bool real;
+        };
+        auto adv = [&](const Pos& p) -> Pos {
+            Pos q = p;
+            if (p.real && p.k + 1 < p.g.nb) {
+                q.k = p.k + 1;
+            } else if (p.real && bits) {
+                q.h = (uint32_t)__builtin_ctzll(bits);
                 bits &= bits - 1;
-                gy = geo(hy), ky = 0;
+                q.g = geo(q.h);
+                q.k = 0;
             } else {
-                any = false;  // clamped: re-read the current block (same loads every step)
-                gy = gx, hy = hx, ky = kx;
+                q.real = false;
             }
-            load_range_block(Y, buf, gy, ky, lane);
+            return q;
+        };
+        uint32_t A[16], B[16], Cq[16];
+        Pos pA;
+        pA.h = (uint32_t)__builtin_ctzll(bits);
+        bits &= bits - 1;
+        pA.g = geo(pA.h);
+        pA.k = 0;
+        pA.real = true;
+        load_range_block(A, buf, pA.g, pA.k, lane);
+        Pos pB = adv(pA);
+        load_range_block(B, buf, pB.g, pB.k, lane);
+        Pos pC = pB;
+        uint32_t s = 0;
+        // consume X (two blocks of loads in flight behind it) after issuing the
+        // loads of position py into Y
+        auto step = [&](uint32_t (&X)[16], const Pos& px, uint32_t (&Y)[16], const Pos& py) {
+            load_range_block(Y, buf, py.g, py.k, lane);
+            const RangeGeo& gx = px.g;
+            const uint32_t kx = px.k;
             mask_range_block(X, gx, kx, lane);
-            const uint32_t rib = gx.rows - 16u * kx;  // rows of this block inside the range (>= 1)
+            // all 16 rows of every block: rows past the range are zeros (loaded
+            // out of range), i.e. a trailing pad the x^(-8t) below removes
             s = kx == 0 ? X[0] : apply_g_xor(tab, s, X[0], c0, c1);
 #pragma unroll
-            for (int j = 1; j < 16; j++)
-                if ((uint32_t)j < rib) s = apply_g_xor(tab, s, X[j], c0, c1);
+            for (int j = 1; j < 16; j++) s = apply_g_xor(tab, s, X[j], c0, c1);
             if (kx + 1 == gx.nb) {  // range done
                 const uint32_t raw_pad = wave_xor(apply_fin(tab, s, cf));
-                const uint32_t t = (uint32_t)(((uint64_t)gx.rows << 8) - gx.lim);  // zero pad in the last row
+                const uint32_t t = (uint32_t)(((uint64_t)gx.nb << 12) - gx.lim);  // zero pad in the last block
                 uint32_t v = mulmod_dev(c_xinv.t[t], raw_pad);
                 if (gx.len >= 4) {
                     v ^= 0xFFFFFFFFu;
                 } else {
                     v ^= ~mulmod_dev(xpow_wave(gx.len << 3, lane), 0xFFFFFFFFu);
                 }
-                if (lane == 0) out[base + (uint64_t)hx * W] = v;
+                if (lane == 0) out[base + (uint64_t)px.h * W] = v;
             }
-            return any;
         };
         for (;;) {
-            if (!step(A, gA, hA, kA, B, gB, hB, kB)) break;
-            if (!step(B, gB, hB, kB, A, gA, hA, kA)) break;
+            if (!pA.real) break;
+            pC = adv(pB);
+            step(A, pA, Cq, pC);
+            if (!pB.real) break;
+            pA = adv(pC);
+            step(B, pB, A, pA);
+            if (!pC.real) break;
+            pB = adv(pA);
+            step(Cq, pC, B, pB);
         }
     }
 }
@@ -1288,7 +1311,7 @@ hipError_t launch_fold(const FoldLaunch& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t upload_xinv(const uint32_t* t260) { return hipMemcpyToSymbol(HIP_SYMBOL(c_xinv), t260, sizeof(XInv)); }
+hipError_t upload_xinv(const uint32_t* table) { return hipMemcpyToSymbol(HIP_SYMBOL(c_xinv), table, sizeof(XInv)); }
 
 hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, const void* image,
                             uint32_t* out, int blocks, hipStream_t s) {
