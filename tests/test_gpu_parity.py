@@ -618,6 +618,25 @@ def test_write_log_delta_keeps_latent_corruption(dev, oracle, page_bytes):
     assert np.flatnonzero(got != new_c).tolist() == rotten  # exactly the rotten pages still fail
 
 
+def test_crc_ranges_large_batch(dev, oracle):
+    """cc_crc_ranges_dev over a batch larger than the grid (several 64-range
+    descriptor batches per wave): 10,000 ranges of every shape (empty, 1-3
+    bytes, unaligned, multi-block, one 3 MiB giant) == the oracle."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(4096)
+    buf = rng.integers(0, 256, 8 << 20, dtype=np.uint8)
+    d = to_dev(buf, dev)
+    n = 10000
+    lens = rng.integers(0, 70000, n)
+    lens[:40] = [0, 1, 2, 3, 4, 5, 255, 256, 257, 4095, 4096, 4097] + list(range(28))
+    lens[5000] = 3 << 20
+    offs = rng.integers(0, (8 << 20) - lens - 1)
+    got = u32(C.crc_ranges(d, offs, lens))
+    want = np.array([oracle.crc32c(buf[o:o + l].tobytes()) for o, l in zip(offs, lens)], dtype=np.uint32)
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, (bad[:10], offs[bad[:3]], lens[bad[:3]])
+
+
 def test_crc_ranges_arbitrary(dev, oracle):
     """cc_crc_ranges_dev: any offset / alignment / length (0 .. > 1 row)."""
     from curve_amd import crc as C
