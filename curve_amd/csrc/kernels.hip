@@ -422,12 +422,12 @@ __device__ __forceinline__ void load_range_block(uint32_t (&w)[16], const unsign
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(buf + g.a + ((uint64_t)k << 12)), 0, 4096u,
                                           kBufFlags);
     const uint64_t rem = g.lim - ((uint64_t)k << 12);  // > 0 for every block of the range
-    const uint32_t remc = rem > 4096u ? 4096u : (uint32_t)rem;
+    // bytes of the block left after this lane's dword in row 0: row j's dword
+    // starts inside the range iff 256 j < left (one compare + select per row)
+    const int32_t left = (int32_t)(rem > 4096u ? 4096u : (uint32_t)rem) - (int32_t)(4u * lane);
 #pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const uint32_t o = 256u * j + 4u * lane;
-        w[j] = __builtin_amdgcn_raw_buffer_load_b32(r, o < remc ? o : kBufOOB, 0, 2);
-    }
+    for (int j = 0; j < 16; j++)
+        w[j] = __builtin_amdgcn_raw_buffer_load_b32(r, left > 256 * j ? 4u * lane : kBufOOB, 256 * j, 2);
 }
 
 // Zero the bytes outside the range (first / last dword) and fold butil's init
@@ -435,12 +435,14 @@ __device__ __forceinline__ void load_range_block(uint32_t (&w)[16], const unsign
 __device__ __forceinline__ void mask_range_block(uint32_t (&w)[16], const RangeGeo& g, uint32_t k, uint32_t lane) {
     const uint64_t last = g.lim - 1;  // byte offset (from a) of the range's last byte
     const uint32_t tail = (uint32_t)(g.lim & 3u);
-    const uint32_t mhi = tail ? 0xFFFFFFFFu >> (8u * (4u - tail)) : 0xFFFFFFFFu;
-    const uint64_t lrow = last >> 8;
-    uint32_t rl = (lane == (uint32_t)((last >> 2) & 63u) && (lrow >> 4) == k) ? (uint32_t)(lrow & 15u) : 0xFFFFu;
-    asm volatile("" : "+v"(rl));
+    if (tail && k + 1 == g.nb) {  // uniform: only a range's last block has bytes after its end
+        const uint32_t mhi = 0xFFFFFFFFu >> (8u * (4u - tail));
+        const uint64_t lrow = last >> 8;
+        uint32_t rl = lane == (uint32_t)((last >> 2) & 63u) ? (uint32_t)(lrow & 15u) : 0xFFFFu;
+        asm volatile("" : "+v"(rl));
 #pragma unroll
-    for (int j = 0; j < 16; j++) w[j] = rl == (uint32_t)j ? w[j] & mhi : w[j];
+        for (int j = 0; j < 16; j++) w[j] = rl == (uint32_t)j ? w[j] & mhi : w[j];
+    }
     if (k == 0) {  // uniform
         uint32_t lo = lane == 0 ? 0xFFFFFFFFu << (8u * g.head) : 0xFFFFFFFFu;
         uint32_t init = 0u;
