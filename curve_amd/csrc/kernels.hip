@@ -381,7 +381,7 @@ __device__ __forceinline__ uint32_t xpow_wave(uint64_t n, uint32_t lane) {
 // ---------------------------------------------------------------------------
 // CRC32C of arbitrary byte ranges (WAL entries on replay, raw-file hashes).
 // The range [off, off+len) is viewed as whole 256-byte rows starting at the
-// 4-byte-aligned address a = off & ~3, bytes before off and at/after off+len
+// row-aligned address a = off & ~255, bytes before off and at/after off+len
 // masked to zero.  Leading zeros do not change a zero-init (raw) CRC, so the
 // page-kernel chain yields raw(data' || 0^t) = x^(8t) raw(data'), t = pad after
 // the range in its last 4 KiB block; multiplying by x^(-8t) removes the pad.  butil's
@@ -397,7 +397,7 @@ __device__ __forceinline__ uint32_t xpow_wave(uint64_t n, uint32_t lane) {
 // offset for rows past the range (no branches around them: exact vmcnt waits).
 // ---------------------------------------------------------------------------
 struct RangeGeo {
-    uint64_t a;      // 4-byte-aligned start
+    uint64_t a;      // 256-byte-aligned start
     uint64_t lim;    // bytes from a to the range's end
     uint64_t len;
     uint32_t head;   // off - a
@@ -406,7 +406,7 @@ struct RangeGeo {
 };
 __device__ __forceinline__ RangeGeo range_geo(uint64_t off, uint64_t len) {
     RangeGeo g;
-    g.a = off & ~3ull;
+    g.a = off & ~255ull;  // row-aligned: a 256-byte row load touches 2 cache lines, not 3
     g.head = (uint32_t)(off - g.a);
     g.len = len;
     g.lim = len + g.head;
@@ -443,12 +443,17 @@ __device__ __forceinline__ void mask_range_block(uint32_t (&w)[16], const RangeG
 #pragma unroll
         for (int j = 0; j < 16; j++) w[j] = rl == (uint32_t)j ? w[j] & mhi : w[j];
     }
-    if (k == 0) {  // uniform
-        uint32_t lo = lane == 0 ? 0xFFFFFFFFu << (8u * g.head) : 0xFFFFFFFFu;
-        uint32_t init = 0u;
-        if (g.len >= 4) init = lane == 0 ? 0xFFFFFFFFu << (8u * g.head)
-                                         : (lane == 1 && g.head ? 0xFFFFFFFFu >> (8u * (4u - g.head)) : 0u);
+    if (k == 0) {  // uniform: row 0 holds the bytes before the range (head < 256) and its first 4
+        const uint32_t hl = g.head >> 2, hb = g.head & 3u;
+        const uint32_t lo = lane < hl ? 0u : (lane == hl ? 0xFFFFFFFFu << (8u * hb) : 0xFFFFFFFFu);
+        uint32_t init = 0u, spill = 0u;  // butil's ~0 init over the range's first 4 bytes
+        if (g.len >= 4) {
+            const uint32_t rest = hb ? 0xFFFFFFFFu >> (8u * (4u - hb)) : 0u;  // bytes of it in the next dword
+            init = lane == hl ? 0xFFFFFFFFu << (8u * hb) : (lane == hl + 1 ? rest : 0u);
+            spill = (hl == 63u && lane == 0) ? rest : 0u;  // next dword is row 1, lane 0
+        }
         w[0] = (w[0] & lo) ^ init;
+        w[1] ^= spill;
     }
 }
 
