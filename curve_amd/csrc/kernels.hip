@@ -418,16 +418,16 @@ __device__ __forceinline__ RangeGeo range_geo(uint64_t off, uint64_t len) {
 // Block k of range g (16 rows, lane l holds dwords l + 64j of the block).
 __device__ __forceinline__ void load_range_block(uint32_t (&w)[16], const unsigned char* buf, const RangeGeo& g,
                                                  uint32_t k, uint32_t lane) {
-    const __amdgpu_buffer_rsrc_t r =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(buf + g.a + ((uint64_t)k << 12)), 0, 4096u,
-                                          kBufFlags);
+    // the descriptor's record count ends the block at the range's last dword
+    // (rounded up to 4 bytes: a dword that starts inside the range is in
+    // bounds, the next one is not, whether the unit tests the dword's start or
+    // its end), so rows past the range read 0 with no per-row select
     const uint64_t rem = g.lim - ((uint64_t)k << 12);  // > 0 for every block of the range
-    // bytes of the block left after this lane's dword in row 0: row j's dword
-    // starts inside the range iff 256 j < left (one compare + select per row)
-    const int32_t left = (int32_t)(rem > 4096u ? 4096u : (uint32_t)rem) - (int32_t)(4u * lane);
+    const uint32_t nr = rem >= 4096u ? 4096u : (((uint32_t)rem + 3u) & ~3u);
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(buf + g.a + ((uint64_t)k << 12)), 0, nr, kBufFlags);
 #pragma unroll
-    for (int j = 0; j < 16; j++)
-        w[j] = __builtin_amdgcn_raw_buffer_load_b32(r, left > 256 * j ? 4u * lane : kBufOOB, 256 * j, 2);
+    for (int j = 0; j < 16; j++) w[j] = __builtin_amdgcn_raw_buffer_load_b32(r, 4u * lane + 256u * j, 0, 2);
 }
 
 // Zero the bytes outside the range (first / last dword) and fold butil's init
