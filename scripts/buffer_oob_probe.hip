@@ -11,8 +11,13 @@ __global__ void probe(const unsigned char* buf, uint32_t nr, uint32_t* out) {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(buf), 0, nr, 0x00020000u);
     const uint32_t t = threadIdx.x;  // byte offset t (0..23) as voffset
     out[t] = __builtin_amdgcn_raw_buffer_load_b32(r, t, 0, 0);
-    // same byte offsets with the constant part in the immediate field: voffset t&~7, imm t&7
-    out[32 + t] = __builtin_amdgcn_raw_buffer_load_b32(r, (t & ~7u) + 0u, 0, 0);
+    // offsets that wrap when 4 is added in 32 bits (0xFFFFFFFC..0xFFFFFFFF), 0x80000000,
+    // and -256..-1 style negatives: OOB only if the unit checks without 32-bit wrap
+    if (t < 8) {
+        const uint32_t big[8] = {0xFFFFFFFCu, 0xFFFFFFFDu, 0xFFFFFFFEu, 0xFFFFFFFFu,
+                                 0x80000000u, 0xFFFFFF00u, 0xFFFFFFF8u, 0x7FFFFFFCu};
+        out[32 + t] = __builtin_amdgcn_raw_buffer_load_b32(r, big[t], 0, 0);
+    }
 }
 
 int main() {
@@ -29,6 +34,10 @@ int main() {
     if (hipMemcpy(ho, o, sizeof ho, hipMemcpyDeviceToHost) != hipSuccess) return 1;
     printf("{\"num_records\": %u, \"loads\": [", nr);
     for (int t = 0; t < 24; t++) printf("%s{\"offset\": %d, \"value\": \"0x%08x\"}", t ? ", " : "", t, ho[t]);
+    printf("], \"wrap_probe\": [");
+    const char* names[8] = {"0xFFFFFFFC", "0xFFFFFFFD", "0xFFFFFFFE", "0xFFFFFFFF", "0x80000000", "0xFFFFFF00",
+                            "0xFFFFFFF8", "0x7FFFFFFC"};
+    for (int t = 0; t < 8; t++) printf("%s{\"offset\": \"%s\", \"value\": \"0x%08x\"}", t ? ", " : "", names[t], ho[32 + t]);
     printf("]}\n");
     return 0;
 }
