@@ -36,7 +36,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=10, help="untimed steps: the first ~7 launches after idle run slow while clocks ramp")
     p.add_argument("--chunks", type=int, default=1024, help="chunks per GPU")
     p.add_argument("--page-bytes", type=int, default=4096)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (rank 0, N=1)")
