@@ -457,19 +457,23 @@ __device__ __forceinline__ void mask_range_block(uint32_t (&w)[16], const RangeG
     }
 }
 
-__global__ __launch_bounds__(kBlockThreads) void range_crc_kernel(const unsigned char* __restrict__ buf,
+#ifndef CC_RANGE_WAVES
+#define CC_RANGE_WAVES 12  // waves per CU of the range kernel (A/B: 12 ~3 % over 8, 16 equal)
+#endif
+constexpr int kRangeWaves = CC_RANGE_WAVES;
+__global__ __launch_bounds__(64 * kRangeWaves) void range_crc_kernel(const unsigned char* __restrict__ buf,
                                                                   const RangeDesc* __restrict__ ranges, uint64_t n,
                                                                   const uint4* __restrict__ image,
                                                                   uint32_t* __restrict__ out) {
     __shared__ uint32_t tab[kLdsBytes / 4];
-    fill_lds(tab, image);
+    fill_lds<64 * kRangeWaves>(tab, image);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t c0 = lane << 2 & 0x7Cu;
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
-    const uint64_t W = (uint64_t)gridDim.x * kWavesPerBlock;
-    for (uint64_t base = (uint64_t)blockIdx.x * kWavesPerBlock + wave; base < n; base += 64u * W) {
+    const uint64_t W = (uint64_t)gridDim.x * kRangeWaves;
+    for (uint64_t base = (uint64_t)blockIdx.x * kRangeWaves + wave; base < n; base += 64u * W) {
         const uint64_t ri = base + (uint64_t)lane * W;
         const bool valid = ri < n;
         const RangeDesc rd = ranges[valid ? ri : base];
@@ -1323,7 +1327,7 @@ hipError_t upload_xinv(const uint32_t* table) { return hipMemcpyToSymbol(HIP_SYM
 hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, const void* image,
                             uint32_t* out, int blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(range_crc_kernel, dim3(blocks), dim3(kBlockThreads), 0, s, buf, ranges, n,
+    hipLaunchKernelGGL(range_crc_kernel, dim3(blocks), dim3(64 * kRangeWaves), 0, s, buf, ranges, n,
                        static_cast<const uint4*>(image), out);
     return hipGetLastError();
 }
