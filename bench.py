@@ -40,6 +40,7 @@ def parse():
     p.add_argument("--chunks", type=int, default=1024, help="chunks per GPU")
     p.add_argument("--page-bytes", type=int, default=4096)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (rank 0, N=1)")
+    p.add_argument("--cpu-sample-chunks", type=int, default=256, help="CPU baseline sample: 16 MiB chunks (256 = 4 GiB)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--e2e-gib", type=float, default=1.0, help="pinned host buffer for the e2e leg")
@@ -59,49 +60,76 @@ def log(rank, *a):
         print("[bench]", *a, flush=True)
 
 
+def host_cores():
+    """Threads this process may run on (the cpuset, not the machine: a GPU box
+    hands each GPU a share of a larger host) and the cgroup CPU quota if any."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return aff, quota
+
+
 def cpu_baseline(pool, args, rank):
     """Reference CPU path restated (oracle, single-stream SSE4.2 crc32q as butil
-    builds it) timed on this host over a bounded sample of the same workload:
-    whole chunks copied from HBM, hashed page by page with CRC32(page, 4096)."""
+    builds it, one CRC32(page, 4096) call per page) timed on this host over a
+    DRAM-resident sample of the same workload: `--cpu-sample-chunks` 16 MiB
+    chunks (default 256 = 4 GiB, far above the L3) copied from HBM.  Timed at
+    1 thread and at every core this process may use (page-partitioned), plus a
+    cache-resident microbench of libcurvecrc's own CPU primitive (3-way crc32q)
+    against the single-stream oracle at 4 KiB and 64 KiB per call."""
+    import ctypes
     import sys
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
-    sample_chunks = min(16, pool.n)
+    sample_chunks = min(args.cpu_sample_chunks, pool.n)
     host = pool.data[:sample_chunks].cpu().numpy()
-    dev_crcs = pool.page_crcs[: sample_chunks * (pool.chunk_size // args.page_bytes)].cpu().numpy().view(np.uint32)
-    want = O.page_crcs(host, args.page_bytes)
-    parity = bool((want == dev_crcs).all())
+    pages_per_chunk = pool.chunk_size // args.page_bytes
+    dev_crcs = pool.page_crcs[: sample_chunks * pages_per_chunk].cpu().numpy().view(np.uint32)
+    aff, quota = host_cores()
+    threads_all = max(1, aff if quota is None else min(aff, int(quota)))
     res = {}
-    for threads, budget in ((1, args.cpu_seconds), (16, max(1.0, args.cpu_seconds / 4))):
+    for threads, budget in ((1, args.cpu_seconds), (threads_all, max(2.0, args.cpu_seconds / 2))):
         nbytes, t0 = 0, time.perf_counter()
         while True:
-            O.page_crcs(host, args.page_bytes, threads=threads)
+            want = O.page_crcs(host, args.page_bytes, threads=threads)
             nbytes += host.nbytes
             el = time.perf_counter() - t0
             if el >= budget:
                 break
         res[threads] = (nbytes / GiB / el, nbytes, el)
-    # libcurvecrc's own CPU primitive (3-way crc32q, the drop-in for
-    # curve::common::CRC32 on small/CPU-side buffers), whole chunks per call
+    parity = bool((want == dev_crcs).all())
+    # cache-resident per-call rate: the product's crc32c_extend vs the oracle's
+    # single stream, both driven by the same C loop (no Python per call)
     from curve_amd import _lib
-    L = _lib.lib()
-    nbytes, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < 2.0:
-        for k in range(sample_chunks):
-            L.crc32c_value(host[k].ctypes.data, host[k].nbytes)
-            nbytes += host[k].nbytes
-    prim = nbytes / GiB / (time.perf_counter() - t0)
+    L, P = O.lib(), _lib.lib()
+    L.oc_time_calls.restype = ctypes.c_double
+    L.oc_time_calls.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p]
+    buf = host[0, : 1 << 16]
+    micro = {}
+    for n in (4096, 65536):
+        for name, fn in (("oracle_single_stream", L.oc_crc32c_sse42), ("libcurvecrc_3way", P.crc32c_extend)):
+            it = max(1, (2 << 30) // n)  # 2 GiB per measurement
+            t = L.oc_time_calls(ctypes.cast(fn, ctypes.c_void_p).value, buf.ctypes.data, n, it, None)
+            micro[f"{name}_{n // 1024}KiB_GiBps"] = round(it * n / GiB / t, 2)
     v1, nb1, el1 = res[1]
-    v16, _, _ = res[16]
+    vN, nbN, elN = res[threads_all]
     return {
         "value": round(v1, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-        "sample": f"{sample_chunks} x 16 MiB chunks copied from HBM, CRC32(page, {args.page_bytes}) per page, "
-                  f"{nb1 / GiB:.1f} GiB hashed in {el1:.1f} s (oracle/crc32c_oracle.c oc_crc32c_sse42, "
-                  f"single-stream crc32q as butil builds it)",
-        "value_16_threads": round(v16, 3),
+        "sample": f"{sample_chunks} x 16 MiB chunks ({sample_chunks * pool.chunk_size / GiB:.1f} GiB, DRAM-resident) "
+                  f"copied from HBM, CRC32(page, {args.page_bytes}) per page, {nb1 / GiB:.1f} GiB hashed in {el1:.1f} s "
+                  "(oracle/crc32c_oracle.c oc_crc32c_sse42, single-stream crc32q as butil builds it)",
+        "all_cores": {"value": round(vN, 3), "cores": threads_all, "seconds": round(elN, 2),
+                      "hashed_GiB": round(nbN / GiB, 1), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                      "machine_cpus": os.cpu_count()},
         "parity_vs_device": parity,
         "cpu_model": cpu_model(),
-        "lib_cpu_primitive_GiBps": round(prim, 3),
+        "per_call_cache_resident": micro,
     }
 
 
@@ -133,65 +161,93 @@ def e2e_leg(args, dev):
     return round(reps * nb / GiB / el, 2)
 
 
-def stream_leg(args):
-    """BASELINE config 4: scan-service stream of `--stream-chunks` x 16 MiB chunk
-    files from host memory (pinned, as pread into pinned buffers would leave
-    them), pipelined H2D + hashing (cc_scan_host), ScanMap slice CRCs + file CRCs,
-    then the per-copyset digests (100 chunks per copyset).  A pinned pool of 64
-    distinct chunk files is re-referenced to keep host RAM bounded."""
+def _stream_sources(n, pool_n, rank=0):
+    """`pool_n` distinct pinned 16 MiB data chunks (re-referenced round robin:
+    10,000 distinct chunks would need 156 GiB of host RAM) and `n` DISTINCT
+    pinned metapages (sn = global chunk index), so every chunk FILE -- metapage
+    || data -- and its file CRC differ."""
     from curve_amd import crc as C
-    from curve_amd.pool import copyset_layout
-    n = args.stream_chunks
-    pool_n = 64
+    from curve_amd.chunkfile import ChunkFileMetaPage
     data = torch.empty((pool_n, C.CHUNK_SIZE), dtype=torch.uint8, pin_memory=True)
     data.random_(0, 256)
-    meta = torch.zeros((pool_n, C.META_PAGE_SIZE), dtype=torch.uint8, pin_memory=True)
-    meta[:, 0] = 2
-    dn, mn = data.numpy(), meta.numpy()
-    chunks = [(mn[i % pool_n], dn[i % pool_n]) for i in range(n)]
-    C.scan_host(chunks[:8])  # warm
-    t0 = time.perf_counter()
-    mc, sc, fc = C.scan_host(chunks)
-    el = time.perf_counter() - t0
-    per = 100
-    lay = copyset_layout(list(range(n)), [i // per for i in range(n)], [C.CHUNK_SIZE + C.META_PAGE_SIZE] * n)
-    dig = [0] * lay.n_groups
+    meta = torch.zeros((n, C.META_PAGE_SIZE), dtype=torch.uint8, pin_memory=True)
+    mn = meta.numpy()
     for i in range(n):
-        dig[lay.group[i]] ^= C.shift(int(fc[i]), lay.after_bytes[i])
-    el_all = time.perf_counter() - t0
-    return {"chunks": n, "GiBps_e2e": round(n * (C.CHUNK_SIZE + C.META_PAGE_SIZE) / GiB / el, 2),
-            "seconds": round(el, 3), "with_digest_seconds": round(el_all, 3), "copysets": lay.n_groups,
-            "scan_maps": int(sc.size + mc.size), "source": "pinned host pool of 64 chunk files, re-referenced"}
+        mn[i] = np.frombuffer(ChunkFileMetaPage(sn=rank * n + i + 1).encode(), dtype=np.uint8)
+    dn = data.numpy()
+    return dn, mn, [(mn[i], dn[i % pool_n]) for i in range(n)]
+
+
+def _stream_expected(dn, mn, n, pool_n, lay, lo):
+    """Expected CRCs of the stream from libcurvecrc's CPU primitive (not the
+    oracle): slice CRCs of the distinct data chunks, every metapage CRC, file
+    CRC = combine(metapage, data, 16 MiB), digest = XOR of shifted file CRCs."""
+    from curve_amd import crc as C
+    S = C.CHUNK_SIZE // C.SCAN_SIZE
+    sl = np.array([[C.CRC32(dn[k][j * C.SCAN_SIZE:(j + 1) * C.SCAN_SIZE]) for j in range(S)] for k in range(pool_n)],
+                  dtype=np.uint32)
+    dc = np.empty(pool_n, dtype=np.uint32)
+    for k in range(pool_n):  # chunk data CRC = the slices chained
+        c = int(sl[k][0])
+        for j in range(1, S):
+            c = C.combine(c, int(sl[k][j]), C.SCAN_SIZE)
+        dc[k] = c
+    mc = np.array([C.CRC32(mn[i]) for i in range(n)], dtype=np.uint32)
+    fc = np.array([C.combine(int(mc[i]), int(dc[i % pool_n]), C.CHUNK_SIZE) for i in range(n)], dtype=np.uint32)
+    dig = np.zeros(lay.n_groups, dtype=np.uint32)
+    for i in range(n):
+        dig[lay.group[lo + i]] ^= C.shift(int(fc[i]), lay.after_bytes[lo + i])
+    return mc, sl, fc, dig
+
+
+def stream_leg(args):
+    """BASELINE config 4: scan-service stream of `--stream-chunks` x 16 MiB chunk
+    files from pinned host memory (as pread into pinned buffers would leave
+    them): pipelined H2D + page kernel + fused epilogue per batch, ScanMap
+    slice CRCs, file CRCs AND the per-copyset digests (100 chunks per copyset)
+    computed on the device -- ONE cc_scan_host_digest call.  Every output is
+    checked afterwards against libcurvecrc's CPU primitive."""
+    from curve_amd import crc as C
+    from curve_amd.pool import copyset_layout
+    n, pool_n, per = args.stream_chunks, 64, 100
+    dn, mn, chunks = _stream_sources(n, pool_n)
+    lay = copyset_layout(list(range(n)), [i // per for i in range(n)], [C.CHUNK_SIZE + C.META_PAGE_SIZE] * n)
+    C.scan_host(chunks[:8])  # warm (staging)
+    t0 = time.perf_counter()
+    mc, sc, fc, dig = C.scan_host(chunks, after_bytes=lay.after_bytes, group=lay.group, n_groups=lay.n_groups)
+    el = time.perf_counter() - t0
+    w_mc, w_sl, w_fc, w_dig = _stream_expected(dn, mn, n, pool_n, lay, 0)
+    bad = {"meta": int((mc != w_mc).sum()), "slices": int((sc != w_sl[np.arange(n) % pool_n]).sum()),
+           "files": int((fc != w_fc).sum()), "digests": int((dig != w_dig).sum())}
+    out = {"chunks": n, "GiBps_e2e": round(n * (C.CHUNK_SIZE + C.META_PAGE_SIZE) / GiB / el, 2),
+           "seconds": round(el, 3), "copysets": lay.n_groups, "scan_maps": int(sc.size + mc.size),
+           "digest": "device (fused epilogue, cc_scan_host_digest)",
+           "crc_check": {"vs": "libcurvecrc CPU primitive", "mismatches": bad, "ok": not any(bad.values())},
+           "source": f"{n} distinct pinned metapages + {pool_n} distinct pinned 16 MiB data chunks (re-referenced)"}
+    assert out["crc_check"]["ok"], f"stream leg CRC mismatch: {bad}"
+    return out
 
 
 def stream_all_ranks_leg(args, rank, world, dev):
     """Config 5 end to end: each rank streams `--stream-chunks-per-rank` chunk
-    files (a pinned pool of 64 distinct files, re-referenced) through
-    cc_scan_host on its own GPU, computes its copysets' digest partials from the
-    file CRCs and joins the digest exchange; aggregate = all ranks' bytes / the
-    slowest rank's time (barrier on both sides)."""
+    files from pinned host memory through cc_scan_host_digest on its own GPU
+    (file CRCs + per-copyset digest partials on the device), then joins the
+    digest exchange; aggregate = all ranks' bytes / the slowest rank's time
+    (barrier on both sides).  Rank 0 checks the exchanged digests against the
+    CPU primitive over every rank's chunks."""
     from curve_amd import crc as C
     from curve_amd.pool import copyset_layout, reduce_digests
-    n = args.stream_chunks_per_rank
-    pool_n = 64
-    data = torch.empty((pool_n, C.CHUNK_SIZE), dtype=torch.uint8, pin_memory=True)
-    data.random_(0, 256)
-    meta = torch.zeros((pool_n, C.META_PAGE_SIZE), dtype=torch.uint8, pin_memory=True)
-    meta[:, 0] = 2
-    dn, mn = data.numpy(), meta.numpy()
-    chunks = [(mn[i % pool_n], dn[i % pool_n]) for i in range(n)]
+    n, pool_n, per = args.stream_chunks_per_rank, 64, 100
     total = n * world
-    per = 100  # chunks per copyset, over the whole pool
     lay = copyset_layout(list(range(total)), [i // per for i in range(total)],
                          [C.CHUNK_SIZE + C.META_PAGE_SIZE] * total)
+    dn, mn, chunks = _stream_sources(n, pool_n, rank)
+    lo = rank * n
     C.scan_host(chunks[:4])  # warm
     dist.barrier()
     t0 = time.perf_counter()
-    _, _, fc = C.scan_host(chunks)
-    part = np.zeros(lay.n_groups, dtype=np.uint32)
-    lo = rank * n
-    for i in range(n):
-        part[lay.group[lo + i]] ^= C.shift(int(fc[i]), lay.after_bytes[lo + i])
+    *_, part = C.scan_host(chunks, after_bytes=lay.after_bytes[lo:lo + n], group=lay.group[lo:lo + n],
+                           n_groups=lay.n_groups)
     dig = reduce_digests(torch.from_numpy(part.view(np.int32)).to(dev), dist)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
@@ -199,10 +255,14 @@ def stream_all_ranks_leg(args, rank, world, dev):
                      device="cpu" if dist.get_backend() == "gloo" else dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
+    # untimed check: every rank's expected partial, XORed, == the exchanged digests
+    *_, w_part = _stream_expected(dn, mn, n, pool_n, lay, lo)
+    want = reduce_digests(torch.from_numpy(w_part.view(np.int32)).to(dev), dist)
+    ok = bool((dig.cpu().numpy().view(np.uint32) == want.cpu().numpy().view(np.uint32)).all())
     return {"chunks_per_rank": n, "ranks": world, "seconds_max_rank": round(el, 3),
             "GiBps_e2e_aggregate": round(total * (C.CHUNK_SIZE + C.META_PAGE_SIZE) / GiB / el, 2),
-            "copysets": lay.n_groups, "digests": int(dig.numel()),
-            "source": "pinned host pool of 64 chunk files per rank, re-referenced; cc_scan_host per rank"}
+            "copysets": lay.n_groups, "digests": int(dig.numel()), "digest_check_ok": ok,
+            "source": "pinned host chunk files per rank; cc_scan_host_digest per rank + digest exchange"}
 
 
 def files_leg(args):
@@ -423,15 +483,47 @@ def load_traffic(args):
     return t.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
 
 
+def launch_ranks(args):
+    """`--gpus N` is honoured whoever starts the bench: under torchrun (the
+    driver's multi-GPU form) WORLD_SIZE must equal N; started plainly with
+    N > 1, the bench starts one rank per GPU itself -- torch.distributed.run as
+    a CHILD process, before this process touches the GPU -- and exits with its
+    status."""
+    import subprocess
+    import sys
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(json.dumps({"error": f"--gpus {args.gpus} but WORLD_SIZE={ws}: refusing to report a "
+                                       f"{ws}-rank run as {args.gpus} GPUs"}), flush=True)
+            sys.exit(2)
+        return
+    if args.gpus <= 1:
+        return
+    import socket
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
 def main():
     args = parse()
+    launch_ranks(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; BENCH_DIST_BACKEND=gloo + more ranks than GPUs only to
     # rehearse the multi-rank flow on a 1-GPU box (the driver uses nccl = RCCL)
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()
+    if world > 1 and backend == "nccl" and ndev < int(os.environ.get("LOCAL_WORLD_SIZE", world)):
+        raise SystemExit(f"{world} ranks need {world} GPUs, {ndev} visible (BENCH_DIST_BACKEND=gloo rehearses "
+                         "the multi-rank flow on fewer)")
+    local = local % max(1, ndev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -599,7 +691,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_e2e:
         out["e2e_pinned_GiBps"] = e2e_leg(args, dev)
         if args.stream_chunks:
-            out["stream"] = stream_leg(args)
+            try:
+                out["stream"] = stream_leg(args)
+            except Exception as e:  # a CRC mismatch is reported in the line, never hidden
+                out["stream"] = {"error": repr(e)}
         if args.file_chunks:
             out["files"] = files_leg(args)
     if rank == 0:

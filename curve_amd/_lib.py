@@ -21,6 +21,8 @@ CC_ENOMEM = -12
 CC_EHIP = -5
 CC_ECORRUPT = -74
 CC_ECOMM = -71
+CC_EIO = -5001
+CC_ESTALE = -116
 CC_COMM_ID_BYTES = 128
 
 # every symbol include/curve_crc.h declares: (name, restype, argtypes)
@@ -39,6 +41,14 @@ class CcChunkSrc(ctypes.Structure):
     _fields_ = [("meta", _vp), ("data", _vp)]
 
 
+class CcScanDigest(ctypes.Structure):  # include/curve_crc.h cc_scan_digest
+    _fields_ = [("h_after_bytes", _vp), ("h_group", _vp), ("n_groups", _u64), ("h_digest", _vp)]
+
+
+class IoVec(ctypes.Structure):  # struct iovec
+    _fields_ = [("iov_base", _vp), ("iov_len", _sz)]
+
+
 class CcPoolShard(ctypes.Structure):  # include/curve_crc.h cc_pool_shard
     _fields_ = [("d_data", _vp), ("d_meta", _vp), ("n_chunks", _u64), ("chunk_bytes", _u32),
                 ("meta_bytes", _u32), ("page_bytes", _u32), ("slice_bytes", _u32), ("d_after_mult", _vp),
@@ -54,6 +64,12 @@ SIGNATURES = {
     "crc32c_shift": (_u32, [_u32, _u64]),
     "crc32c_zeros": (_u32, [_u64]),
     "cc_fold_host": (_u32, [_vp, _u64, _u64]),
+    "crc32c_extend_iov": (_u32, [_u32, _vp, _sz]),
+    "cc_slice_fold": (_int, [_vp, _u64, _u32, _u32, _vp]),
+    "cc_crc_bufs_host": (_int, [_vp, _vp, _u64, _vp]),
+    "cc_digest_fold_dev": (_int, [_vp, _u32, _u64, _vp, _vp]),
+    "cc_scan_host_digest": (_int, [ctypes.POINTER(CcChunkSrc), _u64, _u32, _u32, _u32, _u32, _vp, _vp, _vp,
+                                   ctypes.POINTER(CcScanDigest)]),
     "cc_engine_init": (_int, [ctypes.POINTER(CcOpts)]),
     "cc_engine_fini": (_int, []),
     "cc_device_count": (_int, []),

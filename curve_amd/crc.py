@@ -55,6 +55,42 @@ def CRC32(*args) -> int:
     return int(lib().crc32c_extend(int(crc) & 0xFFFFFFFF, p, n))
 
 
+def CRC32_iov(fragments, crc: int = 0) -> int:
+    """crc32c_extend_iov: one CRC over a scattered buffer, as braft::crc32(const
+    butil::IOBuf&) extends it across the IOBuf's blocks (raftlog/curve_segment.cpp:405)."""
+    keep = [_host_buf(f) for f in fragments]
+    iov = (_lib.IoVec * max(1, len(keep)))()
+    for i, (p, n, _k) in enumerate(keep):
+        iov[i].iov_base = ctypes.cast(p, ctypes.c_void_p).value if n else None
+        iov[i].iov_len = n
+    return int(lib().crc32c_extend_iov(int(crc) & 0xFFFFFFFF, iov, len(keep)))
+
+
+def slice_fold(page_crcs, pages_per_slice: int, page_bytes: int = PAGE_SIZE):
+    """cc_slice_fold: page CRCs -> one CRC per slice of pages_per_slice pages (host)."""
+    import numpy as np
+    a = np.ascontiguousarray(page_crcs, dtype=np.uint32)
+    if pages_per_slice <= 0 or a.size % pages_per_slice:
+        raise CurveCrcError(_lib.CC_EINVAL, "page count is not a multiple of pages_per_slice")
+    out = np.empty(a.size // pages_per_slice, dtype=np.uint32)
+    check(lib().cc_slice_fold(ctypes.c_void_p(a.ctypes.data), a.size, pages_per_slice, page_bytes,
+                              ctypes.c_void_p(out.ctypes.data)), "cc_slice_fold")
+    return out
+
+
+def crc_bufs_host(bufs):
+    """cc_crc_bufs_host: CRC32 of every host buffer in one blocking device call."""
+    import numpy as np
+    keep = [_host_buf(b) for b in bufs]
+    n = len(keep)
+    ptrs = (ctypes.c_void_p * max(1, n))(*[ctypes.cast(p, ctypes.c_void_p).value for p, _, _ in keep])
+    lens = np.array([k[1] for k in keep], dtype=np.uint64)
+    out = np.empty(n, dtype=np.uint32)
+    check(lib().cc_crc_bufs_host(ptrs, ctypes.c_void_p(lens.ctypes.data), n, ctypes.c_void_p(out.ctypes.data)),
+          "cc_crc_bufs_host")
+    return out
+
+
 def combine(crc_a: int, crc_b: int, len_b: int) -> int:
     return int(lib().crc32c_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, int(len_b)))
 
@@ -101,6 +137,22 @@ def _stream_handle(stream) -> Optional[int]:
     return ctypes.c_void_p(stream.cuda_stream)
 
 
+def _on_stream(stream):
+    """Context in which tensors are created on `stream` (the stream the native
+    call enqueues on), so an output's initialisation (torch.full / zeros) is
+    ordered before the kernel that writes it."""
+    import contextlib
+    torch = _torch()
+    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
+
+def _stream_key(device, stream):
+    """Cache key of per-stream scratch: (device, HIP stream handle)."""
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return (device, s.cuda_stream)
+
+
 def _dev_ptr(t, what: str):
     if not t.is_cuda:
         raise CurveCrcError(_lib.CC_EINVAL, f"{what} must be a device tensor")
@@ -143,7 +195,8 @@ def page_verify(pages, expected, page_bytes: int = PAGE_SIZE, stream=None, count
     if expected.numel() < n or expected.element_size() != 4:
         raise CurveCrcError(_lib.CC_EINVAL, "expected must hold one 32-bit CRC per page")
     if counters is None:
-        counters = torch.tensor([0, -1], dtype=torch.int64, device=pages.device)
+        with _on_stream(stream):
+            counters = torch.tensor([0, -1], dtype=torch.int64, device=pages.device)
     base = counters.data_ptr()
     with torch.cuda.device(pages.device):
         check(lib().cc_page_verify_dev(_dev_ptr(pages, "pages"), n, page_bytes, _dev_ptr(expected, "expected"),
@@ -170,8 +223,9 @@ def page_verify_list(pages, expected, page_bytes: int = PAGE_SIZE, max_bad: int 
     n = nb // page_bytes
     if expected.numel() < n or expected.element_size() != 4:
         raise CurveCrcError(_lib.CC_EINVAL, "expected must hold one 32-bit CRC per page")
-    counters = torch.tensor([0, -1], dtype=torch.int64, device=pages.device)
-    bad = torch.full((max(1, max_bad),), -1, dtype=torch.int64, device=pages.device)
+    with _on_stream(stream):
+        counters = torch.tensor([0, -1], dtype=torch.int64, device=pages.device)
+        bad = torch.full((max(1, max_bad),), -1, dtype=torch.int64, device=pages.device)
     base = counters.data_ptr()
     with torch.cuda.device(pages.device):
         check(lib().cc_page_verify_list_dev(_dev_ptr(pages, "pages"), n, page_bytes, _dev_ptr(expected, "expected"),
@@ -224,9 +278,10 @@ def crc_ranges(buf, offsets, lengths, out=None, stream=None):
         raise CurveCrcError(_lib.CC_EINVAL, "range beyond the buffer")
     rec = np.empty((offs.size, 2), dtype=np.uint64)
     rec[:, 0], rec[:, 1] = offs, lens
-    d_rec = torch.from_numpy(rec.view(np.uint8).reshape(-1)).to(buf.device)
-    if out is None:
-        out = torch.empty(offs.size, dtype=torch.int32, device=buf.device)
+    with _on_stream(stream):
+        d_rec = torch.from_numpy(rec.view(np.uint8).reshape(-1)).to(buf.device)
+        if out is None:
+            out = torch.empty(offs.size, dtype=torch.int32, device=buf.device)
     with torch.cuda.device(buf.device):
         check(lib().cc_crc_ranges_dev(_dev_ptr(buf, "buf"), _dev_ptr(d_rec, "ranges"), offs.size,
                                       _dev_ptr(out, "out"), _stream_handle(stream)), "cc_crc_ranges_dev")
@@ -276,6 +331,20 @@ def combine_dev(a, b, len_b: int, out=None, stream=None):
     return out
 
 
+def digest_fold_dev(gathered, nranks: int, out=None, stream=None):
+    """cc_digest_fold_dev: gathered [nranks * n] int32 device partials -> XOR over ranks [n]."""
+    torch = _torch()
+    if nranks <= 0 or gathered.numel() % nranks:
+        raise CurveCrcError(_lib.CC_EINVAL, "gathered size is not a multiple of nranks")
+    n = gathered.numel() // nranks
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=gathered.device)
+    with torch.cuda.device(gathered.device):
+        check(lib().cc_digest_fold_dev(_dev_ptr(gathered, "gathered"), nranks, n, _dev_ptr(out, "out"),
+                                       _stream_handle(stream)), "cc_digest_fold_dev")
+    return out
+
+
 def digest_dev(file_crcs, after_bytes, group, n_groups: int, out=None, stream=None):
     """Per-copyset digest partials: out[group[i]] ^= shift(file_crcs[i], after_bytes[i])."""
     torch = _torch()
@@ -305,10 +374,13 @@ def page_crc_host(data, page_bytes: int = PAGE_SIZE):
 
 
 def scan_host(chunks, chunk_bytes: int = CHUNK_SIZE, meta_bytes: int = META_PAGE_SIZE,
-              page_bytes: int = PAGE_SIZE, slice_bytes: int = SCAN_SIZE):
-    """Streaming scan of host-resident chunk files (cc_scan_host).
-    `chunks`: sequence of (meta, data) numpy uint8 arrays (pinned or pageable).
-    Returns (meta_crcs[n], slice_crcs[n, chunk/slice], file_crcs[n]) as uint32 numpy."""
+              page_bytes: int = PAGE_SIZE, slice_bytes: int = SCAN_SIZE, after_bytes=None, group=None,
+              n_groups: int = 0):
+    """Streaming scan of host-resident chunk files (cc_scan_host / cc_scan_host_digest).
+    `chunks`: sequence of (meta, data) numpy uint8 arrays (pinned or pageable, mixed).
+    Returns (meta_crcs[n], slice_crcs[n, chunk/slice], file_crcs[n]) as uint32 numpy;
+    with after_bytes / group / n_groups also the per-copyset digests [n_groups]
+    computed on the device (4th element)."""
     import numpy as np
     n = len(chunks)
     arr = (_lib.CcChunkSrc * max(n, 1))()
@@ -325,10 +397,21 @@ def scan_host(chunks, chunk_bytes: int = CHUNK_SIZE, meta_bytes: int = META_PAGE
     mc = np.empty(n, dtype=np.uint32)
     sc = np.empty((n, S), dtype=np.uint32)
     fc = np.empty(n, dtype=np.uint32)
-    check(lib().cc_scan_host(arr, n, chunk_bytes, meta_bytes, page_bytes, slice_bytes,
-                             ctypes.c_void_p(mc.ctypes.data), ctypes.c_void_p(sc.ctypes.data),
-                             ctypes.c_void_p(fc.ctypes.data)), "cc_scan_host")
-    return mc, sc, fc
+    if after_bytes is None:
+        check(lib().cc_scan_host(arr, n, chunk_bytes, meta_bytes, page_bytes, slice_bytes,
+                                 ctypes.c_void_p(mc.ctypes.data), ctypes.c_void_p(sc.ctypes.data),
+                                 ctypes.c_void_p(fc.ctypes.data)), "cc_scan_host")
+        return mc, sc, fc
+    ab = np.ascontiguousarray(after_bytes, dtype=np.uint64)
+    gr = np.ascontiguousarray(group, dtype=np.uint32)
+    if ab.size != n or gr.size != n:
+        raise CurveCrcError(_lib.CC_EINVAL, "after_bytes / group must hold one entry per chunk")
+    dig = np.empty(max(1, n_groups), dtype=np.uint32)
+    d = _lib.CcScanDigest(ab.ctypes.data, gr.ctypes.data, n_groups, dig.ctypes.data)
+    check(lib().cc_scan_host_digest(arr, n, chunk_bytes, meta_bytes, page_bytes, slice_bytes,
+                                    ctypes.c_void_p(mc.ctypes.data), ctypes.c_void_p(sc.ctypes.data),
+                                    ctypes.c_void_p(fc.ctypes.data), ctypes.byref(d)), "cc_scan_host_digest")
+    return mc, sc, fc, dig[:n_groups]
 
 
 UPDATE_DTYPE = None
@@ -365,19 +448,52 @@ def split_nonoverlapping(dst, lens):
     if new_cluster.all():
         return [np.arange(n)]  # no overlaps at all: one batch
     level = np.zeros(n, dtype=np.int64)
-    cid = np.cumsum(new_cluster) - 1
     starts = np.flatnonzero(new_cluster)
     sizes = np.diff(np.append(starts, n))
     for c in np.flatnonzero(sizes > 1):  # only the (few, small) overlapping clusters
         mem = np.sort(order[starts[c]:starts[c] + sizes[c]])  # original (write) order
-        for x, j in enumerate(mem):
-            lv = 0
-            for i in mem[:x]:
-                if dst[i] < end[j] and dst[j] < end[i]:
-                    lv = max(lv, level[i] + 1)
-            level[j] = lv
-    del cid
+        _cluster_levels(dst, end, mem, level)
     return [np.flatnonzero(level == v) for v in range(int(level.max()) + 1)]
+
+
+def _cluster_levels(dst, end, mem, level):
+    """Levels of one cluster of overlapping writes, in write order: a max
+    segment tree over the cluster's distinct endpoints (values = level + 1 of
+    the latest-levelled write covering each elementary segment): O(k log k)."""
+    import numpy as np
+    xs = np.unique(np.concatenate([dst[mem], end[mem]]))
+    size = 1
+    while size < xs.size - 1:
+        size <<= 1
+    mx = [0] * (2 * size)
+    tag = [0] * (2 * size)
+
+    def query(v, vl, vr, l, r):
+        if r <= vl or vr <= l:
+            return 0
+        if l <= vl and vr <= r:
+            return mx[v]
+        mid = (vl + vr) // 2
+        return max(tag[v], query(2 * v, vl, mid, l, r), query(2 * v + 1, mid, vr, l, r))
+
+    def update(v, vl, vr, l, r, val):
+        if r <= vl or vr <= l:
+            return
+        if l <= vl and vr <= r:
+            mx[v] = max(mx[v], val)
+            tag[v] = max(tag[v], val)
+            return
+        mid = (vl + vr) // 2
+        update(2 * v, vl, mid, l, r, val)
+        update(2 * v + 1, mid, vr, l, r, val)
+        mx[v] = max(mx[v], mx[2 * v], mx[2 * v + 1])
+
+    for j in mem:
+        l = int(np.searchsorted(xs, dst[j]))
+        r = int(np.searchsorted(xs, end[j]))
+        lv = query(1, 0, size, l, r)
+        level[j] = lv
+        update(1, 0, size, l, r, lv + 1)
 
 
 def plan_updates(rec_in, max_batches: int = 1 << 16):
@@ -421,10 +537,13 @@ def apply_log(pool, page_crcs, src, d_log, n_updates: int, max_len: int, page_by
     need = int(lib().cc_apply_log_work_bytes(n_updates, max_len, page_bytes))
     if need == 0:
         raise CurveCrcError(_lib.CC_EINVAL, "unsupported log geometry")
-    key = pool.device
+    # scratch per (device, stream): calls on different streams may run at the
+    # same time (the apply-thread model) and must not share keys / heads
+    key = _stream_key(pool.device, stream)
     work = _log_work.get(key)
     if work is None or work.numel() < need:
-        work = torch.empty(need, dtype=torch.uint8, device=pool.device)
+        with _on_stream(stream):
+            work = torch.empty(need, dtype=torch.uint8, device=pool.device)
         _log_work[key] = work
     with torch.cuda.device(pool.device):
         fn = "cc_apply_log_delta_dev" if delta else "cc_apply_log_dev"
@@ -453,7 +572,8 @@ def apply_updates(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int 
     if (lens == 0).any() or (dst_off + lens > _nbytes(pool)).any() or (src_off + lens > _nbytes(src)).any():
         raise CurveCrcError(_lib.CC_EINVAL, "update out of range or empty")
     rec = log_records(dst_off, src_off, lens)
-    d_log = torch.from_numpy(rec.view(np.uint8)).to(pool.device)
+    with _on_stream(stream):
+        d_log = torch.from_numpy(rec.view(np.uint8)).to(pool.device)
     n = apply_log(pool, page_crcs, src, d_log, rec.size, int(lens.max()), page_bytes, stream, delta)
     if stream is not None:
         d_log.record_stream(stream)
@@ -507,15 +627,17 @@ def verify_read_records(pool, page_crcs, d_reads, n_reads: int, bad, total, page
     """cc_verify_reads_dev on a batch already resident on the device: `d_reads`
     = int64 device tensor of n_reads (offset, length) pairs; mismatches are
     ADDED to `bad` (int32 [n_reads], -1 marks a read past the pool) and
-    `total` (int64 [1]).  Work buffer cached per device.  No host sync."""
+    `total` (int64 [1]).  Work buffer cached per (device, stream).  No host sync."""
     torch = _torch()
     need = int(lib().cc_verify_reads_work_bytes(n_reads))
     if need == 0:
         raise CurveCrcError(_lib.CC_EINVAL, "unsupported read batch")
-    work = _reads_work.get(pool.device)
+    key = _stream_key(pool.device, stream)
+    work = _reads_work.get(key)
     if work is None or work.numel() < need:
-        work = torch.empty(need, dtype=torch.uint8, device=pool.device)
-        _reads_work[pool.device] = work
+        with _on_stream(stream):
+            work = torch.empty(need, dtype=torch.uint8, device=pool.device)
+        _reads_work[key] = work
     with torch.cuda.device(pool.device):
         check(lib().cc_verify_reads_dev(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, _dev_ptr(d_reads, "reads"),
                                         n_reads, _dev_ptr(page_crcs, "page_crcs"), _dev_ptr(bad, "bad"),
@@ -536,13 +658,14 @@ def verify_reads(pool, page_crcs, offsets, lengths, page_bytes: int = PAGE_SIZE,
     if off.size != ln.size:
         raise CurveCrcError(_lib.CC_EINVAL, "offsets/lengths size mismatch")
     n = off.size
-    bad = torch.zeros(max(n, 1), dtype=torch.int32, device=pool.device)
-    total = torch.zeros(1, dtype=torch.int64, device=pool.device)
-    if n == 0:
-        return bad[:0], total
-    rng = torch.from_numpy(np.stack([off, ln], axis=1).reshape(-1).view(np.int64)).to(pool.device)
-    need = int(lib().cc_verify_reads_work_bytes(n))
-    work = torch.empty(need, dtype=torch.uint8, device=pool.device)
+    with _on_stream(stream):
+        bad = torch.zeros(max(n, 1), dtype=torch.int32, device=pool.device)
+        total = torch.zeros(1, dtype=torch.int64, device=pool.device)
+        if n == 0:
+            return bad[:0], total
+        rng = torch.from_numpy(np.stack([off, ln], axis=1).reshape(-1).view(np.int64)).to(pool.device)
+        need = int(lib().cc_verify_reads_work_bytes(n))
+        work = torch.empty(need, dtype=torch.uint8, device=pool.device)
     with torch.cuda.device(pool.device):
         check(lib().cc_verify_reads_dev(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, _dev_ptr(rng, "reads"), n,
                                         _dev_ptr(page_crcs, "page_crcs"), _dev_ptr(bad, "bad"),

@@ -126,12 +126,40 @@ uint32_t crc32c_zeros(uint64_t nbytes) {
     return ~cc::shift_bytes(0xFFFFFFFFu, nbytes);
 }
 
+uint32_t crc32c_extend_iov(uint32_t crc, const struct iovec* iov, size_t n) {
+    // one raw register carried across the fragments: the same value as
+    // extending fragment by fragment, without the per-fragment ~ in and out
+    uint32_t reg = ~crc;
+    for (size_t i = 0; i < n; i++)
+        if (iov[i].iov_len) reg = raw_update(reg, static_cast<const unsigned char*>(iov[i].iov_base), iov[i].iov_len);
+    return ~reg;
+}
+
 uint32_t cc_fold_host(const uint32_t* page_crcs, uint64_t n, uint64_t page_bytes) {
     if (n == 0) return 0;
     const uint32_t m = cc::xpow(page_bytes << 3);
     uint32_t acc = page_crcs[0];
     for (uint64_t i = 1; i < n; i++) acc = cc::mulmod(m, acc) ^ page_crcs[i];
     return acc;
+}
+
+int cc_slice_fold(const uint32_t* page_crcs, uint64_t n_pages, uint32_t pages_per_slice, uint32_t page_bytes,
+                  uint32_t* out) {
+    if (n_pages == 0) return CC_OK;
+    if (!page_crcs || !out || pages_per_slice == 0 || page_bytes == 0 || n_pages % pages_per_slice) return CC_EINVAL;
+    // Horner with the constant x^(8*page_bytes) through 4 byte tables: 4 lookups per page
+    const uint32_t m = cc::xpow((uint64_t)page_bytes << 3);
+    uint32_t t[4][256];
+    for (int k = 0; k < 4; k++)
+        for (uint32_t v = 0; v < 256; v++) t[k][v] = cc::mulmod(m, v << (8 * k));
+    for (uint64_t s = 0; s < n_pages / pages_per_slice; s++) {
+        const uint32_t* p = page_crcs + s * pages_per_slice;
+        uint32_t acc = p[0];
+        for (uint32_t i = 1; i < pages_per_slice; i++)
+            acc = (t[0][acc & 0xFF] ^ t[1][(acc >> 8) & 0xFF] ^ t[2][(acc >> 16) & 0xFF] ^ t[3][acc >> 24]) ^ p[i];
+        out[s] = acc;
+    }
+    return CC_OK;
 }
 
 }  // extern "C"
@@ -167,11 +195,17 @@ extern "C" int cc_plan_updates(const cc_update* in, uint64_t n, cc_update* out, 
         key.swap(ktmp);
         idx.swap(tmp);
     }
-    // sweep: clusters of transitively overlapping writes (running max of ends)
+    // sweep: clusters of transitively overlapping writes (running max of ends);
+    // inside a cluster, levels in WRITE order through a max segment tree over
+    // the cluster's distinct endpoints: level(j) = max over the elementary
+    // segments j covers of (1 + level of an earlier write covering them), then
+    // j raises its segments to level(j) + 1 -- O(k log k) per cluster of k
     std::vector<uint32_t> level(n, 0);
     uint32_t maxlv = 0;
     uint64_t i = 0;
     std::vector<uint32_t> mem;
+    std::vector<uint64_t> xs;
+    std::vector<uint32_t> mx, tag;
     while (i < n) {
         uint64_t j = i + 1;
         uint64_t run_end = in[idx[i]].dst + in[idx[i]].len;
@@ -179,18 +213,47 @@ extern "C" int cc_plan_updates(const cc_update* in, uint64_t n, cc_update* out, 
             run_end = std::max(run_end, in[idx[j]].dst + in[idx[j]].len);
             j++;
         }
-        if (j - i > 1) {  // overlapping cluster: levels in WRITE order
+        if (j - i > 1) {  // overlapping cluster
             mem.assign(idx.begin() + i, idx.begin() + j);
-            std::sort(mem.begin(), mem.end());
-            for (size_t x = 0; x < mem.size(); x++) {
-                const cc_update& b = in[mem[x]];
-                uint32_t lv = 0;
-                for (size_t y = 0; y < x; y++) {
-                    const cc_update& a = in[mem[y]];
-                    if (a.dst < b.dst + b.len && b.dst < a.dst + a.len) lv = std::max(lv, level[mem[y]] + 1);
+            std::sort(mem.begin(), mem.end());  // write order
+            xs.clear();
+            for (uint32_t m : mem) {
+                xs.push_back(in[m].dst);
+                xs.push_back(in[m].dst + in[m].len);
+            }
+            std::sort(xs.begin(), xs.end());
+            xs.erase(std::unique(xs.begin(), xs.end()), xs.end());
+            const size_t segs = xs.size() - 1;  // elementary segments [xs[k], xs[k+1])
+            size_t size = 1;
+            while (size < segs) size <<= 1;
+            mx.assign(2 * size, 0);
+            tag.assign(2 * size, 0);
+            // mx[v] = max over v's range (tags included); tag[v] = value applied to all of v
+            auto update = [&](auto&& self, size_t v, size_t vl, size_t vr, size_t l, size_t r, uint32_t val) -> void {
+                if (r <= vl || vr <= l) return;
+                if (l <= vl && vr <= r) {
+                    mx[v] = std::max(mx[v], val);
+                    tag[v] = std::max(tag[v], val);
+                    return;
                 }
-                level[mem[x]] = lv;
+                const size_t mid = (vl + vr) / 2;
+                self(self, 2 * v, vl, mid, l, r, val);
+                self(self, 2 * v + 1, mid, vr, l, r, val);
+                mx[v] = std::max(mx[v], std::max(mx[2 * v], mx[2 * v + 1]));
+            };
+            auto query = [&](auto&& self, size_t v, size_t vl, size_t vr, size_t l, size_t r) -> uint32_t {
+                if (r <= vl || vr <= l) return 0;
+                if (l <= vl && vr <= r) return mx[v];
+                const size_t mid = (vl + vr) / 2;
+                return std::max(tag[v], std::max(self(self, 2 * v, vl, mid, l, r), self(self, 2 * v + 1, mid, vr, l, r)));
+            };
+            for (uint32_t m : mem) {
+                const size_t l = std::lower_bound(xs.begin(), xs.end(), in[m].dst) - xs.begin();
+                const size_t r = std::lower_bound(xs.begin(), xs.end(), in[m].dst + in[m].len) - xs.begin();
+                const uint32_t lv = query(query, 1, 0, size, l, r);  // stored values are level + 1
+                level[m] = lv;
                 maxlv = std::max(maxlv, lv);
+                update(update, 1, 0, size, l, r, lv + 1);
             }
         }
         i = j;

@@ -2,9 +2,12 @@
 // (LDS image, CU count, pinned staging), argument checking, error mapping.
 //
 // Threading: the reference calls its CRC primitive from raft apply threads and
-// brpc bthread workers.  Device contexts are created once under a
-// mutex; *_dev calls are lock-free after that (they only enqueue).  The
-// blocking *_host call serialises on a per-device submission lock.
+// brpc bthread workers.  A device context is created once under a
+// mutex and then reached through a lock-free shared_ptr load, so *_dev calls
+// take no lock (they only enqueue).  Every call holds its own reference to the
+// context: cc_engine_fini unpublishes the contexts and the last call still
+// using one frees it.  The blocking *_host calls serialise on a per-device
+// submission lock.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -17,6 +20,7 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
@@ -73,21 +77,44 @@ struct Staging {
     hipStream_t stream[2] = {nullptr, nullptr};
     hipEvent_t done[2] = {nullptr, nullptr};
     SlotSignal sig[2];
+    // per-call device inputs of the streamed digest (after bytes, multipliers,
+    // copyset index per chunk, digest accumulator): grown on demand
+    void* aux = nullptr;
+    size_t aux_bytes = 0;
+    hipEvent_t aux_ready = nullptr;
 };
 
+// Product tables of the fused epilogue, one per (page_bytes, q): a small
+// lock-free cache (lookups from concurrent *_dev calls take no lock; the rare
+// insert takes the context's table mutex).
+constexpr int kEpiSlots = 16;
+
 struct DevCtx {
+    int device = -1;
     bool ready = false;
     int cus = 256;
     void* image = nullptr;
     std::mutex submit;  // serialises *_host calls on this device
     Staging st;
-    std::unordered_map<uint64_t, void*> epi_tables;  // epilogue product tables per (page_bytes, q)
-    std::unordered_map<void*, uint32_t> work_gen;    // partial-write generation per work buffer
-    std::unordered_map<void*, uint64_t> work_pages;
+    std::mutex tab_mu;  // epilogue-table inserts
+    std::atomic<uint64_t> epi_key[kEpiSlots];  // key + 1 (0 = empty); published after epi_ptr
+    std::atomic<void*> epi_ptr[kEpiSlots];
+    std::mutex work_mu;  // partial-write generation tags (cc_apply_updates_dev)
+    std::unordered_map<void*, std::pair<uint32_t, uint64_t>> work_gen;  // work buffer -> (gen, n_pages)
+    DevCtx() {
+        for (int i = 0; i < kEpiSlots; i++) {
+            epi_key[i].store(0);
+            epi_ptr[i].store(nullptr);
+        }
+    }
+    ~DevCtx();
 };
 
-std::mutex g_mu;
-std::vector<DevCtx*> g_ctx;
+using CtxRef = std::shared_ptr<DevCtx>;
+
+constexpr int kMaxDevices = 64;
+std::mutex g_mu;                 // context creation / teardown only
+CtxRef g_ctx[kMaxDevices];       // read with std::atomic_load (lock-free fast path)
 cc_opts g_opts = {4096u, 4u << 20, 256ull << 20};
 
 int map_err(hipError_t e) {
@@ -99,38 +126,84 @@ int map_err(hipError_t e) {
     return CC_EHIP;
 }
 
+void staging_free(Staging& st) {
+    for (int i = 0; i < 2; i++) {
+        if (st.stream[i]) hipStreamSynchronize(st.stream[i]);
+        if (st.host[i]) hipHostFree(st.host[i]);
+        if (st.dev[i]) hipFree(st.dev[i]);
+        if (st.dcrc[i]) hipFree(st.dcrc[i]);
+        if (st.hcrc[i]) hipHostFree(st.hcrc[i]);
+        if (st.stream[i]) hipStreamDestroy(st.stream[i]);
+        if (st.done[i]) hipEventDestroy(st.done[i]);
+        st.host[i] = st.dev[i] = nullptr;
+        st.dcrc[i] = st.hcrc[i] = nullptr;
+        st.stream[i] = nullptr;
+        st.done[i] = nullptr;
+        st.sig[i].fired = true;
+    }
+    if (st.aux) hipFree(st.aux);
+    if (st.aux_ready) hipEventDestroy(st.aux_ready);
+    st.aux = nullptr;
+    st.aux_ready = nullptr;
+    st.aux_bytes = 0;
+    st.ready = false;
+    st.bytes = 0;
+}
+
+// Runs when the last reference drops (cc_engine_fini, or the last call still
+// holding the context after it): nothing can be enqueued on it any more, so
+// finish whatever was enqueued and free on the context's own device.
+DevCtx::~DevCtx() {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (device >= 0 && hipSetDevice(device) == hipSuccess) {
+        (void)hipDeviceSynchronize();  // kernels enqueued by *_dev calls may still read the image / tables
+        staging_free(st);
+        if (image) hipFree(image);
+        for (int i = 0; i < kEpiSlots; i++)
+            if (void* p = epi_ptr[i].load()) hipFree(p);
+    }
+    if (cur >= 0) (void)hipSetDevice(cur);
+}
+
 // Context of the calling thread's current device, created on first use.
-int get_ctx(DevCtx** out) {
+int get_ctx(CtxRef* out) {
     int dev = -1, n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CC_ENODEV;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return CC_ENODEV;
-    std::lock_guard<std::mutex> lk(g_mu);
-    if ((int)g_ctx.size() < n) g_ctx.resize(n, nullptr);
-    if (!g_ctx[dev]) g_ctx[dev] = new DevCtx();
-    DevCtx* c = g_ctx[dev];
-    if (!c->ready) {
-        hipDeviceProp_t prop;
-        hipError_t e = hipGetDeviceProperties(&prop, dev);
-        if (e != hipSuccess) return map_err(e);
-        c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-        std::vector<uint32_t> img(kLdsBytes / 4);
-        build_lds_image(img.data());
-        e = hipMalloc(&c->image, kLdsBytes);
-        if (e != hipSuccess) return map_err(e);
-        e = hipMemcpy(c->image, img.data(), kLdsBytes, hipMemcpyHostToDevice);
-        if (e != hipSuccess) return map_err(e);
-        e = upload_x2k(x2k().t);
-        if (e != hipSuccess) return map_err(e);
-        static uint32_t xinv[kXinvEntries];
-        uint32_t r = xinv_bytes(0);
-        for (uint32_t t = 0; t < kXinvEntries; t++, r = div_x8(r)) xinv[t] = r;  // x^(-8t)
-        e = upload_xinv(xinv);
-        if (e != hipSuccess) return map_err(e);
-        c->ready = true;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return CC_ENODEV;
+    CtxRef c = std::atomic_load(&g_ctx[dev]);
+    if (c) {
+        *out = std::move(c);
+        return CC_OK;
     }
-    *out = c;
+    std::lock_guard<std::mutex> lk(g_mu);
+    c = std::atomic_load(&g_ctx[dev]);
+    if (c) {
+        *out = std::move(c);
+        return CC_OK;
+    }
+    c = std::make_shared<DevCtx>();
+    c->device = dev;
+    hipDeviceProp_t prop;
+    hipError_t e = hipGetDeviceProperties(&prop, dev);
+    if (e != hipSuccess) return map_err(e);
+    c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    std::vector<uint32_t> img(kLdsBytes / 4);
+    build_lds_image(img.data());
+    if ((e = hipMalloc(&c->image, kLdsBytes)) != hipSuccess) return map_err(e);
+    if ((e = hipMemcpy(c->image, img.data(), kLdsBytes, hipMemcpyHostToDevice)) != hipSuccess) return map_err(e);
+    if ((e = upload_x2k(x2k().t)) != hipSuccess) return map_err(e);
+    static uint32_t xinv[kXinvEntries];
+    uint32_t r = xinv_bytes(0);
+    for (uint32_t t = 0; t < kXinvEntries; t++, r = div_x8(r)) xinv[t] = r;  // x^(-8t)
+    if ((e = upload_xinv(xinv)) != hipSuccess) return map_err(e);
+    c->ready = true;
+    std::atomic_store(&g_ctx[dev], c);
+    *out = std::move(c);
     return CC_OK;
 }
+
+inline uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 
 inline bool page_size_ok(uint32_t page_bytes) {
     return page_bytes >= 256 && page_bytes <= (1u << 20) && page_bytes % 256 == 0;
@@ -172,6 +245,8 @@ int staging_init(DevCtx* c) {
         if ((e = hipStreamCreateWithFlags(&st.stream[i], hipStreamNonBlocking)) != hipSuccess) return map_err(e);
         if ((e = hipEventCreateWithFlags(&st.done[i], hipEventDisableTiming)) != hipSuccess) return map_err(e);
     }
+    hipError_t e = hipEventCreateWithFlags(&st.aux_ready, hipEventDisableTiming);
+    if (e != hipSuccess) return map_err(e);
     st.ready = true;
     return CC_OK;
 }
@@ -226,24 +301,41 @@ bool is_pinned(const void* p) {
     return attr.type == hipMemoryTypeHost;
 }
 
-void staging_free(Staging& st) {
-    for (int i = 0; i < 2; i++) {
-        if (st.stream[i]) hipStreamSynchronize(st.stream[i]);
-        if (st.host[i]) hipHostFree(st.host[i]);
-        if (st.dev[i]) hipFree(st.dev[i]);
-        if (st.dcrc[i]) hipFree(st.dcrc[i]);
-        if (st.hcrc[i]) hipHostFree(st.hcrc[i]);
-        if (st.stream[i]) hipStreamDestroy(st.stream[i]);
-        if (st.done[i]) hipEventDestroy(st.done[i]);
-        st.host[i] = st.dev[i] = nullptr;
-        st.dcrc[i] = st.hcrc[i] = nullptr;
-        st.stream[i] = nullptr;
-        st.done[i] = nullptr;
-        st.sig[i].fired = true;
+// The two staging slots' in-flight batches of one blocking call.  Every exit
+// goes through drain() or fail(): a call never returns while a batch it
+// enqueued may still read or write the shared pinned staging (the next call,
+// possibly from another thread, reuses the same slots).
+struct SlotRing {
+    Staging& st;
+    uint64_t first[2] = {0, 0};
+    uint64_t n[2] = {0, 0};
+    explicit SlotRing(Staging& s) : st(s) {}
+    // wait for slot s's batch; `take` copies its results out
+    template <class F>
+    int drain(int s, F&& take) {
+        if (!n[s]) return CC_OK;
+        const hipError_t e = park_slot(st, s);
+        const uint64_t f = first[s], k = n[s];
+        n[s] = 0;
+        if (e != hipSuccess) return fail(map_err(e));
+        take(f, k);
+        return CC_OK;
     }
-    st.ready = false;
-    st.bytes = 0;
-}
+    // error exit: park whatever is still in flight (its status no longer
+    // matters) and hand back rc
+    int fail(int rc) {
+        for (int s = 0; s < 2; s++)
+            if (n[s]) {
+                (void)park_slot(st, s);
+                n[s] = 0;
+            }
+        // a slot armed by arm_slot may have failed before its host function was
+        // enqueued: make sure the streams are idle either way
+        for (int s = 0; s < 2; s++)
+            if (st.stream[s]) (void)hipStreamSynchronize(st.stream[s]);
+        return rc;
+    }
+};
 
 }  // namespace
 }  // namespace cc
@@ -252,7 +344,7 @@ using namespace cc;
 
 extern "C" {
 
-const char* cc_version(void) { return "libcurvecrc 0.1 (gfx950)"; }
+const char* cc_version(void) { return "libcurvecrc 0.2 (gfx950)"; }
 
 const char* cc_strerror(int code) {
     switch (code) {
@@ -263,6 +355,8 @@ const char* cc_strerror(int code) {
         case CC_EHIP: return "HIP runtime error";
         case CC_ECORRUPT: return "checksum mismatch";
         case CC_ECOMM: return "RCCL communication error";
+        case CC_EIO: return "I/O error";
+        case CC_ESTALE: return "per-page CRC table is stale";
         default: return "unknown error";
     }
 }
@@ -276,7 +370,7 @@ int cc_lds_image(void* out, size_t bytes) {
 int cc_hbm_read_probe_dev(const void* d_buf, uint64_t bytes, uint32_t* d_sink, void* stream) {
     if (!d_buf || !d_sink || bytes % 4096 || ((uintptr_t)d_buf & 15u)) return CC_EINVAL;
     if (bytes == 0) return CC_OK;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     return map_err(launch_read_probe(d_buf, bytes, d_sink, 2 * c->cus, static_cast<hipStream_t>(stream)));
@@ -298,27 +392,22 @@ int cc_engine_init(const cc_opts* opts) {
             if (opts->staging_bytes) g_opts.staging_bytes = opts->staging_bytes;
         }
     }
-    DevCtx* c = nullptr;
+    CtxRef c;
     return get_ctx(&c);
 }
 
 int cc_engine_fini(void) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    int cur = -1;
-    (void)hipGetDevice(&cur);
-    for (size_t d = 0; d < g_ctx.size(); d++) {
-        DevCtx* c = g_ctx[d];
-        if (!c) continue;
-        if (hipSetDevice((int)d) == hipSuccess) {
-            staging_free(c->st);
-            if (c->image) hipFree(c->image);
-            for (auto& kv : c->epi_tables)
-                if (kv.second) hipFree(kv.second);
+    // unpublish every context; each is freed here, or by the last call still
+    // holding it (that call's kernels are synchronised before the free)
+    std::vector<CtxRef> old;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (int d = 0; d < kMaxDevices; d++) {
+            CtxRef c = std::atomic_exchange(&g_ctx[d], CtxRef());
+            if (c) old.push_back(std::move(c));
         }
-        delete c;
-        g_ctx[d] = nullptr;
     }
-    if (cur >= 0) (void)hipSetDevice(cur);
+    old.clear();
     return CC_OK;
 }
 
@@ -326,7 +415,7 @@ int cc_page_crc_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes, 
     if (!page_size_ok(page_bytes)) return CC_EINVAL;
     if (n_pages == 0) return CC_OK;
     if (!d_pages || !d_out || ((uintptr_t)d_pages & 3u)) return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     PageLaunch a = {};
@@ -336,7 +425,7 @@ int cc_page_crc_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes, 
     a.image = c->image;
     a.kconst = kconst_for(page_bytes);
     a.out = d_out;
-    geometry_for(c, n_pages, &a);
+    geometry_for(c.get(), n_pages, &a);
     return map_err(launch_page_crc(a, static_cast<hipStream_t>(stream)));
 }
 
@@ -347,7 +436,7 @@ int cc_page_verify_list_dev(const void* d_pages, uint64_t n_pages, uint32_t page
     if (n_pages == 0) return CC_OK;
     if (!d_pages || !d_expected || !d_bad_count || !d_first_bad || ((uintptr_t)d_pages & 3u)) return CC_EINVAL;
     if (max_bad_pages && !d_bad_pages) return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     PageLaunch a = {};
@@ -361,7 +450,7 @@ int cc_page_verify_list_dev(const void* d_pages, uint64_t n_pages, uint32_t page
     a.sink.first_bad = reinterpret_cast<unsigned long long*>(d_first_bad);
     a.sink.list = max_bad_pages ? reinterpret_cast<unsigned long long*>(d_bad_pages) : nullptr;
     a.sink.max_list = max_bad_pages;
-    geometry_for(c, n_pages, &a);
+    geometry_for(c.get(), n_pages, &a);
     return map_err(launch_page_verify(a, static_cast<hipStream_t>(stream)));
 }
 
@@ -375,7 +464,7 @@ int cc_fold_dev(const uint32_t* d_crcs, uint64_t n_groups, uint32_t per_group, u
                 uint32_t* d_out, void* stream) {
     if (n_groups == 0) return CC_OK;
     if (!d_crcs || !d_out || per_group == 0 || unit_bytes == 0) return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     FoldLaunch a = {};
@@ -392,7 +481,7 @@ int cc_fold_dev(const uint32_t* d_crcs, uint64_t n_groups, uint32_t per_group, u
 int cc_shift_dev(const uint32_t* d_crcs, const uint64_t* d_shift_bytes, uint64_t n, uint32_t* d_out, void* stream) {
     if (n == 0) return CC_OK;
     if (!d_crcs || !d_shift_bytes || !d_out) return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     return map_err(launch_shift(d_crcs, d_shift_bytes, n, d_out, static_cast<hipStream_t>(stream)));
@@ -401,18 +490,121 @@ int cc_shift_dev(const uint32_t* d_crcs, const uint64_t* d_shift_bytes, uint64_t
 int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, uint32_t* d_out, void* stream) {
     if (n == 0) return CC_OK;
     if (!d_buf || !d_ranges || !d_out) return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
 #ifndef CC_RANGE_GRID_MULT
 #define CC_RANGE_GRID_MULT 1  // workgroups per CU launched for a range batch (> 1: hardware re-balances waves)
 #endif
-    const uint64_t need = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    // one descriptor per wave: enough workgroups of range_waves() waves to give
+    // every range its wave, capped at CC_RANGE_GRID_MULT workgroups per CU
+    const uint64_t wpb = (uint64_t)range_waves();
+    const uint64_t need = (n + wpb - 1) / wpb;
     const uint64_t cap = (uint64_t)c->cus * CC_RANGE_GRID_MULT;
     const int blocks = (int)(need < cap ? need : cap);
     return map_err(launch_range_crc(static_cast<const unsigned char*>(d_buf),
                                     reinterpret_cast<const RangeDesc*>(d_ranges), n, c->image, d_out, blocks,
                                     static_cast<hipStream_t>(stream)));
+}
+
+int cc_crc_bufs_host(const void* const* h_bufs, const uint64_t* h_lens, uint64_t n, uint32_t* h_out) {
+    if (n == 0) return CC_OK;
+    if (!h_bufs || !h_lens || !h_out) return CC_EINVAL;
+    for (uint64_t i = 0; i < n; i++)
+        if (h_lens[i] && !h_bufs[i]) return CC_EINVAL;
+    CtxRef c;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->submit);
+    if ((rc = staging_init(c.get()))) return rc;
+    Staging& st = c->st;
+    SlotRing ring(st);
+    // batches of whole buffers packed back to back (4-byte aligned) into a
+    // staging slot; a buffer larger than a slot is hashed in slot-sized pieces
+    // combined on the host.  Records go in the result region's tail.
+    const uint64_t slot = st.bytes;
+    // result region per slot (st.bytes / 64 bytes): k CRCs, then the k range
+    // records at the next 256-byte boundary
+    const uint64_t max_recs = (st.bytes / 64 - 256) / (sizeof(RangeDesc) + 4);
+    uint64_t i = 0, off_in_i = 0;
+    int s = 0;
+    struct Item {
+        uint64_t buf;  // index of the buffer
+        uint64_t off;  // byte offset inside the buffer
+        uint64_t len;
+    };
+    std::vector<Item> items[2];
+    std::vector<uint32_t> acc(n, 0);       // running CRC of each buffer (pieces in order)
+    std::vector<uint8_t> started(n, 0);
+    auto take = [&](int sl) {
+        return [&, sl](uint64_t, uint64_t k) {
+            const uint32_t* r = st.hcrc[sl];
+            for (uint64_t j = 0; j < k; j++) {
+                const Item& it = items[sl][j];
+                acc[it.buf] = started[it.buf] ? crc32c_combine(acc[it.buf], r[j], it.len) : r[j];
+                started[it.buf] = 1;
+            }
+        };
+    };
+    while (i < n) {
+        if ((rc = ring.drain(s, take(s)))) return rc;
+        items[s].clear();
+        unsigned char* hs = static_cast<unsigned char*>(st.host[s]);
+        uint64_t used = 0;
+        while (i < n && items[s].size() < max_recs) {
+            const uint64_t rem = h_lens[i] - off_in_i;
+            const uint64_t room = slot - used;
+            if (rem == 0) {  // empty buffer: CRC 0, no bytes
+                if (!started[i]) acc[i] = 0;
+                started[i] = 1;
+                i++;
+                off_in_i = 0;
+                continue;
+            }
+            if (room < 256) break;
+            const uint64_t take_n = rem < room ? rem : (room & ~255ull);
+            memcpy(hs + used, static_cast<const unsigned char*>(h_bufs[i]) + off_in_i, take_n);
+            items[s].push_back(Item{i, off_in_i, take_n});
+            used = (used + take_n + 255) & ~255ull;
+            off_in_i += take_n;
+            if (off_in_i == h_lens[i]) {
+                i++;
+                off_in_i = 0;
+            }
+        }
+        const uint64_t k = items[s].size();
+        if (k == 0) continue;
+        hipStream_t strm = st.stream[s];
+        const uint64_t rec_off = align256(k * 4);
+        RangeDesc* recs = reinterpret_cast<RangeDesc*>(reinterpret_cast<unsigned char*>(st.hcrc[s]) + rec_off);
+        RangeDesc* drecs = reinterpret_cast<RangeDesc*>(reinterpret_cast<unsigned char*>(st.dcrc[s]) + rec_off);
+        uint64_t o = 0;
+        for (uint64_t j = 0; j < k; j++) {
+            recs[j] = RangeDesc{o, items[s][j].len};
+            o = (o + items[s][j].len + 255) & ~255ull;
+        }
+        hipError_t e;
+        if ((e = hipMemcpyAsync(st.dev[s], hs, used, hipMemcpyHostToDevice, strm)) != hipSuccess)
+            return ring.fail(map_err(e));
+        if ((e = hipMemcpyAsync(drecs, recs, k * sizeof(RangeDesc), hipMemcpyHostToDevice, strm)) != hipSuccess)
+            return ring.fail(map_err(e));
+        const uint64_t wpb = (uint64_t)range_waves();
+        const uint64_t need = (k + wpb - 1) / wpb;
+        const int blocks = (int)(need < (uint64_t)c->cus ? need : (uint64_t)c->cus);
+        if ((e = launch_range_crc(static_cast<const unsigned char*>(st.dev[s]), drecs, k, c->image, st.dcrc[s],
+                                  blocks, strm)) != hipSuccess)
+            return ring.fail(map_err(e));
+        if ((e = hipMemcpyAsync(st.hcrc[s], st.dcrc[s], k * 4, hipMemcpyDeviceToHost, strm)) != hipSuccess)
+            return ring.fail(map_err(e));
+        if ((e = arm_slot(st, s, strm)) != hipSuccess) return ring.fail(map_err(e));
+        ring.first[s] = 0;
+        ring.n[s] = k;
+        s ^= 1;
+    }
+    if ((rc = ring.drain(s, take(s)))) return rc;
+    if ((rc = ring.drain(s ^ 1, take(s ^ 1)))) return rc;
+    for (uint64_t j = 0; j < n; j++) h_out[j] = acc[j];
+    return CC_OK;
 }
 
 namespace cc {
@@ -431,29 +623,40 @@ bool epilogue_geometry(DevCtx* c, uint32_t pages_per_chunk, uint32_t page_bytes,
     a->q = q;
     a->slice_shift = j;
     // product tables of the 10 geometry constants, built on the host once per
-    // (page_bytes, q) and kept on the device
-    const uint64_t key = ((uint64_t)page_bytes << 32) | q;
-    std::lock_guard<std::mutex> lk(g_mu);
-    void*& dev = c->epi_tables[key];
-    if (!dev) {
-        uint32_t m[10];
-        m[0] = xpow((uint64_t)page_bytes << 3);
-        for (int k = 0; k < 8; k++) m[1 + k] = xpow(((uint64_t)page_bytes * q << k) << 3);
-        m[9] = xpow((uint64_t)pages_per_chunk * page_bytes << 3);
-        std::vector<uint32_t> h(10 * 1024);
-        for (int t = 0; t < 10; t++)
-            for (uint32_t k = 0; k < 4; k++)
-                for (uint32_t b = 0; b < 256; b++) h[t * 1024 + k * 256 + b] = mulmod(m[t], b << (8 * k));
-        if (hipMalloc(&dev, h.size() * 4) != hipSuccess) {
-            dev = nullptr;
-            return false;
+    // (page_bytes, q) and kept on the device; looked up without a lock
+    const uint64_t key = (((uint64_t)page_bytes << 32) | q) + 1;
+    for (int i = 0; i < kEpiSlots; i++)
+        if (c->epi_key[i].load(std::memory_order_acquire) == key) {
+            a->mtab = static_cast<const uint32_t*>(c->epi_ptr[i].load(std::memory_order_relaxed));
+            return true;
         }
-        if (hipMemcpy(dev, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
-            hipFree(dev);  // never leave a half-initialised table in the cache
-            dev = nullptr;
-            return false;
+    std::lock_guard<std::mutex> lk(c->tab_mu);
+    int free_slot = -1;
+    for (int i = 0; i < kEpiSlots; i++) {
+        const uint64_t k = c->epi_key[i].load(std::memory_order_acquire);
+        if (k == key) {
+            a->mtab = static_cast<const uint32_t*>(c->epi_ptr[i].load(std::memory_order_relaxed));
+            return true;
         }
+        if (k == 0 && free_slot < 0) free_slot = i;
     }
+    if (free_slot < 0) return false;  // more geometries than slots: refuse rather than evict a table in use
+    uint32_t m[10];
+    m[0] = xpow((uint64_t)page_bytes << 3);
+    for (int k = 0; k < 8; k++) m[1 + k] = xpow(((uint64_t)page_bytes * q << k) << 3);
+    m[9] = xpow((uint64_t)pages_per_chunk * page_bytes << 3);
+    std::vector<uint32_t> h(10 * 1024);
+    for (int t = 0; t < 10; t++)
+        for (uint32_t k = 0; k < 4; k++)
+            for (uint32_t b = 0; b < 256; b++) h[t * 1024 + k * 256 + b] = mulmod(m[t], b << (8 * k));
+    void* dev = nullptr;
+    if (hipMalloc(&dev, h.size() * 4) != hipSuccess) return false;
+    if (hipMemcpy(dev, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        hipFree(dev);  // never publish a half-initialised table
+        return false;
+    }
+    c->epi_ptr[free_slot].store(dev, std::memory_order_relaxed);
+    c->epi_key[free_slot].store(key, std::memory_order_release);
     a->mtab = static_cast<const uint32_t*>(dev);
     return true;
 }
@@ -463,7 +666,7 @@ bool epilogue_geometry(DevCtx* c, uint32_t pages_per_chunk, uint32_t page_bytes,
 int cc_xpow8_dev(const uint64_t* d_nbytes, uint64_t n, uint32_t* d_out, void* stream) {
     if (n == 0) return CC_OK;
     if (!d_nbytes || !d_out) return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     return map_err(launch_xpow8(d_nbytes, n, d_out, static_cast<hipStream_t>(stream)));
@@ -477,11 +680,11 @@ int cc_scan_epilogue_dev(const uint32_t* d_page_crcs, const uint32_t* d_meta_crc
     if (!d_page_crcs || !d_meta_crcs || !d_slice_crcs || page_bytes == 0) return CC_EINVAL;
     const bool dig = d_after_mult || d_group || d_digest;
     if (dig && !(d_after_mult && d_group && d_digest)) return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     EpilogueLaunch a = {};
-    if (!epilogue_geometry(c, pages_per_chunk, page_bytes, pages_per_slice, &a)) return CC_EINVAL;
+    if (!epilogue_geometry(c.get(), pages_per_chunk, page_bytes, pages_per_slice, &a)) return CC_EINVAL;
     a.page_crcs = d_page_crcs;
     a.meta_crcs = d_meta_crcs;
     a.n_chunks = n_chunks;
@@ -497,7 +700,7 @@ int cc_combine_dev(const uint32_t* d_a, const uint32_t* d_b, uint64_t len_b, uin
                    void* stream) {
     if (n == 0) return CC_OK;
     if (!d_a || !d_b || !d_out) return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     return map_err(launch_combine(d_a, d_b, xpow(len_b << 3), n, d_out, static_cast<hipStream_t>(stream)));
@@ -507,11 +710,20 @@ int cc_digest_dev(const uint32_t* d_file_crcs, const uint64_t* d_after_bytes, co
                   uint64_t n_files, uint32_t* d_digest, void* stream) {
     if (n_files == 0) return CC_OK;
     if (!d_file_crcs || !d_after_bytes || !d_group || !d_digest) return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     return map_err(launch_digest(d_file_crcs, d_after_bytes, d_group, n_files, d_digest,
                                  static_cast<hipStream_t>(stream)));
+}
+
+int cc_digest_fold_dev(const uint32_t* d_gathered, uint32_t nranks, uint64_t n, uint32_t* d_digest, void* stream) {
+    if (n == 0) return CC_OK;
+    if (!d_gathered || !d_digest || nranks == 0) return CC_EINVAL;
+    CtxRef c;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    return map_err(launch_xor_fold(d_gathered, nranks, n, d_digest, static_cast<hipStream_t>(stream)));
 }
 
 // Host in / host out.  Two-slot pipeline: while slot i's pages are copied in
@@ -522,27 +734,26 @@ int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
     if (!page_size_ok(page_bytes)) return CC_EINVAL;
     if (n_pages == 0) return CC_OK;
     if (!h_pages || !h_out) return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(c->submit);
-    if ((rc = staging_init(c))) return rc;
+    if ((rc = staging_init(c.get()))) return rc;
     Staging& st = c->st;
+    SlotRing ring(st);
     const bool pinned = is_pinned(h_pages);
     const uint64_t per_slot = st.bytes / page_bytes;
     const unsigned char* src = static_cast<const unsigned char*>(h_pages);
+    auto take = [&](int s) {
+        return [&, s](uint64_t f, uint64_t k) { memcpy(h_out + f, st.hcrc[s], k * 4); };
+    };
     uint64_t done = 0;
-    uint64_t pending_first[2] = {0, 0}, pending_n[2] = {0, 0};
     int slot = 0;
     hipError_t e = hipSuccess;
     while (done < n_pages) {
         const uint64_t n = (n_pages - done < per_slot) ? n_pages - done : per_slot;
         // reclaim this slot: wait for its previous batch and copy its CRCs out
-        if (pending_n[slot]) {
-            if ((e = park_slot(st, slot)) != hipSuccess) return map_err(e);
-            memcpy(h_out + pending_first[slot], st.hcrc[slot], pending_n[slot] * 4);
-            pending_n[slot] = 0;
-        }
+        if ((rc = ring.drain(slot, take(slot)))) return rc;
         const void* hsrc = src + done * page_bytes;
         if (!pinned) {
             memcpy(st.host[slot], hsrc, n * page_bytes);
@@ -550,7 +761,7 @@ int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
         }
         if ((e = hipMemcpyAsync(st.dev[slot], hsrc, n * page_bytes, hipMemcpyHostToDevice, st.stream[slot])) !=
             hipSuccess)
-            return map_err(e);
+            return ring.fail(map_err(e));
         PageLaunch a = {};
         a.pages = static_cast<const uint32_t*>(st.dev[slot]);
         a.n_pages = n;
@@ -558,28 +769,19 @@ int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
         a.image = c->image;
         a.kconst = kconst_for(page_bytes);
         a.out = st.dcrc[slot];
-        geometry_for(c, n, &a);
-        if ((e = launch_page_crc(a, st.stream[slot])) != hipSuccess) return map_err(e);
+        geometry_for(c.get(), n, &a);
+        if ((e = launch_page_crc(a, st.stream[slot])) != hipSuccess) return ring.fail(map_err(e));
         if ((e = hipMemcpyAsync(st.hcrc[slot], st.dcrc[slot], n * 4, hipMemcpyDeviceToHost, st.stream[slot])) !=
             hipSuccess)
-            return map_err(e);
-        if ((e = arm_slot(st, slot, st.stream[slot])) != hipSuccess) return map_err(e);
-        pending_first[slot] = done;
-        pending_n[slot] = n;
+            return ring.fail(map_err(e));
+        if ((e = arm_slot(st, slot, st.stream[slot])) != hipSuccess) return ring.fail(map_err(e));
+        ring.first[slot] = done;
+        ring.n[slot] = n;
         done += n;
         slot ^= 1;
     }
-    for (int k = 0; k < 2; k++) {
-        if (!pending_n[slot]) {
-            slot ^= 1;
-            continue;
-        }
-        if ((e = park_slot(st, slot)) != hipSuccess) return map_err(e);
-        memcpy(h_out + pending_first[slot], st.hcrc[slot], pending_n[slot] * 4);
-        pending_n[slot] = 0;
-        slot ^= 1;
-    }
-    return CC_OK;
+    if ((rc = ring.drain(slot, take(slot)))) return rc;
+    return ring.drain(slot ^ 1, take(slot ^ 1));
 }
 
 uint64_t cc_update_work_bytes(uint64_t n_pages, uint64_t n_updates, uint32_t max_len, uint32_t page_bytes) {
@@ -599,23 +801,26 @@ int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes,
     if (pool_bytes % page_bytes || ((uintptr_t)d_pool & 3u) || ((uintptr_t)d_src & 3u)) return CC_EINVAL;
     const uint64_t n_pages = pool_bytes / page_bytes;
     if (work_bytes < cc_update_work_bytes(n_pages, n_updates, max_len, page_bytes)) return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e;
     // generation tags: a work buffer seen for the first time (or after 2^32-1
-    // calls) is zeroed once; afterwards each call just bumps its tag
+    // calls) is zeroed once; afterwards each call just bumps its tag.  The map
+    // is bounded: forgetting a buffer only costs it one more zeroing.
     uint32_t gen;
     {
-        std::lock_guard<std::mutex> lk(g_mu);
-        uint32_t& g = c->work_gen[d_work];
-        if (g == 0 || g == 0xFFFFFFFFu || c->work_pages[d_work] != n_pages) {
+        constexpr size_t kMaxTracked = 64;
+        std::lock_guard<std::mutex> lk(c->work_mu);
+        auto it = c->work_gen.find(d_work);
+        if (it == c->work_gen.end() && c->work_gen.size() >= kMaxTracked) c->work_gen.clear();
+        auto& g = c->work_gen[d_work];
+        if (g.first == 0 || g.first == 0xFFFFFFFFu || g.second != n_pages) {
             if ((e = hipMemsetAsync(d_work, 0, n_pages * 4, s)) != hipSuccess) return map_err(e);
-            g = 0;
-            c->work_pages[d_work] = n_pages;
+            g = {0u, n_pages};
         }
-        gen = ++g;
+        gen = ++g.first;
     }
     UpdateLaunch a = {};
     a.pool = static_cast<unsigned char*>(d_pool);
@@ -654,7 +859,6 @@ inline bool log_page_ok(uint32_t page_bytes) {
     return page_bytes % kWaveBytes == 0 && m >= 1 && m <= 32 && (m & (m - 1)) == 0;
 }
 inline uint32_t log_slots(uint32_t max_len, uint32_t page_bytes) { return (max_len - 1) / page_bytes + 2; }
-inline uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 }  // namespace
 
 uint64_t cc_apply_log_work_bytes(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes) {
@@ -678,7 +882,7 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
     if (n_pages >= kNoPiece) return CC_EINVAL;  // page index must fit a 32-bit key below kNoPiece
     const uint64_t need = cc_apply_log_work_bytes(n_updates, max_len, page_bytes);
     if (need == 0 || work_bytes < need) return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -754,7 +958,7 @@ int cc_verify_reads_dev(const void* d_pool, uint64_t pool_bytes, uint32_t page_b
     if (pool_bytes % page_bytes || ((uintptr_t)d_pool & 3u)) return CC_EINVAL;
     const uint64_t need = cc_verify_reads_work_bytes(n_reads);
     if (need == 0 || work_bytes < need) return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -784,30 +988,47 @@ int cc_verify_reads_dev(const void* d_pool, uint64_t pool_bytes, uint32_t page_b
 
 // Streaming scan.  Each staging slot holds a batch of whole chunks (data and
 // metapages in separate device regions) plus the per-chunk results; a batch is
-// {H2D data+meta, page kernel over data, page kernel over metapages, fold to
-// slices, fold to chunk data CRC, combine to file CRC, D2H results} on the
+// {H2D data+meta, page kernel over data, page kernel over metapages, fused
+// epilogue (slices, file CRCs, digest contributions), D2H results} on the
 // slot's stream, so consecutive batches on the two streams overlap copy and
-// compute.
-int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_bytes, uint32_t meta_bytes,
-                 uint32_t page_bytes, uint32_t slice_bytes, uint32_t* h_meta_crcs, uint32_t* h_slice_crcs,
-                 uint32_t* h_file_crcs) {
-    if (n_chunks == 0) return CC_OK;
+// compute.  Pinned sources are DMA'd directly, chunk by chunk (a mix of pinned
+// and pageable chunks is fine); pageable ones are staged through the slot's
+// pinned buffer first.
+int cc_scan_host_digest(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_bytes, uint32_t meta_bytes,
+                        uint32_t page_bytes, uint32_t slice_bytes, uint32_t* h_meta_crcs, uint32_t* h_slice_crcs,
+                        uint32_t* h_file_crcs, const cc_scan_digest* dg) {
+    if (n_chunks == 0) {
+        if (dg && dg->h_digest && dg->n_groups) memset(dg->h_digest, 0, dg->n_groups * 4);
+        return CC_OK;
+    }
     if (!chunks || !page_size_ok(page_bytes) || !page_size_ok(meta_bytes) || chunk_bytes == 0 ||
         slice_bytes == 0 || chunk_bytes % slice_bytes || slice_bytes % page_bytes)
         return CC_EINVAL;
-    DevCtx* c = nullptr;
+    // every argument is checked before the first byte moves: a bad chunk or a
+    // copyset index outside the digest must not surface half way through
+    for (uint64_t i = 0; i < n_chunks; i++)
+        if (!chunks[i].data || !chunks[i].meta) return CC_EINVAL;
+    if (dg) {
+        if (!dg->h_after_bytes || !dg->h_group || !dg->h_digest || dg->n_groups == 0 ||
+            dg->n_groups >= (1ull << 32))
+            return CC_EINVAL;
+        for (uint64_t i = 0; i < n_chunks; i++)
+            if (dg->h_group[i] >= dg->n_groups) return CC_EINVAL;
+    }
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(c->submit);
-    if ((rc = staging_init(c))) return rc;
+    if ((rc = staging_init(c.get()))) return rc;
     Staging& st = c->st;
+    SlotRing ring(st);
     const uint64_t per_chunk_dev = (uint64_t)chunk_bytes + meta_bytes;
     const uint64_t batch = st.bytes / per_chunk_dev;
     if (batch == 0) return CC_EINVAL;  // staging smaller than one chunk file
     const uint32_t slices = chunk_bytes / slice_bytes;
     const uint64_t pages_per_chunk = chunk_bytes / page_bytes;
     // per-slot device result region (carved from dcrc, sized per/256*4 bytes):
-    // page CRCs [batch*pages_per_chunk] | meta [batch] | slices [batch*slices] | data [batch] | file [batch]
+    // meta [batch] | slices [batch*slices] | file [batch] | data [batch] | page CRCs [batch*pages_per_chunk]
     const uint64_t need_words = batch * pages_per_chunk + batch * (3 + (uint64_t)slices);
     if (need_words * 4 > st.bytes / 256 * 4) return CC_EINVAL;
     const uint32_t k_page = kconst_for(page_bytes), k_meta = kconst_for(meta_bytes);
@@ -821,53 +1042,85 @@ int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_b
     const uint32_t m_chunk = xpow((uint64_t)chunk_bytes << 3);
     EpilogueLaunch epi = {};
     const bool use_epi = chunk_bytes % page_bytes == 0 &&
-                         epilogue_geometry(c, (uint32_t)pages_per_chunk, page_bytes, slice_bytes / page_bytes, &epi);
-
-    const bool pinned0 = is_pinned(chunks[0].data) && is_pinned(chunks[0].meta);
-    uint64_t pend_first[2] = {0, 0}, pend_n[2] = {0, 0};
+                         epilogue_geometry(c.get(), (uint32_t)pages_per_chunk, page_bytes, slice_bytes / page_bytes,
+                                           &epi);
     hipError_t e = hipSuccess;
-    auto drain = [&](int s) -> int {
-        if (!pend_n[s]) return CC_OK;
-        hipError_t ee = park_slot(st, s);
-        if (ee != hipSuccess) return map_err(ee);
-        const uint32_t* r = st.hcrc[s];
-        const uint64_t nb = pend_n[s], f = pend_first[s];
-        const uint32_t* rm = r;
-        const uint32_t* rs = r + nb;
-        const uint32_t* rf = r + nb + nb * slices;
-        if (h_meta_crcs) memcpy(h_meta_crcs + f, rm, nb * 4);
-        if (h_slice_crcs) memcpy(h_slice_crcs + f * slices, rs, nb * slices * 4);
-        if (h_file_crcs) memcpy(h_file_crcs + f, rf, nb * 4);
-        pend_n[s] = 0;
-        return CC_OK;
+
+    // streamed digest: after bytes + copyset index uploaded once, multipliers
+    // x^(8*after) computed on the device, accumulator zeroed; both slot streams
+    // wait for that before their first epilogue
+    uint64_t* d_after = nullptr;
+    uint32_t *d_mult = nullptr, *d_group = nullptr, *d_digest = nullptr;
+    if (dg) {
+        const uint64_t bytes = align256(n_chunks * 8) + 2 * align256(n_chunks * 4) + align256(dg->n_groups * 4);
+        if (bytes > st.aux_bytes) {
+            if (st.aux) (void)hipFree(st.aux);  // previous calls are drained: not in use
+            st.aux = nullptr;
+            st.aux_bytes = 0;
+            if ((e = hipMalloc(&st.aux, bytes)) != hipSuccess) return map_err(e);
+            st.aux_bytes = bytes;
+        }
+        unsigned char* a = static_cast<unsigned char*>(st.aux);
+        d_after = reinterpret_cast<uint64_t*>(a);
+        d_mult = reinterpret_cast<uint32_t*>(a + align256(n_chunks * 8));
+        d_group = reinterpret_cast<uint32_t*>(a + align256(n_chunks * 8) + align256(n_chunks * 4));
+        d_digest = reinterpret_cast<uint32_t*>(a + align256(n_chunks * 8) + 2 * align256(n_chunks * 4));
+        hipStream_t s0 = st.stream[0];
+        if ((e = hipMemcpyAsync(d_after, dg->h_after_bytes, n_chunks * 8, hipMemcpyHostToDevice, s0)) != hipSuccess ||
+            (e = hipMemcpyAsync(d_group, dg->h_group, n_chunks * 4, hipMemcpyHostToDevice, s0)) != hipSuccess ||
+            (e = hipMemsetAsync(d_digest, 0, dg->n_groups * 4, s0)) != hipSuccess ||
+            (e = launch_xpow8(d_after, n_chunks, d_mult, s0)) != hipSuccess ||
+            (e = hipEventRecord(st.aux_ready, s0)) != hipSuccess ||
+            (e = hipStreamWaitEvent(st.stream[1], st.aux_ready, 0)) != hipSuccess)
+            return ring.fail(map_err(e));
+    }
+
+    auto take = [&](int s) {
+        return [&, s](uint64_t f, uint64_t nb) {
+            const uint32_t* r = st.hcrc[s];
+            if (h_meta_crcs) memcpy(h_meta_crcs + f, r, nb * 4);
+            if (h_slice_crcs) memcpy(h_slice_crcs + f * slices, r + nb, nb * slices * 4);
+            if (h_file_crcs) memcpy(h_file_crcs + f, r + nb + nb * slices, nb * 4);
+        };
     };
     int slot = 0;
     for (uint64_t first = 0; first < n_chunks; first += batch) {
         const uint64_t nb = (n_chunks - first < batch) ? n_chunks - first : batch;
-        if ((rc = drain(slot))) return rc;
+        if ((rc = ring.drain(slot, take(slot)))) return rc;  // the slot's staging is free again
         unsigned char* ddata = static_cast<unsigned char*>(st.dev[slot]);
         unsigned char* dmeta = ddata + nb * (uint64_t)chunk_bytes;
         unsigned char* hstage = static_cast<unsigned char*>(st.host[slot]);
         hipStream_t s = st.stream[slot];
+        // pageable metapages are staged contiguously and copied as runs
+        uint64_t run0 = 0, run_n = 0;
+        auto flush_meta_run = [&]() -> hipError_t {
+            if (!run_n) return hipSuccess;
+            const uint64_t o = nb * (uint64_t)chunk_bytes + run0 * (uint64_t)meta_bytes;
+            const hipError_t ee = hipMemcpyAsync(ddata + o, hstage + o, run_n * meta_bytes, hipMemcpyHostToDevice, s);
+            run_n = 0;
+            return ee;
+        };
         for (uint64_t i = 0; i < nb; i++) {
             const cc_chunk_src& cs = chunks[first + i];
-            if (!cs.data || !cs.meta) return CC_EINVAL;
-            const void* sd = cs.data;
-            const void* sm = cs.meta;
-            if (!pinned0) {
-                memcpy(hstage + i * (uint64_t)chunk_bytes, cs.data, chunk_bytes);
-                memcpy(hstage + nb * (uint64_t)chunk_bytes + i * (uint64_t)meta_bytes, cs.meta, meta_bytes);
-                continue;
+            const uint64_t od = i * (uint64_t)chunk_bytes;
+            if (is_pinned(cs.data)) {
+                e = hipMemcpyAsync(ddata + od, cs.data, chunk_bytes, hipMemcpyHostToDevice, s);
+            } else {
+                memcpy(hstage + od, cs.data, chunk_bytes);
+                e = hipMemcpyAsync(ddata + od, hstage + od, chunk_bytes, hipMemcpyHostToDevice, s);
             }
-            if ((e = hipMemcpyAsync(ddata + i * (uint64_t)chunk_bytes, sd, chunk_bytes, hipMemcpyHostToDevice, s)) !=
-                hipSuccess)
-                return map_err(e);
-            if ((e = hipMemcpyAsync(dmeta + i * (uint64_t)meta_bytes, sm, meta_bytes, hipMemcpyHostToDevice, s)) !=
-                hipSuccess)
-                return map_err(e);
+            if (e != hipSuccess) return ring.fail(map_err(e));
+            if (is_pinned(cs.meta)) {
+                if ((e = flush_meta_run()) != hipSuccess) return ring.fail(map_err(e));
+                e = hipMemcpyAsync(dmeta + i * (uint64_t)meta_bytes, cs.meta, meta_bytes, hipMemcpyHostToDevice, s);
+                if (e != hipSuccess) return ring.fail(map_err(e));
+            } else {
+                memcpy(hstage + nb * (uint64_t)chunk_bytes + i * (uint64_t)meta_bytes, cs.meta, meta_bytes);
+                if (!run_n) run0 = i;
+                run_n++;
+            }
         }
-        if (!pinned0 && (e = hipMemcpyAsync(ddata, hstage, nb * per_chunk_dev, hipMemcpyHostToDevice, s)) != hipSuccess)
-            return map_err(e);
+        if ((e = flush_meta_run()) != hipSuccess) return ring.fail(map_err(e));
         uint32_t* res = st.dcrc[slot];
         uint32_t* d_pages = res + nb * (3 + (uint64_t)slices);
         uint32_t* d_meta = res;
@@ -881,51 +1134,78 @@ int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_b
         a.image = c->image;
         a.kconst = k_page;
         a.out = d_pages;
-        geometry_for(c, a.n_pages, &a);
-        if ((e = launch_page_crc(a, s)) != hipSuccess) return map_err(e);
+        geometry_for(c.get(), a.n_pages, &a);
+        if ((e = launch_page_crc(a, s)) != hipSuccess) return ring.fail(map_err(e));
         a.pages = reinterpret_cast<const uint32_t*>(dmeta);
         a.n_pages = nb;
         a.words_per_lane = meta_bytes / kWaveBytes;
         a.kconst = k_meta;
         a.out = d_meta;
-        geometry_for(c, nb, &a);
-        if ((e = launch_page_crc(a, s)) != hipSuccess) return map_err(e);
-        if (use_epi) {  // one fused launch: slices + file CRCs
+        geometry_for(c.get(), nb, &a);
+        if ((e = launch_page_crc(a, s)) != hipSuccess) return ring.fail(map_err(e));
+        if (use_epi) {  // one fused launch: slices + file CRCs (+ digest contributions)
             EpilogueLaunch ea = epi;
             ea.page_crcs = d_pages;
             ea.meta_crcs = d_meta;
             ea.n_chunks = nb;
             ea.slice_crcs = d_slices;
             ea.file_crcs = d_file;
-            if ((e = launch_epilogue(ea, s)) != hipSuccess) return map_err(e);
+            if (dg) {
+                ea.after_mult = d_mult + first;
+                ea.group = d_group + first;
+                ea.digest = d_digest;
+            }
+            if ((e = launch_epilogue(ea, s)) != hipSuccess) return ring.fail(map_err(e));
         } else {
             f1.crcs = d_pages;
             f1.n_groups = nb * slices;
             f1.out = d_slices;
-            if ((e = launch_fold(f1, s)) != hipSuccess) return map_err(e);
+            if ((e = launch_fold(f1, s)) != hipSuccess) return ring.fail(map_err(e));
             f2.crcs = d_slices;
             f2.n_groups = nb;
             f2.out = d_data;
-            if ((e = launch_fold(f2, s)) != hipSuccess) return map_err(e);
-            if ((e = launch_combine(d_meta, d_data, m_chunk, nb, d_file, s)) != hipSuccess) return map_err(e);
+            if ((e = launch_fold(f2, s)) != hipSuccess) return ring.fail(map_err(e));
+            if ((e = launch_combine(d_meta, d_data, m_chunk, nb, d_file, s)) != hipSuccess)
+                return ring.fail(map_err(e));
+            if (dg && (e = launch_digest(d_file, d_after + first, d_group + first, nb, d_digest, s)) != hipSuccess)
+                return ring.fail(map_err(e));
         }
         if ((e = hipMemcpyAsync(st.hcrc[slot], res, nb * (2 + (uint64_t)slices) * 4, hipMemcpyDeviceToHost, s)) !=
             hipSuccess)
-            return map_err(e);
-        if ((e = arm_slot(st, slot, s)) != hipSuccess) return map_err(e);
-        pend_first[slot] = first;
-        pend_n[slot] = nb;
+            return ring.fail(map_err(e));
+        if ((e = arm_slot(st, slot, s)) != hipSuccess) return ring.fail(map_err(e));
+        ring.first[slot] = first;
+        ring.n[slot] = nb;
         slot ^= 1;
     }
-    if ((rc = drain(slot))) return rc;
-    if ((rc = drain(slot ^ 1))) return rc;
+    if ((rc = ring.drain(slot, take(slot)))) return rc;
+    if ((rc = ring.drain(slot ^ 1, take(slot ^ 1)))) return rc;
+    if (dg) {  // every epilogue has completed (both slots drained)
+        hipStream_t s0 = st.stream[0];
+        if ((e = hipMemcpyAsync(st.hcrc[0], d_digest, dg->n_groups * 4 <= st.bytes / 256 * 4 ? dg->n_groups * 4 : 0,
+                                hipMemcpyDeviceToHost, s0)) != hipSuccess ||
+            (e = hipStreamSynchronize(s0)) != hipSuccess)
+            return map_err(e);
+        if (dg->n_groups * 4 <= st.bytes / 256 * 4) {
+            memcpy(dg->h_digest, st.hcrc[0], dg->n_groups * 4);
+        } else if ((e = hipMemcpy(dg->h_digest, d_digest, dg->n_groups * 4, hipMemcpyDeviceToHost)) != hipSuccess) {
+            return map_err(e);
+        }
+    }
     return CC_OK;
 }
 
-// Native file scan.  Batch layout in a staging slot = the pageable layout of
-// cc_scan_host (data of the batch's files back to back, then their metapages),
-// so one H2D per batch; files that fail get status != 0 and their slots are
-// zero-filled (their CRCs are discarded).
+int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_bytes, uint32_t meta_bytes,
+                 uint32_t page_bytes, uint32_t slice_bytes, uint32_t* h_meta_crcs, uint32_t* h_slice_crcs,
+                 uint32_t* h_file_crcs) {
+    return cc_scan_host_digest(chunks, n_chunks, chunk_bytes, meta_bytes, page_bytes, slice_bytes, h_meta_crcs,
+                               h_slice_crcs, h_file_crcs, nullptr);
+}
+
+// Native file scan.  Batch layout in a staging slot = data of the batch's
+// files back to back, then their metapages, so one H2D per batch; files that
+// fail get status != 0 and their slots are zero-filled (their CRCs are
+// discarded).
 namespace {
 constexpr uint64_t kReadPiece = 2ull << 20;  // io work item
 
@@ -952,12 +1232,13 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
     if (!paths || !h_results || !page_size_ok(page_bytes) || !page_size_ok(meta_bytes) || chunk_bytes == 0 ||
         slice_bytes == 0 || chunk_bytes % slice_bytes || slice_bytes % page_bytes)
         return CC_EINVAL;
-    DevCtx* c = nullptr;
+    CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(c->submit);
-    if ((rc = staging_init(c))) return rc;
+    if ((rc = staging_init(c.get()))) return rc;
     Staging& st = c->st;
+    SlotRing ring(st);
     const uint64_t per_file = (uint64_t)chunk_bytes + meta_bytes;
     const uint64_t batch = st.bytes / per_file;
     if (batch == 0) return CC_EINVAL;
@@ -965,7 +1246,8 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
     const uint64_t pages_per_chunk = chunk_bytes / page_bytes;
     if (batch * pages_per_chunk + batch * (3 + (uint64_t)slices) > st.bytes / 256) return CC_EINVAL;
     EpilogueLaunch epi = {};
-    const bool use_epi = epilogue_geometry(c, (uint32_t)pages_per_chunk, page_bytes, slice_bytes / page_bytes, &epi);
+    const bool use_epi =
+        epilogue_geometry(c.get(), (uint32_t)pages_per_chunk, page_bytes, slice_bytes / page_bytes, &epi);
     FoldLaunch f1 = {}, f2 = {};
     f1.per_group = slice_bytes / page_bytes;
     f1.m_unit = xpow((uint64_t)page_bytes << 3);
@@ -976,28 +1258,23 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
     const uint32_t m_chunk = xpow((uint64_t)chunk_bytes << 3);
     const uint32_t threads = io_threads ? (io_threads > 64 ? 64 : io_threads) : 8;
 
-    uint64_t pend_first[2] = {0, 0}, pend_n[2] = {0, 0};
-    auto drain = [&](int s) -> int {
-        if (!pend_n[s]) return CC_OK;
-        hipError_t ee = park_slot(st, s);
-        if (ee != hipSuccess) return map_err(ee);
-        const uint32_t* r = st.hcrc[s];
-        const uint64_t nb = pend_n[s], f = pend_first[s];
-        for (uint64_t i = 0; i < nb; i++) {
-            cc_file_result& fr = h_results[f + i];
-            if (fr.status != 0) continue;
-            fr.meta_crc = r[i];
-            fr.file_crc = r[nb + nb * slices + i];
-            if (h_slice_crcs) memcpy(h_slice_crcs + (f + i) * slices, r + nb + i * slices, slices * 4);
-        }
-        pend_n[s] = 0;
-        return CC_OK;
+    auto take = [&](int s) {
+        return [&, s](uint64_t f, uint64_t nb) {
+            const uint32_t* r = st.hcrc[s];
+            for (uint64_t i = 0; i < nb; i++) {
+                cc_file_result& fr = h_results[f + i];
+                if (fr.status != 0) continue;
+                fr.meta_crc = r[i];
+                fr.file_crc = r[nb + nb * slices + i];
+                if (h_slice_crcs) memcpy(h_slice_crcs + (f + i) * slices, r + nb + i * slices, slices * 4);
+            }
+        };
     };
     int slot = 0;
     hipError_t e;
     for (uint64_t first = 0; first < n_files; first += batch) {
         const uint64_t nb = (n_files - first < batch) ? n_files - first : batch;
-        if ((rc = drain(slot))) return rc;  // slot's previous batch done: its staging is free
+        if ((rc = ring.drain(slot, take(slot)))) return rc;  // slot's previous batch done: its staging is free
         unsigned char* hstage = static_cast<unsigned char*>(st.host[slot]);
         // open + size check serially (cheap), then the reads as ~2 MiB pieces
         // pulled by the io threads (a batch holds only a few 16 MiB files)
@@ -1055,7 +1332,7 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
         unsigned char* ddata = static_cast<unsigned char*>(st.dev[slot]);
         unsigned char* dmeta = ddata + nb * (uint64_t)chunk_bytes;
         if ((e = hipMemcpyAsync(ddata, hstage, nb * per_file, hipMemcpyHostToDevice, s)) != hipSuccess)
-            return map_err(e);
+            return ring.fail(map_err(e));
         uint32_t* res = st.dcrc[slot];
         uint32_t* d_pages = res + nb * (3 + (uint64_t)slices);
         uint32_t* d_meta = res;
@@ -1069,15 +1346,15 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
         a.image = c->image;
         a.kconst = kconst_for(page_bytes);
         a.out = d_pages;
-        geometry_for(c, a.n_pages, &a);
-        if ((e = launch_page_crc(a, s)) != hipSuccess) return map_err(e);
+        geometry_for(c.get(), a.n_pages, &a);
+        if ((e = launch_page_crc(a, s)) != hipSuccess) return ring.fail(map_err(e));
         a.pages = reinterpret_cast<const uint32_t*>(dmeta);
         a.n_pages = nb;
         a.words_per_lane = meta_bytes / kWaveBytes;
         a.kconst = kconst_for(meta_bytes);
         a.out = d_meta;
-        geometry_for(c, nb, &a);
-        if ((e = launch_page_crc(a, s)) != hipSuccess) return map_err(e);
+        geometry_for(c.get(), nb, &a);
+        if ((e = launch_page_crc(a, s)) != hipSuccess) return ring.fail(map_err(e));
         if (use_epi) {
             EpilogueLaunch ea = epi;
             ea.page_crcs = d_pages;
@@ -1085,29 +1362,29 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
             ea.n_chunks = nb;
             ea.slice_crcs = d_slices;
             ea.file_crcs = d_file;
-            if ((e = launch_epilogue(ea, s)) != hipSuccess) return map_err(e);
+            if ((e = launch_epilogue(ea, s)) != hipSuccess) return ring.fail(map_err(e));
         } else {
             f1.crcs = d_pages;
             f1.n_groups = nb * slices;
             f1.out = d_slices;
-            if ((e = launch_fold(f1, s)) != hipSuccess) return map_err(e);
+            if ((e = launch_fold(f1, s)) != hipSuccess) return ring.fail(map_err(e));
             f2.crcs = d_slices;
             f2.n_groups = nb;
             f2.out = d_data;
-            if ((e = launch_fold(f2, s)) != hipSuccess) return map_err(e);
-            if ((e = launch_combine(d_meta, d_data, m_chunk, nb, d_file, s)) != hipSuccess) return map_err(e);
+            if ((e = launch_fold(f2, s)) != hipSuccess) return ring.fail(map_err(e));
+            if ((e = launch_combine(d_meta, d_data, m_chunk, nb, d_file, s)) != hipSuccess)
+                return ring.fail(map_err(e));
         }
         if ((e = hipMemcpyAsync(st.hcrc[slot], res, nb * (2 + (uint64_t)slices) * 4, hipMemcpyDeviceToHost, s)) !=
             hipSuccess)
-            return map_err(e);
-        if ((e = arm_slot(st, slot, s)) != hipSuccess) return map_err(e);
-        pend_first[slot] = first;
-        pend_n[slot] = nb;
+            return ring.fail(map_err(e));
+        if ((e = arm_slot(st, slot, s)) != hipSuccess) return ring.fail(map_err(e));
+        ring.first[slot] = first;
+        ring.n[slot] = nb;
         slot ^= 1;
     }
-    if ((rc = drain(slot))) return rc;
-    if ((rc = drain(slot ^ 1))) return rc;
-    return CC_OK;
+    if ((rc = ring.drain(slot, take(slot)))) return rc;
+    return ring.drain(slot ^ 1, take(slot ^ 1));
 }
 
 }  // extern "C"

@@ -151,10 +151,12 @@ size_t scan_temp_bytes(uint64_t n);
 hipError_t exclusive_scan_u64(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
                               hipStream_t s);
 hipError_t launch_read_verify(const ReadVerifyLaunch& a, hipStream_t s);
-// CRC32C (butil Value) of arbitrary byte ranges of one device buffer.
+// CRC32C (butil Value) of arbitrary byte ranges of one device buffer; one
+// wave per range descriptor batch, range_waves() waves per workgroup.
+int range_waves();
 hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, const void* image,
                             uint32_t* out, int blocks, hipStream_t s);
-// x^(-8t) mod P for t = 0..259 (undoing a row's trailing zero padding)
+// x^(-8t) mod P for t = 0..kXinvEntries-1 (undoing the zero pad after a range in its last 4 KiB block)
 constexpr uint32_t kXinvEntries = 4100;  // x^(-8t), t < 4096 + 4: the zero pad after a range in its last 4 KiB block
 hipError_t upload_xinv(const uint32_t* table);
 

@@ -1324,6 +1324,8 @@ hipError_t launch_fold(const FoldLaunch& a, hipStream_t s) {
 
 hipError_t upload_xinv(const uint32_t* table) { return hipMemcpyToSymbol(HIP_SYMBOL(c_xinv), table, sizeof(XInv)); }
 
+int range_waves() { return kRangeWaves; }
+
 hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, const void* image,
                             uint32_t* out, int blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;

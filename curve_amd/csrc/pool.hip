@@ -116,12 +116,11 @@ int cc_digest_allreduce_dev(cc_comm* comm, uint32_t* d_digest, uint64_t n, void*
     // ring all-gather of the partials into [rank][n], then out = XOR over ranks
     int rc = map_nccl(ncclAllGather(d_digest, comm->gather, n, ncclUint32, comm->nc, s));
     if (rc) return rc;
-    return map_hip(cc::launch_xor_fold(comm->gather, (uint32_t)comm->nranks, n, d_digest, s));
+    return cc_digest_fold_dev(comm->gather, (uint32_t)comm->nranks, n, d_digest, stream);
 }
 
 int cc_pool_scan_dev(const cc_pool_shard* p, cc_comm* comm, void* stream) {
     if (!p) return CC_EINVAL;
-    if (p->n_chunks == 0 && !comm) return CC_OK;
     if (p->page_bytes == 0 || p->slice_bytes == 0 || p->chunk_bytes % p->page_bytes ||
         p->chunk_bytes % p->slice_bytes || p->slice_bytes % p->page_bytes)
         return CC_EINVAL;
@@ -134,6 +133,10 @@ int cc_pool_scan_dev(const cc_pool_shard* p, cc_comm* comm, void* stream) {
     const uint64_t pages = p->n_chunks * (uint64_t)(p->chunk_bytes / p->page_bytes);
     int rc;
     hipError_t e;
+    if (p->n_chunks == 0) {  // an empty shard: zero partials (full digests after the exchange)
+        if (dig && (e = hipMemsetAsync(p->d_digest, 0, p->n_groups * 4, s)) != hipSuccess) return map_hip(e);
+        return comm ? cc_digest_allreduce_dev(comm, p->d_digest, p->n_groups, stream) : CC_OK;
+    }
     if (p->ev_pages_begin && (e = hipEventRecord(static_cast<hipEvent_t>(p->ev_pages_begin), s)) != hipSuccess)
         return map_hip(e);
     // the hot kernel: every 4 KiB data page of the shard

@@ -52,22 +52,28 @@ def copyset_layout(chunk_ids: Sequence[int], copyset_of: Sequence[int], file_byt
 
 def reduce_digests(partial, dist, group=None):
     """XOR-reduce per-copyset partials (int32 tensor [n_groups]) over all ranks:
-    all_gather_into_tensor (RCCL/gloo) then a local XOR fold.  Returns the full
-    digests on every rank."""
+    all_gather_into_tensor (RCCL, or gloo through host memory) then the XOR
+    fold -- on the device through libcurvecrc (cc_digest_fold_dev) when the
+    partials live there, on the host for host tensors.  Returns the full digests
+    on every rank, on the partials' device."""
     import torch
     world = dist.get_world_size(group)
     if world == 1:
         return partial
     dev = partial.device
+    src = partial
     if dist.get_backend(group) == "gloo" and partial.is_cuda:
-        partial = partial.cpu()  # gloo moves host tensors; RCCL works on device tensors
-    gathered = torch.empty(world * partial.numel(), dtype=partial.dtype, device=partial.device)
-    dist.all_gather_into_tensor(gathered, partial.contiguous(), group=group)
+        src = partial.cpu()  # gloo moves host tensors; RCCL works on device tensors
+    gathered = torch.empty(world * src.numel(), dtype=src.dtype, device=src.device)
+    dist.all_gather_into_tensor(gathered, src.contiguous(), group=group)
+    if partial.is_cuda:
+        from .crc import digest_fold_dev
+        return digest_fold_dev(gathered.to(dev), world)
     g = gathered.view(world, -1)
     out = g[0].clone()
     for r in range(1, world):
         out.bitwise_xor_(g[r])
-    return out.to(dev)
+    return out
 
 
 def digests_as_hash_strings(digests) -> List[str]:

@@ -21,6 +21,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <sys/uio.h> /* struct iovec */
 
 #ifdef __cplusplus
 extern "C" {
@@ -32,6 +33,8 @@ extern "C" {
 #define CC_ENOMEM (-12)   /* device or pinned-host allocation failed */
 #define CC_EHIP (-5)      /* a HIP runtime call failed */
 #define CC_ECORRUPT (-74) /* verify found mismatching pages (host verify) */
+#define CC_EIO (-5001)    /* reading or writing a file failed (errno is kept where the call says so) */
+#define CC_ESTALE (-116)  /* a per-page CRC table no longer describes its chunk (sn / write generation) */
 
 /* ------------------------------------------------------------------------
  * CPU primitive -- drop-in for the inline header src/common/crc32.h
@@ -54,8 +57,22 @@ uint32_t crc32c_shift(uint32_t crc, uint64_t nbytes);
  * of a freshly formatted pool chunk (src/tools/curve_format_main.cpp:132). */
 uint32_t crc32c_zeros(uint64_t nbytes);
 
+/* CRC32C over a scattered buffer: crc32c_extend(crc, iov[0] || iov[1] || ...).
+ * Replaces braft::crc32(const butil::IOBuf&) -- the checksum CurveSegment::append
+ * takes over every WAL entry's data IOBuf (src/chunkserver/raftlog/curve_segment.cpp:405,
+ * get_checksum :283-288) -- which walks the IOBuf's blocks and extends one CRC
+ * across them.  Fragments of any length/alignment (0 allowed). */
+uint32_t crc32c_extend_iov(uint32_t crc, const struct iovec* iov, size_t n);
+
 /* Fold n page CRCs (each over page_bytes) into the CRC of their concatenation. */
 uint32_t cc_fold_host(const uint32_t* page_crcs, uint64_t n, uint64_t page_bytes);
+
+/* Batched host fold: out[s] = CRC of pages s*pages_per_slice ..
+ * (s+1)*pages_per_slice - 1, for n_pages / pages_per_slice slices; e.g. the
+ * 1024 page CRCs of a 4 MiB scan slice -> its ScanMap.crc (proto/scan.proto:28,
+ * op_request.cpp:794).  n_pages must be a multiple of pages_per_slice. */
+int cc_slice_fold(const uint32_t* page_crcs, uint64_t n_pages, uint32_t pages_per_slice, uint32_t page_bytes,
+                  uint32_t* out);
 
 /* ------------------------------------------------------------------------
  * Engine lifetime -- created next to ScanManager::Init and torn down at
@@ -123,6 +140,14 @@ typedef struct cc_range {
 int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, uint32_t* d_out,
                       void* stream);
 
+/* Host-resident variant for many separate buffers (e.g. the data of a batch
+ * of WAL entries read from a segment file, CurveSegment::_load_entry,
+ * curve_segment.cpp:307-371): h_out[i] = crc32c_value(h_bufs[i], h_lens[i]).
+ * Buffers are packed into the pinned staging ring and hashed on the device by
+ * the range kernel; a buffer larger than a staging slot is hashed in pieces
+ * combined on the host.  Blocking, thread-safe. */
+int cc_crc_bufs_host(const void* const* h_bufs, const uint64_t* h_lens, uint64_t n, uint32_t* h_out);
+
 /* d_out[i] = x^(8 * d_nbytes[i]) mod P: the multiplier that shifts a CRC by
  * d_nbytes[i] bytes (precompute once per static pool layout for the epilogue's
  * digest). */
@@ -165,6 +190,13 @@ int cc_combine_dev(const uint32_t* d_a, const uint32_t* d_b, uint64_t len_b, uin
 int cc_digest_dev(const uint32_t* d_file_crcs, const uint64_t* d_after_bytes,
                   const uint32_t* d_group, uint64_t n_files, uint32_t* d_digest,
                   void* stream);
+
+/* Device XOR fold of gathered digest partials: d_digest[i] = XOR over r <
+ * nranks of d_gathered[r * n + i].  The local half of the per-copyset digest
+ * exchange for callers that move the partials themselves (any
+ * transport: RCCL all-gather, the MDS, a TCP store); cc_digest_allreduce_dev
+ * runs it after its own RCCL all-gather. */
+int cc_digest_fold_dev(const uint32_t* d_gathered, uint32_t nranks, uint64_t n, uint32_t* d_digest, void* stream);
 
 /* ------------------------------------------------------------------------
  * Host-in / host-out convenience (blocking; thread-safe: one internal
@@ -209,7 +241,8 @@ int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes,
  * writes of one level overlap and applying levels in order equals applying the
  * log in order (later writes win, as raft-log order does).  h_batch_ends[b] =
  * end index of level b in h_out; *n_batches = number of levels (<= max_batches,
- * else CC_EINVAL).  Radix sort by offset + one sweep: O(n). */
+ * else CC_EINVAL).  Radix sort by offset, a sweep for clusters of overlapping
+ * writes, and a max segment tree inside each cluster: O(n log n). */
 int cc_plan_updates(const cc_update* h_in, uint64_t n, cc_update* h_out, uint64_t* h_batch_ends,
                     uint32_t max_batches, uint32_t* n_batches);
 
@@ -276,11 +309,32 @@ typedef struct cc_chunk_src {
  *                                             the copyset chain, copyset_node.cpp:964)
  * Pipelined over two pinned staging slots and two HIP streams: the H2D copy of
  * batch i+1 overlaps the hashing of batch i.  Pinned (hipHostMalloc'ed or
- * registered) sources are DMA'd directly; pageable ones are staged by memcpy.
- * Any output pointer may be NULL.  Blocking; thread-safe (per-device lock). */
+ * registered) sources are DMA'd directly; pageable ones are staged by memcpy
+ * (decided per buffer).  Any output pointer may be NULL.  Every chunk pointer
+ * is checked before any work starts; on an error no batch of the call is left
+ * in flight.  Blocking; thread-safe (per-device lock). */
 int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_bytes,
                  uint32_t meta_bytes, uint32_t page_bytes, uint32_t slice_bytes,
                  uint32_t* h_meta_crcs, uint32_t* h_slice_crcs, uint32_t* h_file_crcs);
+
+/* Per-copyset digest of a streamed scan (BASELINE config 4: "per-copyset
+ * digest", CopysetNode::GetHash, copyset_node.cpp:925-975). */
+typedef struct cc_scan_digest {
+    const uint64_t* h_after_bytes; /* [n_chunks] bytes of the chunk's copyset that sort after its file */
+    const uint32_t* h_group;       /* [n_chunks] copyset index of the chunk, < n_groups */
+    uint64_t n_groups;
+    uint32_t* h_digest;            /* [n_groups] out: XOR_c shift(file CRC of c, after bytes of c) over the
+                                      call's chunks -- the copyset's GetHash value when all its files are in
+                                      the call, else this call's partial (XOR partials of disjoint calls) */
+} cc_scan_digest;
+
+/* cc_scan_host plus the per-copyset digest, computed on the device by the
+ * fused epilogue of every batch (no host pass over the file CRCs).  The chunk
+ * list may mix pinned and pageable buffers.  dg NULL = cc_scan_host. */
+int cc_scan_host_digest(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_bytes,
+                        uint32_t meta_bytes, uint32_t page_bytes, uint32_t slice_bytes,
+                        uint32_t* h_meta_crcs, uint32_t* h_slice_crcs, uint32_t* h_file_crcs,
+                        const cc_scan_digest* dg);
 
 /* Per-file outcome of cc_scan_files. */
 typedef struct cc_file_result {
@@ -328,8 +382,9 @@ int cc_comm_size(const cc_comm* comm);
 int cc_comm_rank(const cc_comm* comm);
 
 /* d_digest[0..n) <- XOR over all ranks of their d_digest[0..n) (in place;
- * collective, stream-ordered, enqueue only).  Calls on one communicator must
- * be issued in the same order on every rank, from one stream at a time. */
+ * collective, stream-ordered, enqueue only): ncclAllGather of the partials,
+ * then cc_digest_fold_dev.  Calls on one communicator must be issued in the
+ * same order on every rank, from one stream at a time. */
 int cc_digest_allreduce_dev(cc_comm* comm, uint32_t* d_digest, uint64_t n, void* stream);
 
 /* One rank's shard of the pool and the outputs of one scan pass over it. */

@@ -28,8 +28,10 @@
  * classic zlib crc32_combine construction) -- deliberately a different method
  * from the product's polynomial exponentiation.
  */
+#define _POSIX_C_SOURCE 200809L
 #include <stdint.h>
 #include <stddef.h>
+#include <time.h>
 #include <string.h>
 #include <pthread.h>
 #include <nmmintrin.h>
@@ -186,4 +188,21 @@ int oc_page_crcs_mt(const void *pages, uint64_t n_pages, uint32_t page_bytes, ui
         oc_page_crcs((const unsigned char *)pages + first * (uint64_t)page_bytes, cnt, page_bytes, out + first);
     }
     return started;
+}
+
+/* ---- timing helper (bench.py cpu_baseline leg) -------------------------- */
+/* Calls fn(crc, buf, n) `iters` times back to back, each call seeded with the
+ * previous result (a dependency chain, so the calls cannot overlap), and
+ * returns the elapsed seconds.  fn is any CRC with butil Extend's signature:
+ * oc_crc32c_sse42 here, or libcurvecrc's crc32c_extend passed in by address --
+ * a C loop, so a 4 KiB call is timed without any Python per-call overhead. */
+typedef uint32_t (*oc_crc_fn)(uint32_t, const void *, size_t);
+double oc_time_calls(oc_crc_fn fn, const void *buf, size_t n, uint64_t iters, uint32_t *sink) {
+    struct timespec a, b;
+    uint32_t c = 0;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (uint64_t i = 0; i < iters; i++) c = fn(c, buf, n);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    if (sink) *sink = c;
+    return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
 }

@@ -1,0 +1,18 @@
+"""bench.py honours --gpus (a plain `--gpus 8` used to run one rank
+and report n_gpus 1).  Under a launcher WORLD_SIZE must equal --gpus; the check
+runs before anything touches a GPU, so it is testable here."""
+import json
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+
+def test_world_size_mismatch_refused():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 2, p.stderr[-2000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert "WORLD_SIZE=2" in line["error"]

@@ -72,3 +72,33 @@ def test_fold_host(oracle, golden):
     s = golden["seeded_pages"]
     pages = oracle.splitmix64_bytes(s["seed"], s["n_pages"] * s["page_bytes"])
     assert CR.fold_host(np.array(s["crcs"], dtype=np.uint32), 4096) == oracle.crc32c(pages.tobytes())
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_extend_iov_matches_concatenation(oracle, seed):
+    """crc32c_extend_iov (the drop-in for braft::crc32(const butil::IOBuf&),
+    raftlog/curve_segment.cpp:405) == CRC32(crc, concatenation of the fragments):
+    empty, 1-byte, odd and block-sized fragments at any alignment."""
+    rng = np.random.default_rng(seed)
+    frags = []
+    for _ in range(int(rng.integers(1, 40))):
+        n = int(rng.choice([0, 1, 3, 7, 8, 100, 4096, 8192, int(rng.integers(0, 70000))]))
+        off = int(rng.integers(0, 8))
+        frags.append(rng.integers(0, 256, n + off, dtype=np.uint8)[off:])
+    crc0 = int(rng.integers(0, 2**32)) if seed else 0
+    whole = b"".join(f.tobytes() for f in frags)
+    assert CR.CRC32_iov(frags, crc0) == oracle.crc32c(whole, crc0)
+    assert CR.CRC32_iov([], crc0) == crc0
+
+
+def test_slice_fold_batched(oracle):
+    """cc_slice_fold: page CRCs -> slice CRCs == CRC32 of each slice."""
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, 64 * 4096, dtype=np.uint8)
+    pc = oracle.page_crcs(data, 4096)
+    for pps in (1, 2, 16, 64):
+        got = CR.slice_fold(pc, pps, 4096)
+        want = [oracle.crc32c(data[s * pps * 4096:(s + 1) * pps * 4096].tobytes()) for s in range(64 // pps)]
+        assert got.tolist() == want
+    with pytest.raises(CR.CurveCrcError):
+        CR.slice_fold(pc[:10], 4, 4096)

@@ -1,0 +1,122 @@
+"""BASELINE config 5 (the node-level pool scan) with more than one
+rank, on the one-GPU test box: two (and three) gloo ranks share cuda:0; each
+runs the native one-call shard scan (cc_pool_scan_dev) over its chunk range, the
+per-copyset XOR partials are all-gathered over gloo and folded ON THE DEVICE by
+cc_digest_fold_dev -- the same fold cc_digest_allreduce_dev runs after its RCCL
+all-gather (RCCL itself refuses two ranks on one device, "Duplicate GPU
+detected", so the RCCL transport is exercised at world 1 in test_pool_native.py
+and at N GPUs by the driver's multi-GPU bench).  The reduced digests must equal
+CopysetNode::GetHash's sorted-name chain (copyset_node.cpp:925-975) over the
+WHOLE pool, computed by the oracle."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+N_CHUNKS, CHUNK = 13, 1 << 20
+
+
+def _pool_arrays():
+    rng = np.random.default_rng(2024)
+    data = rng.integers(0, 256, (N_CHUNKS, CHUNK), dtype=np.uint8)
+    meta = rng.integers(0, 256, (N_CHUNKS, 4096), dtype=np.uint8)
+    meta[:, 0] = 2
+    ids = [1, 2, 3, 10, 11, 20, 100, 5, 7, 9, 12, 21, 1000]
+    groups = [i % 4 for i in range(N_CHUNKS)]
+    return data, meta, ids, groups
+
+
+def _rank_main(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from curve_amd import crc as C
+        from curve_amd.pool import copyset_layout, digests_as_hash_strings, pool_scan, reduce_digests, shard_range
+        from curve_amd.scan import DevicePool
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        data, meta, ids, groups = _pool_arrays()
+        lay = copyset_layout(ids, groups, [CHUNK + 4096] * N_CHUNKS)
+        lo, hi = shard_range(N_CHUNKS, rank, world)
+        pool = DevicePool(torch.from_numpy(data[lo:hi]).to(dev), torch.from_numpy(meta[lo:hi]).to(dev), ids[lo:hi],
+                          scan_size=256 << 10)
+        after = torch.tensor(lay.after_bytes[lo:hi], dtype=torch.int64, device=dev)
+        grp = torch.tensor(lay.group[lo:hi], dtype=torch.int32, device=dev)
+        digest = torch.full((lay.n_groups,), -1, dtype=torch.int32, device=dev)
+        pool_scan(pool, C.xpow8(after), grp, digest)  # one native call: pages, slices, files, partials
+        full = reduce_digests(digest, dist)            # gloo all-gather + cc_digest_fold_dev
+        torch.cuda.synchronize()
+        q.put((rank, digests_as_hash_strings(full), [int(x) & 0xFFFFFFFF for x in pool.file_crcs.cpu().tolist()]))
+    except Exception as e:  # report to the parent instead of hanging it
+        q.put((rank, repr(e), None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_pool_scan_device_fold_matches_whole_pool_chain(oracle, world):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.multiprocessing as mp
+    from curve_amd.pool import copyset_layout, shard_range
+    from curve_amd.scan import chunk_file_name
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in ps]
+    try:
+        res = {}
+        for _ in range(world):
+            r, dig, fcs = q.get(timeout=100)
+            res[r] = (dig, fcs)
+    finally:
+        [p.join(timeout=30) for p in ps]
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    data, meta, ids, groups = _pool_arrays()
+    lay = copyset_layout(ids, groups, [CHUNK + 4096] * N_CHUNKS)
+    want = []
+    for g in range(lay.n_groups):
+        files = {chunk_file_name(ids[i]): meta[i].tobytes() + data[i].tobytes()
+                 for i in range(N_CHUNKS) if lay.group[i] == g}
+        want.append(oracle.copyset_hash(files))
+    for r in range(world):
+        assert res[r][0] == want, (r, res[r][0])
+        lo, hi = shard_range(N_CHUNKS, r, world)
+        assert res[r][1] == [oracle.crc32c(meta[i].tobytes() + data[i].tobytes()) for i in range(lo, hi)]
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
+def test_digest_fold_dev_any_rank_count(nranks):
+    """cc_digest_fold_dev (the device XOR fold of the exchange) at 1..8 ranks'
+    worth of gathered partials, against numpy's XOR."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from curve_amd import crc as C
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(nranks)
+    for n in (1, 64, 5000):
+        g = rng.integers(0, 2**32, (nranks, n), dtype=np.uint64).astype(np.uint32)
+        out = C.digest_fold_dev(torch.from_numpy(g.reshape(-1).view(np.int32)).to(dev), nranks)
+        want = np.bitwise_xor.reduce(g, axis=0)
+        assert (out.cpu().numpy().view(np.uint32) == want).all()

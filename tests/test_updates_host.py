@@ -88,3 +88,57 @@ def test_cpp_planner_speed():
     t = time.perf_counter()
     _, _, nb = plan_updates(rec)
     assert 2 <= nb <= 4 and time.perf_counter() - t < 0.05
+
+
+def _levels_bruteforce(dst, lens):
+    """Definition of the level assignment, O(n^2): level(j) = 1 + max level of
+    the earlier writes j overlaps, 0 if none."""
+    lv = []
+    for j in range(len(dst)):
+        m = -1
+        for i in range(j):
+            if dst[i] < dst[j] + lens[j] and dst[j] < dst[i] + lens[i]:
+                m = max(m, lv[i])
+        lv.append(m + 1)
+    return lv
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_levels_match_definition_on_hot_clusters(seed):
+    """The segment-tree level assignment (Python and C++) == the O(n^2)
+    definition on logs that pile onto a few hundred bytes."""
+    from curve_amd.crc import _update_dtype, plan_updates
+    rng = np.random.default_rng(700 + seed)
+    n = 300
+    dst = rng.integers(0, 400, n)
+    lens = rng.integers(1, 120, n)
+    want = _levels_bruteforce(dst.tolist(), lens.tolist())
+    py = split_nonoverlapping(dst, lens)
+    got = np.zeros(n, dtype=int)
+    for b, idx in enumerate(py):
+        got[idx] = b
+    assert got.tolist() == want
+    rec = np.zeros(n, dtype=_update_dtype())
+    rec["dst"], rec["src"], rec["len"] = dst, np.arange(n), lens
+    out, ends, nb = plan_updates(rec)
+    starts = np.concatenate([[0], ends[:-1]]).astype(int)
+    cpp = np.zeros(n, dtype=int)
+    for b, (s0, e0) in enumerate(zip(starts, ends.astype(int))):
+        cpp[out["src"][s0:e0].astype(int)] = b
+    assert cpp.tolist() == want
+
+
+def test_cpp_planner_hot_region_is_not_quadratic():
+    """20,000 writes hammering one 4 KiB block used to cost a pair
+    scan of 2*10^8 checks; the segment tree makes it O(n log n)."""
+    import time
+    from curve_amd.crc import _update_dtype, plan_updates
+    rng = np.random.default_rng(10)
+    n = 20000
+    rec = np.zeros(n, dtype=_update_dtype())
+    rec["dst"] = rng.integers(0, 4096, n)
+    rec["len"] = rng.integers(1, 4096, n)
+    t = time.perf_counter()
+    _, ends, nb = plan_updates(rec, max_batches=n)
+    assert time.perf_counter() - t < 0.5
+    assert nb > 100 and int(ends[-1]) == n
