@@ -861,13 +861,32 @@ inline bool log_page_ok(uint32_t page_bytes) {
 inline uint32_t log_slots(uint32_t max_len, uint32_t page_bytes) { return (max_len - 1) / page_bytes + 2; }
 }  // namespace
 
+namespace {
+// Work layout of the write log: counters (head_count, hot_count) | page table |
+// next links | head slots | hot slots.  Only the counters and the table are
+// cleared per call (one memset).
+struct LogWork {
+    uint64_t n_pieces, table_entries, table_off, next_off, heads_off, hot_off, bytes;
+};
+bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork* w) {
+    if (!log_page_ok(page_bytes) || max_len == 0 || n_updates == 0) return false;
+    w->n_pieces = n_updates * log_slots(max_len, page_bytes);
+    if (w->n_pieces >= (1ull << 31)) return false;
+    uint64_t te = 1024;
+    while (te < 2 * w->n_pieces) te <<= 1;  // <= 50 % load
+    w->table_entries = te;
+    w->table_off = 256;
+    w->next_off = w->table_off + te * 8;
+    w->heads_off = w->next_off + align256(w->n_pieces * 4);
+    w->hot_off = w->heads_off + align256(w->n_pieces * 4);
+    w->bytes = w->hot_off + align256(w->n_pieces * 4);
+    return true;
+}
+}  // namespace
+
 uint64_t cc_apply_log_work_bytes(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes) {
-    if (!log_page_ok(page_bytes) || max_len == 0 || n_updates == 0) return 0;
-    const uint64_t nk = n_updates * log_slots(max_len, page_bytes);
-    if (nk >= (1ull << 31)) return 0;
-    const size_t temp = log_sort_temp_bytes(nk);
-    if (!temp) return 0;
-    return 5 * align256(nk * 4) + 256 + align256(temp);
+    LogWork w;
+    return log_work(n_updates, max_len, page_bytes, &w) ? w.bytes : 0;
 }
 
 namespace {
@@ -879,13 +898,14 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
     if (!d_pool || !d_src || !d_log || !d_page_crcs || !d_work || max_len == 0) return CC_EINVAL;
     if (pool_bytes % page_bytes || ((uintptr_t)d_pool & 3u) || ((uintptr_t)d_src & 3u)) return CC_EINVAL;
     const uint64_t n_pages = pool_bytes / page_bytes;
-    if (n_pages >= kNoPiece) return CC_EINVAL;  // page index must fit a 32-bit key below kNoPiece
-    const uint64_t need = cc_apply_log_work_bytes(n_updates, max_len, page_bytes);
-    if (need == 0 || work_bytes < need) return CC_EINVAL;
+    if (n_pages >= kNoPiece) return CC_EINVAL;  // page + 1 must fit the table entry's 32-bit key
+    LogWork lw;
+    if (!log_work(n_updates, max_len, page_bytes, &lw) || work_bytes < lw.bytes) return CC_EINVAL;
     CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    unsigned char* w = static_cast<unsigned char*>(d_work);
     LogLaunch a = {};
     a.pool = static_cast<unsigned char*>(d_pool);
     a.pool_bytes = pool_bytes;
@@ -895,36 +915,26 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
     a.page_bytes = page_bytes;
     a.max_len = max_len;
     a.slots = log_slots(max_len, page_bytes);
-    const uint64_t nk = n_updates * a.slots;
-    unsigned char* w = static_cast<unsigned char*>(d_work);
-    a.keys = reinterpret_cast<uint32_t*>(w);
-    uint32_t* skeys = reinterpret_cast<uint32_t*>(w + align256(nk * 4));
-    a.vals = reinterpret_cast<uint32_t*>(w + 2 * align256(nk * 4));
-    uint32_t* svals = reinterpret_cast<uint32_t*>(w + 3 * align256(nk * 4));
-    a.heads = reinterpret_cast<uint32_t*>(w + 4 * align256(nk * 4));
-    a.head_count = reinterpret_cast<uint32_t*>(w + 5 * align256(nk * 4));
-    void* temp = w + 5 * align256(nk * 4) + 256;
-    a.skeys = skeys;
-    a.svals = svals;
-    a.n_keys = nk;
+    a.n_pieces = lw.n_pieces;
+    a.head_count = reinterpret_cast<uint32_t*>(w);
+    a.hot_count = reinterpret_cast<uint32_t*>(w + 4);
+    a.table = reinterpret_cast<uint64_t*>(w + lw.table_off);
+    a.table_mask = (uint32_t)(lw.table_entries - 1);
+    a.next = reinterpret_cast<uint32_t*>(w + lw.next_off);
+    a.heads = reinterpret_cast<uint32_t*>(w + lw.heads_off);
+    a.hot = reinterpret_cast<uint32_t*>(w + lw.hot_off);
     a.image = c->image;
     a.kconst = kconst_for(page_bytes);
     a.page_crcs = d_page_crcs;
     a.delta = delta;
-    // sort only the bits a page index can have, + 1 so kNoPiece sorts last
-    int end_bit = 1;
-    while (end_bit < 32 && (1ull << end_bit) < n_pages) end_bit++;
-    if (end_bit < 32) end_bit++;
-    // at most n_keys page runs: a wave per run up to one 8-wave block per CU
-    const uint64_t blocks = (nk + kLogWaves - 1) / kLogWaves;
+    // at most n_pieces touched pages: a wave per page up to one block per CU
+    const uint64_t blocks = (lw.n_pieces + kLogWaves - 1) / kLogWaves;
     a.blocks = (int)(blocks < (uint64_t)c->cus ? (blocks ? blocks : 1) : (uint64_t)c->cus);
     hipError_t e;
-    if ((e = launch_log_expand(a, s)) != hipSuccess) return map_err(e);
-    if ((e = log_sort(temp, work_bytes - 5 * align256(nk * 4) - 256, a.keys, skeys, a.vals, svals, nk, end_bit,
-                      s)) != hipSuccess)
-        return map_err(e);
-    if ((e = launch_log_heads(a, s)) != hipSuccess) return map_err(e);
-    return map_err(launch_log_pages(a, s));
+    if ((e = hipMemsetAsync(w, 0, lw.next_off, s)) != hipSuccess) return map_err(e);  // counters + table
+    if ((e = launch_log_insert(a, s)) != hipSuccess) return map_err(e);
+    if ((e = launch_log_pages(a, s)) != hipSuccess) return map_err(e);
+    return map_err(launch_log_hot(a, s));
 }
 }  // namespace
 

@@ -85,10 +85,11 @@ hipError_t launch_apply_updates(const UpdateLaunch& a, hipStream_t s);
 hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s);
 
 // Write-log path (cc_apply_log_dev): every update of an ORDERED log becomes
-// `slots` pieces keyed by the page they touch (0xFFFFFFFF = no piece); a stable
-// sort by page keeps write order inside each page; the page runs' starts are
-// compacted; one wave per touched page (balanced over the grid) then applies
-// its pieces in registers, stores the changed rows and rehashes it.
+// `slots` pieces, one per page it touches; an open-addressing table keyed by
+// page groups them (each entry heads a linked list of the page's pieces) with
+// no sort; one wave per touched page (balanced over the grid) then applies its
+// pieces in log order in registers, stores the changed rows and rehashes it.
+// Pages with more than 64 pieces are finished by a log-replay kernel.
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
 #ifndef CC_LOG_WAVES
 #define CC_LOG_WAVES 12  // waves per CU of the write-log page kernel (A/B: 12 beats 8 by ~6 %; 16 forces <= 128 VGPRs and spills in delta mode)
@@ -103,25 +104,23 @@ struct LogLaunch {
     uint32_t page_bytes;
     uint32_t max_len;
     uint32_t slots;             // pieces per update: (max_len - 1) / page_bytes + 2
-    uint32_t* keys;             // [n_updates * slots] page of each piece
-    uint32_t* vals;             // [n_updates * slots] update index of each piece
-    const uint32_t* skeys;      // sorted
-    const uint32_t* svals;
-    uint64_t n_keys;
-    uint32_t* heads;            // [n_keys] sorted positions that start a page run (unordered)
-    uint32_t* head_count;       // number of them (zeroed by the expand kernel)
+    uint64_t n_pieces;          // n_updates * slots
+    uint64_t* table;            // [table_mask + 1] {page + 1, piece + 1} of the page's list head (0 = empty)
+    uint32_t table_mask;
+    uint32_t* next;             // [n_pieces] next piece of the same page (kNoPiece = end)
+    uint32_t* heads;            // [n_pieces] table slots of the touched pages (unordered)
+    uint32_t* head_count;       // number of them
+    uint32_t* hot;              // [n_pieces] table slots of pages with > 64 pieces
+    uint32_t* hot_count;
     const void* image;
     uint32_t kconst;
     uint32_t* page_crcs;        // out; in delta mode also in (the CRCs before the batch)
     int blocks;
     int delta;                  // 1: update the stored CRCs through linearity (reads touched rows only)
 };
-hipError_t launch_log_expand(const LogLaunch& a, hipStream_t s);
-hipError_t launch_log_heads(const LogLaunch& a, hipStream_t s);
+hipError_t launch_log_insert(const LogLaunch& a, hipStream_t s);
 hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s);
-size_t log_sort_temp_bytes(uint64_t n);
-hipError_t log_sort(void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
-                    const uint32_t* vals_in, uint32_t* vals_out, uint64_t n, int end_bit, hipStream_t s);
+hipError_t launch_log_hot(const LogLaunch& a, hipStream_t s);
 
 struct RangeDesc {
     uint64_t off, len;

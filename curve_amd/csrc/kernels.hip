@@ -762,22 +762,63 @@ __global__ __launch_bounds__(kBlockThreads) void page_flagged_kernel(UpdateLaunc
 // ---------------------------------------------------------------------------
 // Write-log path (cc_apply_log_dev): ordering on the device, no host planning.
 // ---------------------------------------------------------------------------
-// Piece generation: update i -> slots keys (page it touches, or kNoPiece) and
-// values (= i).  Written in write order, so the stable sort keeps it per page.
-// An update that breaks the contract (len 0, len > max_len, beyond the pool)
-// produces no pieces and is not applied at all (never half-applied).
-__global__ void log_expand_kernel(LogLaunch a) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) *a.head_count = 0u;  // for log_heads_kernel, later on the stream
-    if (i >= a.n_updates) return;
-    const UpdateDesc d = a.upd[i];
-    const bool ok = d.len >= 1 && d.len <= a.max_len && d.dst < a.pool_bytes && d.len <= a.pool_bytes - d.dst;
-    const uint64_t p0 = ok ? d.dst / a.page_bytes : 0;
-    const uint64_t p1 = ok ? (d.dst + d.len - 1) / a.page_bytes : 0;
-    for (uint32_t k = 0; k < a.slots; k++) {
-        const bool v = ok && p0 + k <= p1;
-        a.keys[i * a.slots + k] = v ? (uint32_t)(p0 + k) : kNoPiece;
-        a.vals[i * a.slots + k] = (uint32_t)i;
+// Grouping by page without a sort.  Piece t = (update t / slots, its k-th page,
+// k = t % slots).  Every piece inserts its page into an open-addressing table
+// (linear probing, <= 50 % load) whose 64-bit entry holds {page + 1, piece + 1}
+// of the page's most recently inserted piece: one CAS both claims the page and
+// pushes the piece onto the page's list (next[piece] = the previous head).
+// The piece that claims an empty entry appends the entry's slot to the head
+// list (one atomic per wave).  The list order is arbitrary; the page kernel
+// restores log order from the update indices.  An update that breaks the
+// contract (len 0, len > max_len, beyond the pool) produces no pieces and is
+// not applied at all (never half-applied).  The table and the counters were
+// zeroed earlier on the stream.
+__device__ __forceinline__ uint32_t page_hash(uint32_t page, uint32_t mask) {
+    return (page * 2654435761u) & mask;  // Fibonacci hashing; sequential pages spread
+}
+
+__global__ __launch_bounds__(256) void log_insert_kernel(LogLaunch a) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    bool fresh = false;
+    uint32_t slot = 0;
+    if (t < a.n_pieces) {
+        const uint64_t i = t / a.slots;
+        const uint32_t k = (uint32_t)(t - i * a.slots);
+        const UpdateDesc d = a.upd[i];
+        const bool ok = d.len >= 1 && d.len <= a.max_len && d.dst < a.pool_bytes && d.len <= a.pool_bytes - d.dst;
+        const uint64_t p0 = ok ? d.dst / a.page_bytes : 0;
+        const uint64_t p1 = ok ? (d.dst + d.len - 1) / a.page_bytes : 0;
+        if (ok && p0 + k <= p1) {
+            const uint32_t page = (uint32_t)(p0 + k);
+            const unsigned long long tag = (unsigned long long)(page + 1u) << 32;
+            unsigned long long* tab = reinterpret_cast<unsigned long long*>(a.table);
+            slot = page_hash(page, a.table_mask);
+            // CAS first (one atomic for a page seen first, the common case);
+            // next[] is only read by later kernels, so it can follow the CAS
+            unsigned long long cur = 0ull;
+            for (;;) {
+                const unsigned long long old = atomicCAS(tab + slot, cur, tag | (unsigned long long)(t + 1));
+                if (old == cur) {  // claimed (cur == 0) or pushed onto the page's list
+                    a.next[t] = cur ? (uint32_t)cur - 1u : kNoPiece;
+                    fresh = cur == 0ull;
+                    break;
+                }
+                if (old == 0ull || (old & 0xFFFFFFFF00000000ull) == tag) {
+                    cur = old;  // the page's entry (or an empty one): retry against it
+                    continue;
+                }
+                slot = (slot + 1u) & a.table_mask;  // another page: probe on, expecting empty
+                cur = 0ull;
+            }
+        }
+    }
+    const uint64_t m = __ballot(fresh);
+    if (m) {
+        uint32_t base = 0;
+        if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(a.head_count, (uint32_t)__popcll(m));
+        base = __shfl(base, (int)__builtin_ctzll(m), 64);
+        if (fresh) a.heads[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = slot;
     }
 }
 
@@ -911,41 +952,16 @@ __device__ __forceinline__ void merge_piece(uint32_t (&w)[M], uint32_t& dirty, c
 }
 
 
-// Page runs of the sorted pieces: position q starts a run (a "head") when its
-// page differs from position q-1's.  Heads are compacted into a.heads (in no
-// particular order: runs are independent) with one atomic per wave; the count
-// was zeroed by log_expand_kernel earlier on the stream.
-__global__ __launch_bounds__(1024) void log_heads_kernel(LogLaunch a) {
-    __shared__ uint32_t wcount[16], bbase;
-    const uint64_t pos = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const bool in = pos < a.n_keys;
-    const uint32_t key = in ? a.skeys[pos] : kNoPiece;
-    const uint32_t prev = (in && pos > 0) ? a.skeys[pos - 1] : kNoPiece;
-    const bool head = key != kNoPiece && key != prev;
-    const uint64_t m = __ballot(head);
-    if (lane == 0) wcount[wv] = (uint32_t)__popcll(m);
-    __syncthreads();
-    if (threadIdx.x == 0) {  // one global atomic per 1024 positions
-        uint32_t tot = 0;
-        for (uint32_t w = 0; w < blockDim.x / 64; w++) tot += wcount[w];
-        bbase = tot ? atomicAdd(a.head_count, tot) : 0u;
-    }
-    __syncthreads();
-    uint32_t base = bbase;
-    for (uint32_t w = 0; w < wv; w++) base += wcount[w];
-    if (head) a.heads[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)pos;
-}
-
 // One wave per touched page, balanced: wave w owns heads w, w + W, w + 2W, ...
 // (W = waves in the grid), ~pages/W each.  Its lanes load the metadata of up to
-// 64 of its heads at once (position, page, next position's page, update
-// descriptor: one round trip per 64 pages), then the wave software-pipelines
-// them: while page k's pieces are merged, stored and hashed, page k+1's data
-// AND the source bytes of its first piece are in flight.  A page with more
-// pieces (overlapping / neighbouring writes: rare) reads them from the sorted
-// arrays in place, in write order.  Every page is owned by exactly one wave: no
-// write races, no flags, no atomics on the data.
+// 64 of its heads at once (table entry: page + one piece, that piece's list
+// link and update descriptor: a few round trips per 64 pages), then the wave
+// software-pipelines them: while page k's pieces are merged, stored and
+// hashed, page k+1's data AND the source bytes of its piece are in flight.  A
+// page with several pieces (overlapping / neighbouring writes: rare) walks its
+// list, ranks the pieces by update index and applies them in log order; a
+// page with more than 64 goes to the hot list (log_hot_kernel).  Every page is
+// owned by exactly one wave: no write races, no flags, no atomics on the data.
 #if CC_LOG_WAVES == 16
 #define CC_LOG_ATTR __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 4)))
 #else
@@ -986,13 +1002,15 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
         // lane k <- head base + k*W (clamped loads: no branches around them)
         const uint64_t ih = (uint64_t)base + (uint64_t)lane * W;
         const bool hv = ih < H;
-        const uint32_t pos = a.heads[hv ? ih : base];
-        const uint32_t key = a.skeys[pos];
-        const uint32_t nkey = a.skeys[pos + 1 < a.n_keys ? pos + 1 : pos];
-        const UpdateDesc d = a.upd[a.svals[pos]];
+        const uint32_t hslot = a.heads[hv ? ih : base];
+        const unsigned long long ent = reinterpret_cast<const unsigned long long*>(a.table)[hslot];
+        const uint32_t key = (uint32_t)(ent >> 32) - 1u;  // the page
+        const uint32_t pfirst = (uint32_t)ent - 1u;       // one of its pieces (the list head)
+        const uint32_t nxt = a.next[pfirst];
+        const UpdateDesc d = a.upd[pfirst / a.slots];
         const uint64_t ddst = d.dst, dsrc = d.src;
         const uint32_t dlen = d.len;
-        const bool single = pos + 1 >= a.n_keys || nkey != key;  // the page's only piece
+        const bool single = nxt == kNoPiece;  // the page's only piece
         const uint64_t singles = __ballot(single);
         const uint32_t cnt = (uint32_t)__popcll(__ballot(hv));  // valid lanes are 0 .. cnt-1
         // two pages in flight: k (being merged + hashed) and k+1.  (A third
@@ -1043,14 +1061,30 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
 #pragma unroll
                 for (int j = 0; j < M; j++) O[j] = X[j];
             }
-            merge_piece<M>(X, dirty, SX, px, lane);
-            if (!((singles >> hh) & 1ull)) {  // further pieces of this page, in write order
-                for (uint32_t q = __builtin_amdgcn_readlane(pos, hh) + 1; q < a.n_keys; q++) {
-                    if (a.skeys[q] != pg) break;
-                    const UpdateDesc dq = a.upd[a.svals[q]];
-                    const Piece pq = piece_in_page(pbase, pb, dq.dst, dq.src, dq.len, a.src);
-                    fetch_piece<M>(SX, pq, lane);  // SX is consumed: reuse its registers
-                    merge_piece<M>(X, dirty, SX, pq, lane);
+            bool hot = false;
+            if ((singles >> hh) & 1ull) {
+                merge_piece<M>(X, dirty, SX, px, lane);
+            } else {  // several pieces: collect the list, apply in log (update index) order
+                uint32_t q = __builtin_amdgcn_readlane(pfirst, hh), cnt = 0, mine = kNoPiece;
+                while (q != kNoPiece && cnt < 64u) {
+                    mine = lane == cnt ? q : mine;
+                    cnt++;
+                    q = a.next[q];
+                }
+                if (q != kNoPiece) {  // > 64 pieces: the hot-page kernel replays the log for it
+                    hot = true;
+                    if (lane == 0) a.hot[atomicAdd(a.hot_count, 1u)] = __builtin_amdgcn_readlane(hslot, hh);
+                } else {
+                    const uint32_t idx = lane < cnt ? mine / a.slots : 0xFFFFFFFFu;
+                    uint32_t rank = lane < cnt ? 0u : 0xFFFFu;
+                    for (uint32_t j = 0; j < cnt; j++) rank += (uint32_t)__builtin_amdgcn_readlane(idx, j) < idx;
+                    for (uint32_t r = 0; r < cnt; r++) {
+                        const uint32_t l = (uint32_t)__builtin_ctzll(__ballot(rank == r));
+                        const UpdateDesc dq = a.upd[__builtin_amdgcn_readlane(idx, l)];
+                        const Piece pq = piece_in_page(pbase, pb, dq.dst, dq.src, dq.len, a.src);
+                        fetch_piece<M>(SX, pq, lane);  // SX (the prefetched head piece) is not used: reuse it
+                        merge_piece<M>(X, dirty, SX, pq, lane);
+                    }
                 }
             }
             {  // changed rows only; the others get an out-of-range offset and are dropped
@@ -1078,7 +1112,7 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
             } else {
                 crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
             }
-            if (lane == 0) a.page_crcs[pg] = crc;
+            if (lane == 0 && !hot) a.page_crcs[pg] = crc;
             return more;
         };
         // the two register sets alternate (no copies): page k in one while page
@@ -1092,6 +1126,66 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
             if (!step(A, S0, pA, pgA, h, ocA, B, S1, pB, pgB, ocB)) break;
             if (!step(B, S1, pB, pgB, h + 1, ocB, A, S0, pA, pgA, ocA)) break;
         }
+    }
+}
+
+// Pages with more than 64 pieces (a write log hammering a few pages): one wave
+// per hot page replays the whole log in order, 64 records per round trip (a
+// ballot of the records that touch the page), merging their pieces into the
+// page in registers -- log order by construction, any number of pieces.  A
+// grid with no hot page returns before filling its LDS.
+template <int M, bool Delta>
+__global__ CC_LOG_ATTR void log_hot_kernel(LogLaunch a) {
+    __shared__ uint32_t tab[kLdsBytes / 4];
+    const uint32_t HC = *a.hot_count;
+    if ((uint64_t)blockIdx.x * kLogWaves >= HC) return;  // uniform per block: no hot page for it
+    fill_lds<64 * kLogWaves>(tab, static_cast<const uint4*>(a.image));
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t c0 = lane << 2 & 0x7Cu;
+    const uint32_t c1 = c0 | 0x10000u;
+    const uint32_t cf = kFinBase + (lane << 2);
+    const uint32_t* pages = reinterpret_cast<const uint32_t*>(a.pool) + lane;
+    const uint32_t pb = a.page_bytes;
+    const uint32_t W = gridDim.x * kLogWaves;
+    for (uint32_t h = blockIdx.x * kLogWaves + wave; h < HC; h += W) {
+        const unsigned long long ent = reinterpret_cast<const unsigned long long*>(a.table)[a.hot[h]];
+        const uint32_t pg = (uint32_t)(ent >> 32) - 1u;
+        const uint64_t pbase = (uint64_t)pg * pb;
+        uint32_t X[M], O[Delta ? M : 1];
+        load_page<M>(X, pages + (uint64_t)pg * (64u * M));
+        if constexpr (Delta) {
+#pragma unroll
+            for (int j = 0; j < M; j++) O[j] = X[j];
+        }
+        uint32_t dirty = 0;
+        PieceSrc<M> S;
+        for (uint64_t b = 0; b < a.n_updates; b += 64) {
+            const uint64_t i = b + lane;
+            const UpdateDesc d = a.upd[i < a.n_updates ? i : b];
+            const bool ok = i < a.n_updates && d.len >= 1 && d.len <= a.max_len && d.dst < a.pool_bytes &&
+                            d.len <= a.pool_bytes - d.dst && d.dst < pbase + pb && d.dst + d.len > pbase;
+            for (uint64_t m = __ballot(ok); m; m &= m - 1) {  // this round's writes to the page, in log order
+                const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                const Piece pq = piece_in_page(pbase, pb, readlane64(d.dst, l), readlane64(d.src, l),
+                                               __builtin_amdgcn_readlane(d.len, l), a.src);
+                fetch_piece<M>(S, pq, lane);
+                merge_piece<M>(X, dirty, S, pq, lane);
+            }
+        }
+        const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(a.pool + pbase, 0, 256u * M, kBufFlags);
+#pragma unroll
+        for (int j = 0; j < M; j++)
+            __builtin_amdgcn_raw_buffer_store_b32(X[j], rp, (((dirty >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j, 0, 0);
+        uint32_t crc;
+        if constexpr (Delta) {
+#pragma unroll
+            for (int j = 0; j < M; j++) O[j] ^= X[j];
+            crc = wave_xor(apply_fin(tab, chain<M>(tab, O, c0, c1), cf)) ^ a.page_crcs[pg];
+        } else {
+            crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
+        }
+        if (lane == 0) a.page_crcs[pg] = crc;
     }
 }
 
@@ -1367,20 +1461,14 @@ hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_log_expand(const LogLaunch& a, hipStream_t s) {
-    if (a.n_updates == 0) return hipSuccess;
-    hipLaunchKernelGGL(log_expand_kernel, dim3((uint32_t)((a.n_updates + 255) / 256)), dim3(256), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_log_heads(const LogLaunch& a, hipStream_t s) {
-    if (a.n_keys == 0) return hipSuccess;
-    hipLaunchKernelGGL(log_heads_kernel, dim3((uint32_t)((a.n_keys + 1023) / 1024)), dim3(1024), 0, s, a);
+hipError_t launch_log_insert(const LogLaunch& a, hipStream_t s) {
+    if (a.n_pieces == 0) return hipSuccess;
+    hipLaunchKernelGGL(log_insert_kernel, dim3((uint32_t)((a.n_pieces + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s) {
-    if (a.n_keys == 0) return hipSuccess;
+    if (a.n_pieces == 0) return hipSuccess;
 #define CC_GCASE(MM)                                                                                        \
     case MM:                                                                                                \
         if (a.delta)                                                                                        \
@@ -1398,6 +1486,28 @@ hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s) {
         default: return hipErrorInvalidValue;
     }
 #undef CC_GCASE
+    return hipGetLastError();
+}
+
+hipError_t launch_log_hot(const LogLaunch& a, hipStream_t s) {
+    if (a.n_pieces == 0) return hipSuccess;
+#define CC_HCASE(MM)                                                                                      \
+    case MM:                                                                                              \
+        if (a.delta)                                                                                      \
+            hipLaunchKernelGGL((log_hot_kernel<MM, true>), dim3(a.blocks), dim3(64 * kLogWaves), 0, s, a);  \
+        else                                                                                              \
+            hipLaunchKernelGGL((log_hot_kernel<MM, false>), dim3(a.blocks), dim3(64 * kLogWaves), 0, s, a); \
+        break;
+    switch (a.page_bytes / kWaveBytes) {
+        CC_HCASE(1)
+        CC_HCASE(2)
+        CC_HCASE(4)
+        CC_HCASE(8)
+        CC_HCASE(16)
+        CC_HCASE(32)
+        default: return hipErrorInvalidValue;
+    }
+#undef CC_HCASE
     return hipGetLastError();
 }
 

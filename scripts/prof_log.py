@@ -18,6 +18,7 @@ p.add_argument("--reps", type=int, default=5)
 p.add_argument("--lib", default=None, help="libcurvecrc variant to load instead of the in-tree one")
 p.add_argument("--align", type=int, default=1, help="round dst/src offsets and lengths down to this")
 p.add_argument("--delta", action="store_true", help="cc_apply_log_delta_dev (stored CRCs updated by linearity)")
+p.add_argument("--span-gib", type=float, default=0, help="confine write destinations to the first SPAN GiB (locality probe)")
 a = p.parse_args()
 if a.lib:
     from curve_amd import _lib
@@ -31,7 +32,8 @@ rng = np.random.default_rng(1)
 logs = []
 for _ in range(a.reps + 1):
     al = a.align
-    rec = C.log_records(rng.integers(0, pool.numel() - 4096, U) // al * al,
+    span = int(a.span_gib * (1 << 30)) if a.span_gib else pool.numel()
+    rec = C.log_records(rng.integers(0, span - 4096, U) // al * al,
                         rng.integers(0, U * 4096 - 4096, U) // al * al, rng.integers(512, 4097, U) // al * al)
     logs.append(torch.from_numpy(rec.view(np.uint8)).to(dev))
 s = torch.cuda.current_stream()
