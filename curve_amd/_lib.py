@@ -23,6 +23,7 @@ CC_ECORRUPT = -74
 CC_ECOMM = -71
 CC_EIO = -5001
 CC_ESTALE = -116
+CC_ENOENT = -2
 CC_COMM_ID_BYTES = 128
 
 # every symbol include/curve_crc.h declares: (name, restype, argtypes)
@@ -47,6 +48,25 @@ class CcScanDigest(ctypes.Structure):  # include/curve_crc.h cc_scan_digest
 
 class IoVec(ctypes.Structure):  # struct iovec
     _fields_ = [("iov_base", _vp), ("iov_len", _sz)]
+
+
+class CcPcrcHeader(ctypes.Structure):  # include/curve_crc.h cc_pcrc_header
+    _fields_ = [("page_bytes", _u32), ("n_pages", _u32), ("chunk_sn", _u64), ("data_mtime_ns", ctypes.c_int64),
+                ("data_size", _u64)]
+
+
+class CcIntegrityOpts(ctypes.Structure):
+    _fields_ = [("chunk_bytes", _u32), ("meta_bytes", _u32), ("page_bytes", _u32), ("io_threads", _u32),
+                ("create_missing", _u32), ("refresh_stale", _u32)]
+
+
+class CcIntegrityResult(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("table_state", _u32), ("n_pages", _u32), ("bad_pages", _u32),
+                ("first_bad", ctypes.c_int64)]
+
+
+CC_PCRC_HEADER_BYTES = 64
+TABLE_STATES = {0: "ok", 1: "created", 2: "corrupt", 3: "stale", 4: "refreshed", 5: "missing", 6: "rebuilt"}
 
 
 class CcPoolShard(ctypes.Structure):  # include/curve_crc.h cc_pool_shard
@@ -106,6 +126,15 @@ SIGNATURES = {
     "cc_comm_rank": (_int, [_vp]),
     "cc_digest_allreduce_dev": (_int, [_vp, _vp, _u64, _vp]),
     "cc_pool_scan_dev": (_int, [ctypes.POINTER(CcPoolShard), _vp, _vp]),
+    "cc_pcrc_encoded_bytes": (_u64, [_u32]),
+    "cc_pcrc_encode": (_int, [ctypes.POINTER(CcPcrcHeader), _vp, _vp, _u64]),
+    "cc_pcrc_decode": (_int, [_vp, _u64, ctypes.POINTER(CcPcrcHeader), _vp, _u32]),
+    "cc_chunk_meta_sn": (_int, [_vp, _u32, ctypes.POINTER(_u64)]),
+    "cc_pcrc_store": (_int, [ctypes.c_char_p, _u32, ctypes.c_char_p, _vp, _u32, _u32]),
+    "cc_pcrc_load": (_int, [ctypes.c_char_p, ctypes.POINTER(CcPcrcHeader), _vp, _u32]),
+    "cc_integrity_check": (_int, [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p), _u64,
+                                  ctypes.POINTER(CcIntegrityOpts), ctypes.POINTER(CcIntegrityResult), _vp, _u64,
+                                  ctypes.POINTER(_u64)]),
 }
 
 _lib = None

@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -21,6 +22,7 @@
 
 #include "../../include/curve_crc.h"
 #include "chunkserver_host.h"
+#include "integrity_service.h"
 
 extern "C" uint32_t oc_crc32c_sse42(uint32_t crc, const void* buf, size_t n);  // oracle (test only)
 
@@ -353,6 +355,165 @@ void WriteLogBothModes() {  // an ordered write log from plai
     for (void* q : {d_src, d_log, d_work}) EXPECT(hipFree(q) == hipSuccess);
 }
 
+// ---- per-page CRC persistence ------------------------------
+void IntegrityTableAndService() {  // CPU: codec, metapage sn, atomic store / load, service state machine
+    std::vector<uint32_t> pc(256);
+    std::mt19937_64 rng(5);
+    for (auto& c : pc) c = (uint32_t)rng();
+    cc_pcrc_header h = {4096, 256, 9, 123456789, 4096 + (1u << 20)};
+    std::vector<unsigned char> buf(cc_pcrc_encoded_bytes(256));
+    EXPECT(cc_pcrc_encode(&h, pc.data(), buf.data(), buf.size()) == CC_OK);
+    cc_pcrc_header g;
+    std::vector<uint32_t> got(256);
+    EXPECT(cc_pcrc_decode(buf.data(), buf.size(), &g, got.data(), 256) == CC_OK);
+    EXPECT(g.chunk_sn == 9 && g.data_mtime_ns == 123456789 && g.n_pages == 256 && got == pc);
+    for (size_t pos : {0ul, 12ul, 30ul, 58ul, 64ul + 5, buf.size() - 1}) {
+        buf[pos] ^= 1;
+        EXPECT(cc_pcrc_decode(buf.data(), buf.size(), &g, nullptr, 0) == CC_ECORRUPT);
+        buf[pos] ^= 1;
+    }
+    uint64_t sn = 0;
+    const std::string mp = MetaPage(42);
+    EXPECT(cc_chunk_meta_sn(mp.data(), 4096, &sn) == CC_OK && sn == 42);
+    std::string bad = mp;
+    bad[2] ^= 1;
+    EXPECT(cc_chunk_meta_sn(bad.data(), 4096, &sn) == CC_ECORRUPT);
+    const std::string data = MakeDir("integ_cpu"), dd = data + "/data";
+    mkdir(dd.c_str(), 0755);
+    WriteFile(dd + "/chunk_1", mp + std::string(1 << 20, 'z'));
+    const std::string tdir = TableDirFor(dd);
+    EXPECT(tdir == data + "/pcrc");
+    mkdir(tdir.c_str(), 0755);
+    EXPECT(cc_pcrc_store((dd + "/chunk_1").c_str(), 4096, TablePath(tdir, "chunk_1").c_str(), pc.data(), 256, 4096) ==
+           CC_OK);
+    EXPECT(cc_pcrc_load(TablePath(tdir, "chunk_1").c_str(), &g, got.data(), 256) == CC_OK && got == pc && g.chunk_sn == 42);
+    EXPECT(cc_pcrc_store((dd + "/chunk_1").c_str(), 4096, TablePath(tdir, "x").c_str(), pc.data(), 255, 4096) ==
+           CC_EINVAL);  // geometry of the file
+    EXPECT(cc_pcrc_load(TablePath(tdir, "none").c_str(), &g, nullptr, 0) == -ENOENT);
+    // the service state machine (proto/integrity.proto) on a directory with no chunk of the geometry
+    IntegrityOptions o;
+    o.chunkSize = 2u << 20;  // chunk_1 is not of this geometry: nothing to check, no GPU needed
+    IntegrityService svc(o);
+    EXPECT(svc.PauseJob(1) == INTEGRITY_OP_STATUS_FAILURE_UNKNOWN);
+    EXPECT(svc.ScheduleJob(1, 7, dd) == INTEGRITY_OP_STATUS_SUCCESS);
+    EXPECT(svc.ScheduleJob(1, 7, dd) == INTEGRITY_OP_STATUS_FAILURE_UNKNOWN);
+    IntegrityJob j;
+    EXPECT(svc.Wait(1, 20000, &j) && j.state == INTEGRITY_OP_STATE_FINISHED && j.progress == 100 && j.copyset == 7);
+    EXPECT(svc.CancelJob(1) == INTEGRITY_OP_STATUS_FAILURE_UNKNOWN);
+    EXPECT(svc.ScheduleJob(2, 7, dd + "/missing") == INTEGRITY_OP_STATUS_SUCCESS);
+    EXPECT(svc.Wait(2, 20000, &j) && j.state == INTEGRITY_OP_STATE_FAILED && !j.error.empty());
+    std::vector<IntegrityJob> all;
+    EXPECT(svc.ListJobs(&all) == INTEGRITY_OP_STATUS_SUCCESS && all.size() == 2 && all[0].id == 1);
+}
+
+// GPU: the write path keeps the tables current (no false corruption), a write
+// that skips its table is STALE (refreshed, never bad pages), bit rot is
+// reported page-exact.
+void IntegrityWritePath() {
+    const uint32_t pb = 4096, chunk = 1u << 20, meta = 4096, n_chunks = 6, ppc = chunk / pb;
+    const std::string root = MakeDir("integ_gpu"), dd = root + "/data", tdir = root + "/pcrc";
+    mkdir(dd.c_str(), 0755);
+    mkdir(tdir.c_str(), 0755);
+    std::mt19937_64 rng(77);
+    std::string pool((size_t)n_chunks * chunk, '\0');
+    for (auto& c : pool) c = (char)(rng() & 0xFF);
+    std::vector<std::string> paths;
+    for (uint32_t c = 0; c < n_chunks; c++) {
+        paths.push_back(dd + "/" + ChunkFileName(c + 1));
+        WriteFile(paths.back(), MetaPage(c + 1) + pool.substr((size_t)c * chunk, chunk));
+    }
+    // the device pool (data of every chunk) + its CRC table, persisted per chunk
+    void *d_pool, *d_pc, *d_src, *d_log, *d_work;
+    const uint64_t pool_bytes = pool.size(), n_pages = pool_bytes / pb;
+    EXPECT(hipMalloc(&d_pool, pool_bytes) == hipSuccess && hipMalloc(&d_pc, n_pages * 4) == hipSuccess);
+    EXPECT(hipMemcpy(d_pool, pool.data(), pool_bytes, hipMemcpyHostToDevice) == hipSuccess);
+    EXPECT(cc_page_crc_dev(d_pool, n_pages, pb, (uint32_t*)d_pc, nullptr) == CC_OK);
+    std::vector<uint32_t> pc(n_pages);
+    auto persist = [&](uint32_t c) {
+        EXPECT(hipMemcpy(pc.data(), d_pc, n_pages * 4, hipMemcpyDeviceToHost) == hipSuccess);
+        EXPECT(cc_pcrc_store(paths[c].c_str(), meta, TablePath(tdir, ChunkFileName(c + 1)).c_str(),
+                             pc.data() + (size_t)c * ppc, ppc, pb) == CC_OK);
+    };
+    for (uint32_t c = 0; c < n_chunks; c++) persist(c);
+    // an ordered client write log: applied on the device (delta mode keeps the
+    // CRC table current), written to the chunk files (the datastore's pwrite),
+    // then the touched chunks' tables persisted
+    const uint32_t n = 300, max_len = 4096, src_bytes = 1 << 16;
+    std::string src(src_bytes, '\0');
+    for (auto& c : src) c = (char)(rng() & 0xFF);
+    std::vector<cc_update> log(n);
+    std::vector<bool> touched(n_chunks, false);
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t len = 1 + (uint32_t)(rng() % max_len);
+        const uint32_t c = (uint32_t)(rng() % (n_chunks - 1));  // the last chunk stays untouched
+        const uint64_t dst = (uint64_t)c * chunk + rng() % (chunk - len);  // inside one chunk file
+        log[i] = {dst, rng() % (src_bytes - len), len, 0};
+        touched[c] = true;
+    }
+    EXPECT(hipMalloc(&d_src, src_bytes) == hipSuccess && hipMalloc(&d_log, n * sizeof(cc_update)) == hipSuccess);
+    EXPECT(hipMemcpy(d_src, src.data(), src_bytes, hipMemcpyHostToDevice) == hipSuccess);
+    EXPECT(hipMemcpy(d_log, log.data(), n * sizeof(cc_update), hipMemcpyHostToDevice) == hipSuccess);
+    const uint64_t work = cc_apply_log_work_bytes(n, max_len, pb);
+    EXPECT(hipMalloc(&d_work, work) == hipSuccess);
+    EXPECT(cc_apply_log_delta_dev(d_pool, pool_bytes, pb, d_src, (const cc_update*)d_log, n, max_len, (uint32_t*)d_pc,
+                                  d_work, work, nullptr) == CC_OK);
+    EXPECT(hipDeviceSynchronize() == hipSuccess);
+    for (const cc_update& u : log) {
+        const uint32_t c = (uint32_t)(u.dst / chunk);
+        const int fd = open(paths[c].c_str(), O_WRONLY);
+        EXPECT(fd >= 0 && pwrite(fd, src.data() + u.src, u.len, meta + (u.dst % chunk)) == (ssize_t)u.len);
+        close(fd);
+    }
+    for (uint32_t c = 0; c < n_chunks; c++)
+        if (touched[c]) persist(c);
+    IntegrityOptions o;
+    o.chunkSize = chunk;
+    o.batch = 4;
+    IntegrityService svc2(o);
+    IntegrityJob j;
+    EXPECT(svc2.ScheduleJob(1, 1, dd) == INTEGRITY_OP_STATUS_SUCCESS);
+    EXPECT(svc2.Wait(1, 60000, &j) && j.state == INTEGRITY_OP_STATE_FINISHED);
+    EXPECT(j.results.size() == n_chunks);
+    for (const auto& r : j.results) EXPECT(r.tableState == CC_TABLE_OK && r.badPages == 0);
+    // a write that does not persist its table: stale (refreshed), no bad pages
+    {
+        const int fd = open(paths[2].c_str(), O_WRONLY);
+        EXPECT(fd >= 0 && pwrite(fd, "stale!", 6, meta + 12345) == 6);
+        close(fd);
+        struct timespec ts[2] = {{0, UTIME_OMIT}, {0, UTIME_NOW}};
+        utimensat(AT_FDCWD, paths[2].c_str(), ts, 0);  // a later write: mtime moves on
+    }
+    EXPECT(svc2.ScheduleJob(2, 1, dd) == INTEGRITY_OP_STATUS_SUCCESS);
+    EXPECT(svc2.Wait(2, 60000, &j) && j.state == INTEGRITY_OP_STATE_FINISHED);
+    for (const auto& r : j.results)
+        EXPECT(r.badPages == 0 && r.tableState == (r.name == ChunkFileName(3) ? CC_TABLE_REFRESHED : CC_TABLE_OK));
+    // bit rot (mtime unchanged): exactly the flipped page, of exactly that chunk
+    {
+        struct stat sb;
+        EXPECT(stat(paths[4].c_str(), &sb) == 0);
+        const int fd = open(paths[4].c_str(), O_RDWR);
+        char b = 0;
+        const off_t at = meta + 77 * pb + 9;
+        EXPECT(fd >= 0 && pread(fd, &b, 1, at) == 1);
+        b ^= 0x20;
+        EXPECT(pwrite(fd, &b, 1, at) == 1);
+        struct timespec ts[2] = {sb.st_atim, sb.st_mtim};
+        EXPECT(futimens(fd, ts) == 0);
+        close(fd);
+    }
+    EXPECT(svc2.ScheduleJob(3, 1, dd) == INTEGRITY_OP_STATUS_SUCCESS);
+    EXPECT(svc2.Wait(3, 60000, &j) && j.state == INTEGRITY_OP_STATE_FINISHED);
+    for (const auto& r : j.results) {
+        if (r.name == ChunkFileName(5)) {
+            EXPECT(r.tableState == CC_TABLE_OK && r.badPages == 1 && r.firstBad == 77 && r.badList.size() == 1 &&
+                   r.badList[0] == 77);
+        } else {
+            EXPECT(r.badPages == 0 && r.tableState == CC_TABLE_OK);
+        }
+    }
+    for (void* q : {d_pool, d_pc, d_src, d_log, d_work}) EXPECT(hipFree(q) == hipSuccess);
+}
+
 struct Case {
     const char* name;
     bool gpu;
@@ -387,6 +548,8 @@ int main(int argc, char** argv) {
         {"ScanCopysetMaps", true, ScanCopysetMaps},
         {"PoolScanShardRccl", true, PoolScanShardRccl},
         {"WriteLogBothModes", true, WriteLogBothModes},
+        {"IntegrityTableAndService", false, IntegrityTableAndService},
+        {"IntegrityWritePath", true, IntegrityWritePath},
     };
     int ran = 0, skipped = 0, failed_cases = 0;
     for (const Case& c : cases) {

@@ -1,36 +1,35 @@
-"""Per-page CRC persistence + integrity jobs.
+"""Per-page CRC persistence + integrity jobs, Python mirror.
+
+The product surface is libcurvecrc's C ABI (include/curve_crc.h, section
+"Per-page CRC persistence": cc_pcrc_* codec / atomic store / load,
+cc_integrity_check) and the C++ IntegrityService of the host layer
+(curve_amd/host/integrity_service.h).  This module binds the same ABI for the
+tests and tools; it does no checksum arithmetic of its own.
 
 The reference computes no per-page data CRC and has nowhere to keep one (the
 chunk metapage holds version/sn/correctedSn/location/bitmap + a header CRC,
-chunkserver_chunkfile.cpp:64-88), so verify-on-read needs a NEW artefact.  This
-module defines it and drives it through the engine:
-
-Sidecar `<copyset dir>/pcrc/<chunk file name>.pcrc` -- deliberately NOT in the
+chunkserver_chunkfile.cpp:64-88), so verify-on-read needs a NEW artefact: the
+sidecar `<copyset dir>/pcrc/<chunk file name>.pcrc` -- deliberately NOT in the
 data directory, because CopysetNode::GetHash (copyset_node.cpp:931-970) chains
-every file listed there and a sidecar would change the copyset hash.
-Layout (little-endian):
-    0  magic  b"CVPCRC01"
-    8  version u32 (=1) | page_bytes u32 | n_pages u32 | reserved u32
-   24  chunk_sn u64       (sn of the chunk when the table was computed)
-   32  header_crc u32     (CRC32C of bytes [0, 32))
-   36  table_crc u32      (CRC32C of the page-CRC array)
-   40  page CRCs, n_pages x u32
-A table is trusted only if both CRCs check; a bad table is reported as
-`TableCorrupt`, never used to condemn data.
+every file listed there and a sidecar would change the copyset hash.  Layout:
+curve_amd/csrc/integrity.cpp.  A table records the chunk's sn and the chunk
+file's mtime / size when it was written; a table whose chunk changed since is
+"stale" (refreshed by policy) and never condemns data, and a table that fails
+its own CRCs is "corrupt".
 
 Jobs mirror proto/integrity.proto (IntegrityService: ScheduleJob / CancelJob /
 PauseJob / ResumeJob / ListJobs; IntegrityJob{id, copyset, state, progress,
 sched_time, start_time}; INTEGRITY_JOB_STATE) -- declared and compiled in the
 reference (proto/BUILD:78) with no implementation anywhere in src/.  A job walks
-one copyset data directory: every chunk file is read into pinned memory,
-hashed page by page on the GPU, and compared with its sidecar (or the sidecar is
-created when missing).  Bad pages are recorded per file (first bad page, count).
+one copyset data directory in batches; each batch is one cc_integrity_check
+call (native pread into pinned staging, every page rehashed on the GPU, compared
+with its table).
 """
 from __future__ import annotations
 
+import ctypes
 import enum
 import os
-import struct
 import threading
 import time
 from dataclasses import dataclass, field
@@ -38,10 +37,9 @@ from typing import Dict, List, Optional
 
 import numpy as np
 
+from . import _lib
 from . import crc as C
-
-MAGIC = b"CVPCRC01"
-HEADER_BYTES = 40
+from ._lib import check, lib
 
 
 class IntegrityJobState(enum.IntEnum):  # proto/integrity.proto:23-30
@@ -62,25 +60,26 @@ class TableCorrupt(Exception):
     pass
 
 
-def encode_table(page_crcs: np.ndarray, page_bytes: int, chunk_sn: int) -> bytes:
+def encode_table(page_crcs: np.ndarray, page_bytes: int, chunk_sn: int, data_mtime_ns: int = 0,
+                 data_size: int = 0) -> bytes:
+    """cc_pcrc_encode."""
     crcs = np.ascontiguousarray(page_crcs, dtype="<u4")
-    head = MAGIC + struct.pack("<IIIIQ", 1, page_bytes, crcs.size, 0, chunk_sn)
-    body = crcs.tobytes()
-    return head + struct.pack("<II", C.CRC32(head), C.CRC32(body)) + body
+    h = _lib.CcPcrcHeader(page_bytes, crcs.size, chunk_sn, data_mtime_ns, data_size)
+    out = ctypes.create_string_buffer(int(lib().cc_pcrc_encoded_bytes(crcs.size)))
+    check(lib().cc_pcrc_encode(ctypes.byref(h), crcs.ctypes.data, out, len(out)), "cc_pcrc_encode")
+    return out.raw
 
 
 def decode_table(buf: bytes):
-    """-> (page_bytes, chunk_sn, page CRCs as uint32 array); TableCorrupt if bad."""
-    if len(buf) < HEADER_BYTES or buf[:8] != MAGIC:
-        raise TableCorrupt("bad magic / short header")
-    ver, page_bytes, n, _, sn = struct.unpack_from("<IIIIQ", buf, 8)
-    hcrc, tcrc = struct.unpack_from("<II", buf, 32)
-    if C.CRC32(buf[:32]) != hcrc or ver != 1:
-        raise TableCorrupt("header checksum / version")
-    body = buf[HEADER_BYTES:HEADER_BYTES + 4 * n]
-    if len(body) != 4 * n or C.CRC32(body) != tcrc:
-        raise TableCorrupt("table checksum")
-    return page_bytes, sn, np.frombuffer(body, dtype="<u4").copy()
+    """cc_pcrc_decode -> (header, page CRCs as uint32); TableCorrupt if bad."""
+    h = _lib.CcPcrcHeader()
+    rc = lib().cc_pcrc_decode(buf, len(buf), ctypes.byref(h), None, 0)
+    if rc == _lib.CC_ECORRUPT:
+        raise TableCorrupt("sidecar table fails its checks")
+    check(rc, "cc_pcrc_decode")
+    out = np.empty(h.n_pages, dtype=np.uint32)
+    check(lib().cc_pcrc_decode(buf, len(buf), ctypes.byref(h), out.ctypes.data, out.size), "cc_pcrc_decode")
+    return h, out
 
 
 def table_dir_for(data_dir: str) -> str:
@@ -93,13 +92,58 @@ def sidecar_path(chunk_path: str, table_dir: Optional[str] = None) -> str:
     return os.path.join(d, os.path.basename(chunk_path) + ".pcrc")
 
 
+def store_table(chunk_path: str, page_crcs, page_bytes: int = C.PAGE_SIZE, meta_bytes: int = C.META_PAGE_SIZE,
+                table_path: Optional[str] = None) -> str:
+    """cc_pcrc_store: persist the page CRCs of `chunk_path` (host array, or a
+    device tensor -- e.g. the slice of a DevicePool's CRC table that
+    cc_apply_log_delta_dev keeps current) after the write they describe."""
+    if hasattr(page_crcs, "is_cuda"):
+        page_crcs = page_crcs.detach().cpu().numpy()
+    a = np.ascontiguousarray(page_crcs).view(np.uint32)
+    path = table_path or sidecar_path(chunk_path)
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    check(lib().cc_pcrc_store(os.fsencode(chunk_path), meta_bytes, os.fsencode(path), a.ctypes.data, a.size,
+                              page_bytes), "cc_pcrc_store")
+    return path
+
+
+def load_table(table_path: str):
+    """cc_pcrc_load -> (header, page CRCs)."""
+    with open(table_path, "rb") as f:
+        return decode_table(f.read())
+
+
 @dataclass
 class FileResult:
     name: str
     pages: int
     bad_pages: int = 0
     first_bad: int = -1
-    table: str = "ok"          # ok | created | corrupt
+    table: str = "ok"          # ok | created | corrupt | stale | refreshed | missing | rebuilt
+    status: int = 0
+    bad_list: List[int] = field(default_factory=list)
+
+
+def check_files(paths: List[str], table_paths: List[str], chunk_size: int = C.CHUNK_SIZE,
+                meta_size: int = C.META_PAGE_SIZE, page_bytes: int = C.PAGE_SIZE, create_missing: bool = True,
+                refresh_stale: bool = True, io_threads: int = 8, bad_cap: int = 4096) -> List[FileResult]:
+    """cc_integrity_check over one batch of chunk files."""
+    n = len(paths)
+    if n == 0:
+        return []
+    cp = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in paths])
+    tp = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in table_paths])
+    o = _lib.CcIntegrityOpts(chunk_size, meta_size, page_bytes, io_threads, int(create_missing), int(refresh_stale))
+    res = (_lib.CcIntegrityResult * n)()
+    bad = np.zeros(max(1, bad_cap), dtype=np.uint64)
+    nb = ctypes.c_uint64(0)
+    check(lib().cc_integrity_check(cp, tp, n, ctypes.byref(o), res, bad.ctypes.data, bad_cap, ctypes.byref(nb)),
+          "cc_integrity_check")
+    out = [FileResult(os.path.basename(p), int(r.n_pages), int(r.bad_pages), int(r.first_bad),
+                      _lib.TABLE_STATES.get(int(r.table_state), "?"), int(r.status)) for p, r in zip(paths, res)]
+    for v in bad[:min(int(nb.value), bad_cap)].tolist():
+        out[v >> 32].bad_list.append(v & 0xFFFFFFFF)
+    return out
 
 
 @dataclass
@@ -115,27 +159,17 @@ class IntegrityJob:  # proto/integrity.proto:32-39
     error: str = ""
 
 
-def hash_chunk_files(paths: List[str], chunk_size: int, meta_size: int, page_bytes: int):
-    """Page CRCs of the DATA part of each chunk file (file = metapage || data;
-    CSChunkFile::Read reads at offset + metaPageSize).  The engine preads the
-    files itself (cc_scan_files, slice = one page, so the per-slice CRCs ARE the
-    page CRCs).  -> list of uint32 arrays; IOError for an unreadable file."""
-    st, _, pcs, _ = C.scan_files(paths, chunk_size, meta_size, page_bytes, page_bytes)
-    bad = np.flatnonzero(st)
-    if bad.size:
-        raise IOError(f"cannot read {paths[bad[0]]}: status {int(st[bad[0]])}")
-    return [pcs[k].copy() for k in range(len(paths))]
-
-
 class IntegrityService:
     """In-process IntegrityService (ScheduleJob/CancelJob/PauseJob/ResumeJob/
-    ListJobs).  One worker thread runs jobs FIFO; Pause/Cancel take effect at
-    chunk-file batch boundaries."""
+    ListJobs), the Python twin of curve_amd/host/integrity_service.h.  One
+    worker thread runs jobs FIFO; Pause/Cancel take effect at chunk-file batch
+    boundaries.  Work happens on the calling process's current HIP device."""
 
     def __init__(self, chunk_size: int = C.CHUNK_SIZE, meta_size: int = C.META_PAGE_SIZE,
-                 page_bytes: int = C.PAGE_SIZE, batch: int = 16, create_missing: bool = True):
+                 page_bytes: int = C.PAGE_SIZE, batch: int = 16, create_missing: bool = True,
+                 refresh_stale: bool = True):
         self.chunk_size, self.meta_size, self.page_bytes = chunk_size, meta_size, page_bytes
-        self.batch, self.create_missing = batch, create_missing
+        self.batch, self.create_missing, self.refresh_stale = batch, create_missing, refresh_stale
         self._jobs: Dict[int, IntegrityJob] = {}
         self._order: List[int] = []
         self._cv = threading.Condition()
@@ -202,9 +236,6 @@ class IntegrityService:
         return None
 
     def _run(self):
-        import torch
-        if torch.cuda.is_available():
-            torch.cuda.set_device(0)
         while True:
             with self._cv:
                 while not self._stop and self._next() is None:
@@ -225,7 +256,8 @@ class IntegrityService:
     def _do(self, job: IntegrityJob):
         fsize = self.chunk_size + self.meta_size
         names = sorted(n for n in os.listdir(job.data_dir) if os.path.getsize(os.path.join(job.data_dir, n)) == fsize)
-        os.makedirs(table_dir_for(job.data_dir), exist_ok=True)
+        tdir = table_dir_for(job.data_dir)
+        os.makedirs(tdir, exist_ok=True)
         done = {r.name for r in job.results}
         todo = [n for n in names if n not in done]
         for b0 in range(0, len(todo), self.batch):
@@ -235,38 +267,15 @@ class IntegrityService:
                     return
             part = todo[b0:b0 + self.batch]
             paths = [os.path.join(job.data_dir, n) for n in part]
-            crcs = hash_chunk_files(paths, self.chunk_size, self.meta_size, self.page_bytes)
-            for n, p, pc in zip(part, paths, crcs):
-                job.results.append(self._check(n, p, pc))
+            res = check_files(paths, [sidecar_path(p, tdir) for p in paths], self.chunk_size, self.meta_size,
+                              self.page_bytes, self.create_missing, self.refresh_stale)
+            bad = [r for r in res if r.status]
+            if bad:
+                raise IOError(f"cannot check {bad[0].name}: status {bad[0].status}")
+            job.results.extend(res)
             with self._cv:
                 job.progress = int(100 * len(job.results) / max(1, len(names)))
         with self._cv:
             if job.state == IntegrityJobState.RUNNING:
                 job.state, job.progress = IntegrityJobState.FINISHED, 100
             self._cv.notify_all()
-
-    def _check(self, name: str, path: str, pc: np.ndarray) -> FileResult:
-        from .chunkfile import ChunkFileMetaPage
-        side = sidecar_path(path)
-        res = FileResult(name, pc.size)
-        with open(path, "rb") as f:
-            rc, meta = ChunkFileMetaPage.decode(f.read(self.meta_size))
-        sn = meta.sn if meta else 0
-        if not os.path.exists(side):
-            if self.create_missing:
-                with open(side, "wb") as f:
-                    f.write(encode_table(pc, self.page_bytes, sn))
-                res.table = "created"
-            return res
-        try:
-            with open(side, "rb") as f:
-                page_bytes, _, want = decode_table(f.read())
-            if page_bytes != self.page_bytes or want.size != pc.size:
-                raise TableCorrupt("geometry")
-        except TableCorrupt:
-            res.table = "corrupt"
-            return res
-        bad = np.flatnonzero(want != pc)
-        res.bad_pages = int(bad.size)
-        res.first_bad = int(bad[0]) if bad.size else -1
-        return res

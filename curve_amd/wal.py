@@ -111,15 +111,31 @@ def parse_segment(seg, meta_page_size: int = 4096) -> List[EntryHeader]:
     return out
 
 
-def verify_segment_dev(dev_seg, headers: Sequence[EntryHeader], stream=None):
-    """Data checksums of every parsed entry on the device in one call.
-    Returns (device CRCs, list of indices whose data checksum mismatches)."""
+@dataclass
+class SegmentCheck:
+    """Outcome of verify_segment_dev; every index is a position in `headers`."""
+    crcs: object                 # int32 device tensor: the data CRC of every CRC32-checked entry, in order
+    checked: List[int]           # entries whose data checksum was verified on the device
+    bad: List[int]               # ... and did not match (CurveSegment::_load_entry would fail them)
+    unverified: List[int]        # entries not verified here: a non-CRC32 checksum type
+                                 # (CHECKSUM_MURMURHASH32, braft's other type) or an untrusted header
+    corrupt_header: List[int]    # header CRC mismatch: data_real_len is not trusted, data not hashed
+
+
+def verify_segment_dev(dev_seg, headers: Sequence[EntryHeader], stream=None) -> SegmentCheck:
+    """Data checksums of every parsed entry with a trusted header and a CRC32
+    checksum, on the device in ONE call (cc_crc_ranges_dev).  Entries whose
+    header failed its own CRC are never hashed (their length is not trusted);
+    entries of another checksum type are reported as unverified, not skipped
+    silently.  Indices refer to `headers`."""
     import numpy as np
-    crcs = [h for h in headers if h.checksum_type == CHECKSUM_CRC32]
-    offs = [h.offset + ENTRY_HEADER_SIZE for h in crcs]
-    lens = [h.data_real_len for h in crcs]
+    corrupt = [k for k, h in enumerate(headers) if not h.header_ok]
+    checked = [k for k, h in enumerate(headers) if h.header_ok and h.checksum_type == CHECKSUM_CRC32]
+    unverified = [k for k, h in enumerate(headers) if h.header_ok and h.checksum_type != CHECKSUM_CRC32]
+    offs = [headers[k].offset + ENTRY_HEADER_SIZE for k in checked]
+    lens = [headers[k].data_real_len for k in checked]
     got = C.crc_ranges(dev_seg, offs, lens, stream=stream)
     vals = np.asarray(C.as_u32(got), dtype=np.uint64)
-    want = np.asarray([h.data_checksum for h in crcs], dtype=np.uint64)
-    bad = [i for i in np.flatnonzero(vals != want).tolist()]
-    return got, bad
+    want = np.asarray([headers[k].data_checksum for k in checked], dtype=np.uint64)
+    bad = [checked[i] for i in np.flatnonzero(vals != want).tolist()]
+    return SegmentCheck(got, checked, bad, unverified, corrupt)

@@ -422,6 +422,86 @@ typedef struct cc_pool_shard {
 int cc_pool_scan_dev(const cc_pool_shard* shard, cc_comm* comm, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Per-page CRC persistence -- the table verify-on-read and
+ * the integrity jobs of proto/integrity.proto (IntegrityService, :55-61;
+ * declared and compiled in the reference, never implemented) check against.
+ * The reference keeps no data CRC anywhere: the metapage holds a CRC of its own
+ * header only (chunkserver_chunkfile.cpp:64-130), so the table is a NEW sidecar
+ * file per chunk, kept OUTSIDE the copyset data directory (CopysetNode::GetHash
+ * chains every file listed there, copyset_node.cpp:931-970).  It records the
+ * chunk's sn (metapage) and the chunk file's mtime and size when it was
+ * written: a table whose chunk changed since is STALE and never condemns data.
+ * (mtime comes from the kernel's coarse clock: a write path that changes a
+ * chunk must store its table -- cc_pcrc_store after the write, e.g. from the
+ * CRCs cc_apply_log_delta_dev keeps current -- staleness is the safety net.)
+ * ------------------------------------------------------------------------ */
+#define CC_PCRC_HEADER_BYTES 64
+
+typedef struct cc_pcrc_header {
+    uint32_t page_bytes;
+    uint32_t n_pages;
+    uint64_t chunk_sn;      /* metapage sn when the table was written */
+    int64_t data_mtime_ns;  /* the chunk file's st_mtim then */
+    uint64_t data_size;     /* the chunk file's size then */
+} cc_pcrc_header;
+
+/* In-memory codec.  decode: CC_ECORRUPT for a bad magic / version / header CRC
+ * / table CRC / length; page_crcs may be NULL (header only). */
+uint64_t cc_pcrc_encoded_bytes(uint32_t n_pages);
+int cc_pcrc_encode(const cc_pcrc_header* h, const uint32_t* page_crcs, void* out, uint64_t out_bytes);
+int cc_pcrc_decode(const void* buf, uint64_t bytes, cc_pcrc_header* h, uint32_t* page_crcs, uint32_t max_pages);
+
+/* sn of a chunk metapage, after ChunkFileMetaPage::decode's checks
+ * (chunkserver_chunkfile.cpp:90-130: header CRC, version 1 or 2), bounds-checked;
+ * CC_ECORRUPT otherwise. */
+int cc_chunk_meta_sn(const void* metapage, uint32_t bytes, uint64_t* sn);
+
+/* Write the table of chunk file `chunk_path` (metapage of meta_bytes, then
+ * n_pages data pages) to `table_path`, atomically (temp file + fsync + rename),
+ * recording the chunk's current sn, mtime and size.  Call it after the data
+ * write it describes (the write path's CSChunkFile::Write, chunkserver_chunkfile.cpp:287-427). */
+int cc_pcrc_store(const char* chunk_path, uint32_t meta_bytes, const char* table_path, const uint32_t* page_crcs,
+                  uint32_t n_pages, uint32_t page_bytes);
+/* Read + decode a table file (-errno if it cannot be read, -ENOENT if absent). */
+int cc_pcrc_load(const char* table_path, cc_pcrc_header* h, uint32_t* page_crcs, uint32_t max_pages);
+
+/* Table state of one chunk after a check. */
+#define CC_TABLE_OK 0        /* table describes the chunk; bad_pages counted against it */
+#define CC_TABLE_CREATED 1   /* no table: one was written from the current bytes */
+#define CC_TABLE_CORRUPT 2   /* table unreadable (CRC / geometry): reported, not used */
+#define CC_TABLE_STALE 3     /* chunk changed since the table was written: not used */
+#define CC_TABLE_REFRESHED 4 /* stale, and rewritten from the current bytes */
+#define CC_TABLE_MISSING 5   /* no table, none written */
+#define CC_TABLE_REBUILT 6   /* corrupt, and rewritten from the current bytes */
+
+typedef struct cc_integrity_opts {
+    uint32_t chunk_bytes;    /* 16 MiB */
+    uint32_t meta_bytes;     /* 4 KiB */
+    uint32_t page_bytes;     /* 4 KiB */
+    uint32_t io_threads;     /* readers of cc_scan_files (0 = 8) */
+    uint32_t create_missing; /* write a table for a chunk that has none */
+    uint32_t refresh_stale;  /* rewrite stale / corrupt tables from the current bytes */
+} cc_integrity_opts;
+
+typedef struct cc_integrity_result {
+    int32_t status;       /* 0; -errno; CC_EINVAL (not chunk geometry); CC_ECORRUPT (metapage header) */
+    uint32_t table_state; /* CC_TABLE_* */
+    uint32_t n_pages;
+    uint32_t bad_pages;   /* pages whose bytes no longer match the (valid, current) table */
+    int64_t first_bad;    /* -1: none */
+} cc_integrity_result;
+
+/* The integrity check of a batch of chunk files (the work of one
+ * IntegrityService job step): every data page rehashed on the device (native
+ * pread into pinned staging, cc_scan_files) and compared with the chunk's
+ * table; a file that changes while it is read counts as stale.  Bad pages are
+ * listed as (file index << 32 | page) in bad_list (the first bad_cap of them;
+ * *n_bad = all).  Blocking, thread-safe. */
+int cc_integrity_check(const char* const* chunk_paths, const char* const* table_paths, uint64_t n,
+                       const cc_integrity_opts* opts, cc_integrity_result* res, uint64_t* bad_list, uint64_t bad_cap,
+                       uint64_t* n_bad);
+
+/* ------------------------------------------------------------------------
  * Diagnostics (new; no reference counterpart)
  * ------------------------------------------------------------------------ */
 /* Copy the 163840-byte LDS image the page kernel loads into every CU (G tables

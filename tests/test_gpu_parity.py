@@ -665,13 +665,37 @@ def test_wal_segment_replay_verify(dev, oracle):
     hs = wal.parse_segment(bytes(seg))
     assert len(hs) == 300
     d = to_dev(np.frombuffer(bytes(seg), dtype=np.uint8), dev)
-    got, bad = wal.verify_segment_dev(d, hs)
-    assert bad == []
-    assert [int(x) for x in u32(got)] == [oracle.crc32c(e[2]) for e in ents]
+    r = wal.verify_segment_dev(d, hs)
+    assert r.bad == [] and r.unverified == [] and r.corrupt_header == [] and r.checked == list(range(300))
+    assert [int(x) for x in u32(r.crcs)] == [oracle.crc32c(e[2]) for e in ents]
     seg[hs[123].offset + wal.ENTRY_HEADER_SIZE + 5] ^= 0x10
     d = to_dev(np.frombuffer(bytes(seg), dtype=np.uint8), dev)
-    _, bad = wal.verify_segment_dev(d, hs)
-    assert bad == [123]
+    assert wal.verify_segment_dev(d, hs).bad == [123]
+
+
+def test_wal_mixed_checksum_types_and_corrupt_header(dev, oracle):
+    """a MURMURHASH32 entry must not shift the indices of later bad
+    entries, is reported unverified (never silently skipped), and a corrupt
+    last header is reported without hashing its untrusted length."""
+    import struct
+    from curve_amd import wal
+    rng = np.random.default_rng(6)
+    ents = [(2, wal.ENTRY_TYPE_DATA, rng.integers(0, 256, int(rng.integers(1, 9000)), dtype=np.uint8).tobytes())
+            for _ in range(20)]
+    seg = bytearray(wal.build_segment(ents))
+    hs = wal.parse_segment(bytes(seg))
+    # entry 4 declares the murmur checksum type (header re-sealed with a valid header CRC)
+    o = hs[4].offset
+    term, mf, dl, real, dck = struct.unpack_from(">qIIII", seg, o)
+    struct.pack_into(">qIIII", seg, o, term, (mf & ~0xFF0000) | (wal.CHECKSUM_MURMURHASH32 << 16), dl, real, 0x1234)
+    struct.pack_into(">I", seg, o + 24, oracle.crc32c(bytes(seg[o:o + 24])))
+    seg[hs[9].offset + wal.ENTRY_HEADER_SIZE] ^= 1       # bad data in entry 9
+    seg[hs[15].offset + 3] ^= 1                           # corrupt header of entry 15: the walk stops there
+    hs = wal.parse_segment(bytes(seg))
+    assert len(hs) == 16 and not hs[15].header_ok and hs[4].checksum_type == wal.CHECKSUM_MURMURHASH32
+    r = wal.verify_segment_dev(to_dev(np.frombuffer(bytes(seg), dtype=np.uint8), dev), hs)
+    assert r.bad == [9] and r.unverified == [4] and r.corrupt_header == [15]
+    assert r.checked == [k for k in range(15) if k != 4]
 
 
 def test_copyset_dir_real_chunk_files(dev, oracle, tmp_path):
@@ -805,9 +829,8 @@ def test_integrity_job_sidecars(dev, oracle, tmp_path):
         assert all(r.table == "created" for r in j.results) and len(j.results) == 7
         assert sorted(os.listdir(tmp_path)) == sorted(CF.chunk_file_name(c) for c in datas)  # data dir untouched
         for cid, data in datas.items():
-            with open(I.sidecar_path(str(tmp_path / CF.chunk_file_name(cid))), "rb") as f:
-                _, sn, tab = I.decode_table(f.read())
-            assert sn == cid and (tab == oracle.page_crcs(data, 4096)).all()
+            h, tab = I.load_table(I.sidecar_path(str(tmp_path / CF.chunk_file_name(cid))))
+            assert h.chunk_sn == cid and (tab == oracle.page_crcs(data, 4096)).all()
         p3 = str(tmp_path / CF.chunk_file_name(3))
         with open(p3, "r+b") as f:  # data page 77 of chunk 3
             f.seek(4096 + 77 * 4096 + 5)
@@ -818,11 +841,14 @@ def test_integrity_job_sidecars(dev, oracle, tmp_path):
         raw = bytearray(open(s5, "rb").read())
         raw[100] ^= 1
         open(s5, "wb").write(bytes(raw))
+        # bit rot does not move mtime: restore it, as a flipped bit on the medium would
+        st3 = os.stat(p3)
+        os.utime(p3, ns=(st3.st_atime_ns, int(I.load_table(I.sidecar_path(p3))[0].data_mtime_ns)))
         svc.ScheduleJob(2, 1, str(tmp_path))
         j = svc.wait(2, 120)
         res = {r.name: r for r in j.results}
-        assert res["chunk_3"].bad_pages == 1 and res["chunk_3"].first_bad == 77
-        assert res["chunk_5"].table == "corrupt"
+        assert res["chunk_3"].bad_pages == 1 and res["chunk_3"].first_bad == 77 and res["chunk_3"].bad_list == [77]
+        assert res["chunk_5"].table in ("corrupt", "rebuilt")
         assert all(r.bad_pages == 0 for n, r in res.items() if n != "chunk_3")
     finally:
         svc.close()

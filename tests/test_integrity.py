@@ -6,17 +6,59 @@ from curve_amd import integrity as I
 
 
 def test_table_roundtrip_and_corruption():
+    """cc_pcrc_encode / cc_pcrc_decode: round trip; any flipped header or
+    table byte, a truncated table, or a wrong magic is corrupt."""
     pc = np.random.default_rng(0).integers(0, 2**32, 4096, dtype=np.uint64).astype(np.uint32)
-    buf = I.encode_table(pc, 4096, chunk_sn=9)
-    pb, sn, got = I.decode_table(buf)
-    assert pb == 4096 and sn == 9 and (got == pc).all()
-    for pos in (3, 20, 33, I.HEADER_BYTES + 7, len(buf) - 1):
+    buf = I.encode_table(pc, 4096, chunk_sn=9, data_mtime_ns=123456789, data_size=4096 + (16 << 20))
+    h, got = I.decode_table(buf)
+    assert (h.page_bytes, h.n_pages, h.chunk_sn, h.data_mtime_ns, h.data_size) == (4096, 4096, 9, 123456789,
+                                                                                    4096 + (16 << 20))
+    assert (got == pc).all()
+    for pos in (3, 9, 20, 33, 45, 57, 62, 64 + 7, len(buf) - 1):
         b = bytearray(buf)
         b[pos] ^= 0x01
         with pytest.raises(I.TableCorrupt):
             I.decode_table(bytes(b))
     with pytest.raises(I.TableCorrupt):
         I.decode_table(buf[:-4])
+    with pytest.raises(I.TableCorrupt):
+        I.decode_table(b"")
+
+
+def test_metapage_sn_and_store_load(tmp_path):
+    """cc_chunk_meta_sn follows ChunkFileMetaPage::decode (header CRC, version);
+    cc_pcrc_store records the chunk's sn / mtime / size and cc_pcrc_load reads
+    them back (no GPU needed: the store only stats the chunk file)."""
+    import ctypes
+    import os
+    from curve_amd import _lib
+    from curve_amd.chunkfile import ChunkFileMetaPage, write_chunk_file
+    L = _lib.lib()
+    meta = ChunkFileMetaPage(sn=77).encode()
+    sn = ctypes.c_uint64(0)
+    assert L.cc_chunk_meta_sn(meta, 4096, ctypes.byref(sn)) == 0 and sn.value == 77
+    clone = ChunkFileMetaPage(sn=5, location=b"s3://bucket/obj@1", bitmap_bits=4096, bitmap=b"\xff" * 64).encode()
+    assert L.cc_chunk_meta_sn(clone, 4096, ctypes.byref(sn)) == 0 and sn.value == 5
+    bad = bytearray(meta)
+    bad[3] ^= 1
+    assert L.cc_chunk_meta_sn(bytes(bad), 4096, ctypes.byref(sn)) == _lib.CC_ECORRUPT
+    huge = bytearray(meta)
+    huge[17:25] = (1 << 40).to_bytes(8, "little")  # location length past the page
+    assert L.cc_chunk_meta_sn(bytes(huge), 4096, ctypes.byref(sn)) == _lib.CC_ECORRUPT
+    chunk = 1 << 16
+    d = tmp_path / "data"
+    d.mkdir()
+    path = str(d / "chunk_3")
+    write_chunk_file(path, meta, bytes(chunk))
+    pc = np.arange(chunk // 4096, dtype=np.uint32) * 7
+    tp = I.store_table(path, pc, 4096)
+    assert tp == I.sidecar_path(path) and os.path.dirname(tp) == str(tmp_path / "pcrc")
+    h, got = I.load_table(tp)
+    st = os.stat(path)
+    assert (h.chunk_sn, h.data_size, h.data_mtime_ns) == (77, st.st_size, st.st_mtime_ns)
+    assert (got == pc).all()
+    with pytest.raises(I.C.CurveCrcError):  # wrong page count for the file's size
+        I.store_table(path, pc[:-1], 4096)
 
 
 def test_service_state_machine(tmp_path):
