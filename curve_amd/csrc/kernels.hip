@@ -327,6 +327,9 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
     }
 }
 
+#ifndef CC_INSERT_ABLATE
+#define CC_INSERT_ABLATE 0  // timing ablation of log_insert_kernel (wrong results): 1 no atomics
+#endif
 #ifndef CC_LOG_ABLATE
 #define CC_LOG_ABLATE 0  // timing ablations of log_pages_kernel (wrong results): 1 no stores, 2 no source loads, 3 no page loads, 4 no CRC chain, 5 no loads/stores of data
 #endif
@@ -777,9 +780,12 @@ __device__ __forceinline__ uint32_t page_hash(uint32_t page, uint32_t mask) {
     return (page * 2654435761u) & mask;  // Fibonacci hashing; sequential pages spread
 }
 
-__global__ __launch_bounds__(256) void log_insert_kernel(LogLaunch a) {
+constexpr uint32_t kInsertThreads = 1024;  // one head-list atomic per 1024 pieces (a per-wave atomic on the one
+                                          // counter serialised 2048 waves: 26 of the kernel's 31 us)
+__global__ __launch_bounds__(kInsertThreads) void log_insert_kernel(LogLaunch a) {
+    __shared__ uint32_t wcount[kInsertThreads / 64], bbase;
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     bool fresh = false;
     uint32_t slot = 0;
     if (t < a.n_pieces) {
@@ -797,6 +803,13 @@ __global__ __launch_bounds__(256) void log_insert_kernel(LogLaunch a) {
             // CAS first (one atomic for a page seen first, the common case);
             // next[] is only read by later kernels, so it can follow the CAS
             unsigned long long cur = 0ull;
+#if CC_INSERT_ABLATE  // timing only (wrong grouping): a plain store instead of the CAS
+            tab[slot] = tag | (unsigned long long)(t + 1);
+            a.next[t] = kNoPiece;
+            fresh = true;
+            if (true) {
+            } else
+#endif
             for (;;) {
                 const unsigned long long old = atomicCAS(tab + slot, cur, tag | (unsigned long long)(t + 1));
                 if (old == cur) {  // claimed (cur == 0) or pushed onto the page's list
@@ -814,12 +827,17 @@ __global__ __launch_bounds__(256) void log_insert_kernel(LogLaunch a) {
         }
     }
     const uint64_t m = __ballot(fresh);
-    if (m) {
-        uint32_t base = 0;
-        if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(a.head_count, (uint32_t)__popcll(m));
-        base = __shfl(base, (int)__builtin_ctzll(m), 64);
-        if (fresh) a.heads[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = slot;
+    if (lane == 0) wcount[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; w++) tot += wcount[w];
+        bbase = tot ? atomicAdd(a.head_count, tot) : 0u;
     }
+    __syncthreads();
+    uint32_t base = bbase;
+    for (uint32_t w = 0; w < wv; w++) base += wcount[w];
+    if (fresh) a.heads[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = slot;
 }
 
 // The bytes of one update that fall inside one page, page-relative: page bytes
@@ -1463,7 +1481,8 @@ hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s) {
 
 hipError_t launch_log_insert(const LogLaunch& a, hipStream_t s) {
     if (a.n_pieces == 0) return hipSuccess;
-    hipLaunchKernelGGL(log_insert_kernel, dim3((uint32_t)((a.n_pieces + 255) / 256)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(log_insert_kernel, dim3((uint32_t)((a.n_pieces + kInsertThreads - 1) / kInsertThreads)),
+                       dim3(kInsertThreads), 0, s, a);
     return hipGetLastError();
 }
 

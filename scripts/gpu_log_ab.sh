@@ -1,9 +1,15 @@
-# write-log kernel: unaligned vs 4-byte-aligned logs, kernel trace of each
+# write-log A/B: parity tests on the shipped build, then timings of the
+# shipped build and of build/variants/libcurvecrc_<v>.so for each v given
 set -u
 R=$(pwd)
-cd /tmp && export TMPDIR=/tmp
-for al in 1 4; do
-  rm -rf $R/gpurun_out/prof_log_a$al
-  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_log_a$al -o run --output-format csv -- python3 $R/scripts/prof_log.py --align $al > $R/gpurun_out/prof_log_a$al.log 2>&1 || exit 1
-  grep "ms per" $R/gpurun_out/prof_log_a$al.log
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "partial or write_log or beyond or integrity" 2>&1 | tail -2 || exit 1
+for rep in 1 2; do
+  timeout -k 10 120 python -u scripts/prof_log.py --reps 8 || exit 1
+  timeout -k 10 120 python -u scripts/prof_log.py --reps 8 --delta || exit 1
+  for v in "$@"; do
+    echo "variant $v"
+    timeout -k 10 120 python -u scripts/prof_log.py --reps 8 --lib build/variants/libcurvecrc_$v.so || exit 1
+    timeout -k 10 120 python -u scripts/prof_log.py --reps 8 --delta --lib build/variants/libcurvecrc_$v.so || exit 1
+  done
 done
+echo done
