@@ -464,6 +464,9 @@ __device__ __forceinline__ void mask_range_block(uint32_t (&w)[16], const RangeG
 #define CC_RANGE_WAVES 12  // waves per CU of the range kernel (A/B: 12 ~3 % over 8, 16 equal)
 #endif
 constexpr int kRangeWaves = CC_RANGE_WAVES;
+#ifndef CC_RANGE_DEPTH
+#define CC_RANGE_DEPTH 3  // 4 KiB blocks in flight behind the one being folded (A/B: 3 ~3 % over 2 on WAL sizes)
+#endif
 __global__ __launch_bounds__(64 * kRangeWaves) void range_crc_kernel(const unsigned char* __restrict__ buf,
                                                                   const RangeDesc* __restrict__ ranges, uint64_t n,
                                                                   const uint4* __restrict__ image,
@@ -508,7 +511,11 @@ __global__ __launch_bounds__(64 * kRangeWaves) void range_crc_kernel(const unsig
             }
             return q;
         };
+#if CC_RANGE_DEPTH == 3
+        uint32_t A[16], B[16], Cq[16], Dq[16];
+#else
         uint32_t A[16], B[16], Cq[16];
+#endif
         Pos pA;
         pA.h = (uint32_t)__builtin_ctzll(bits);
         bits &= bits - 1;
@@ -518,7 +525,13 @@ __global__ __launch_bounds__(64 * kRangeWaves) void range_crc_kernel(const unsig
         load_range_block(A, buf, pA.g, pA.k, lane);
         Pos pB = adv(pA);
         load_range_block(B, buf, pB.g, pB.k, lane);
+#if CC_RANGE_DEPTH == 3
+        Pos pC = adv(pB);
+        load_range_block(Cq, buf, pC.g, pC.k, lane);
+        Pos pD = pC;
+#else
         Pos pC = pB;
+#endif
         uint32_t s = 0;
         // consume X (two blocks of loads in flight behind it) after issuing the
         // loads of position py into Y
@@ -544,6 +557,22 @@ __global__ __launch_bounds__(64 * kRangeWaves) void range_crc_kernel(const unsig
                 if (lane == 0) out[base + (uint64_t)px.h * W] = v;
             }
         };
+#if CC_RANGE_DEPTH == 3
+        for (;;) {
+            if (!pA.real) break;
+            pD = adv(pC);
+            step(A, pA, Dq, pD);
+            if (!pB.real) break;
+            pA = adv(pD);
+            step(B, pB, A, pA);
+            if (!pC.real) break;
+            pB = adv(pA);
+            step(Cq, pC, B, pB);
+            if (!pD.real) break;
+            pC = adv(pB);
+            step(Dq, pD, Cq, pC);
+        }
+#else
         for (;;) {
             if (!pA.real) break;
             pC = adv(pB);
@@ -555,6 +584,7 @@ __global__ __launch_bounds__(64 * kRangeWaves) void range_crc_kernel(const unsig
             pB = adv(pA);
             step(Cq, pC, B, pB);
         }
+#endif
     }
 }
 

@@ -17,6 +17,8 @@ p.add_argument("--gib", type=int, default=16)
 p.add_argument("--entries", type=int, default=65536)
 p.add_argument("--reps", type=int, default=8)
 p.add_argument("--lib", default=None, help="libcurvecrc variant to load instead of the in-tree one")
+p.add_argument("--fixed", type=int, default=0, help="every entry this many bytes (balance probe)")
+p.add_argument("--sorted", action="store_true", help="entries in decreasing size order (balance probe)")
 a = p.parse_args()
 if a.lib:
     from curve_amd import _lib
@@ -26,6 +28,10 @@ pool = torch.empty(a.gib << 30, dtype=torch.uint8, device=dev).random_(0, 256)
 rng = np.random.default_rng(0x3A1)
 n = a.entries
 real = rng.integers(1024, (128 << 10) + 1, n).astype(np.uint64)
+if a.fixed:
+    real[:] = a.fixed
+if a.sorted:
+    real = np.sort(real)[::-1].copy()
 slot = (28 + real + 4095) // 4096 * 4096
 start = np.concatenate([[0], np.cumsum(slot)[:-1]]).astype(np.uint64) + 4096
 offs = start + 28
