@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum" "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum" "GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_LDS SQ_INSTS_VALU"; do
     name=$(echo "$pass" | cut -d' ' -f1)
-    timeout -k 10 300 rocprofv3 --pmc $pass -d "$OUT/$name" -o run --output-format csv -- \
+    timeout -s KILL 90 rocprofv3 --pmc $pass -d "$OUT/$name" -o run --output-format csv -- \
         python3 "$R/scripts/prof_page.py" --n 2 > "$OUT/$name.log" 2>&1 || { echo "pass $name failed rc=$?"; exit 1; }
 done
 echo "pmc done: $OUT"
