@@ -370,7 +370,7 @@ def partial_write_leg(pool, args):
                       "updates_per_s": round(U / (delta_ms * 1e-3), 1),
                       "all_pages_verify_after": delta_ok,
                       "path": "cc_apply_log_delta_dev: stored CRCs updated by linearity, touched rows read only"},
-            "path": "cc_apply_log_dev: device sort of (page, log index) pieces + one wave per touched page",
+            "path": "cc_apply_log_dev: pieces grouped by page in a device hash table (one CAS per piece, no sort) + one wave per touched page",
             "note": "alg bytes = 2*update bytes + 4100*touched pages; log + data resident in HBM"}
 
 
