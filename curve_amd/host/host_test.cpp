@@ -21,6 +21,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "../../include/curve_crc.h"
+#include "../../include/curve_crc32_compat.h"
 #include "chunkserver_host.h"
 #include "integrity_service.h"
 
@@ -81,6 +82,11 @@ void Crc32Vectors() {
     EXPECT(crc32c_value(dec.data(), 32) == 0x113fdb5cU);
     EXPECT(crc32c_value("hello world", 11) == crc32c_extend(crc32c_value("hello ", 6), "world", 5));
     EXPECT(crc32c_value("a", 1) != crc32c_value("foo", 3));
+    // the drop-in wrapper headers (src/common/crc32.h:40-55, nebd/src/common/crc32.h:31-38)
+    EXPECT(curve::common::CRC32("hello world", 11) == 3381945770u);
+    EXPECT(curve::common::CRC32(curve::common::CRC32("hello ", 6), "world", 5) == 3381945770u);
+    EXPECT(nebd::common::CRC32(z.data(), 32) == 0x8a9136aaU);
+    EXPECT(nebd::common::CRC32(nebd::common::CRC32("hello ", 6), "world", 5) == 3381945770u);
 }
 
 // ---- ChunkFileMetaPage (chunkserver_chunkfile.cpp:64-130) -------------------
