@@ -333,6 +333,18 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
 #ifndef CC_LOG_ABLATE
 #define CC_LOG_ABLATE 0  // timing ablations of log_pages_kernel (wrong results): 1 no stores, 2 no source loads, 3 no page loads, 4 no CRC chain, 5 no loads/stores of data
 #endif
+#ifndef CC_LOG_SKIP_COVERED
+#define CC_LOG_SKIP_COVERED 1  // full mode: do not read page rows the page's only piece overwrites whole
+#endif
+#ifndef CC_LOG_SRC_AUX
+#define CC_LOG_SRC_AUX 0  // cache policy bits of the write-log source loads
+#endif
+#ifndef CC_LOG_CRC_NT
+#define CC_LOG_CRC_NT 0  // nontemporal page-CRC stores in the write-log kernels
+#endif
+#ifndef CC_LOG_STORE_AUX
+#define CC_LOG_STORE_AUX 2  // cache policy bits of the write-log row stores (2 = nontemporal: -20 us a batch)
+#endif
 constexpr uint32_t kBufOOB = 0x80000000u;   // offset past num_records: load 0 / store dropped
 constexpr uint32_t kBufFlags = 0x00020000u;  // buffer resource dword 3 for gfx9-family (CDNA)
 
@@ -810,7 +822,10 @@ __device__ __forceinline__ uint32_t page_hash(uint32_t page, uint32_t mask) {
     return (page * 2654435761u) & mask;  // Fibonacci hashing; sequential pages spread
 }
 
-constexpr uint32_t kInsertThreads = 1024;  // one head-list atomic per 1024 pieces (a per-wave atomic on the one
+#ifndef CC_INSERT_THREADS
+#define CC_INSERT_THREADS 1024
+#endif
+constexpr uint32_t kInsertThreads = CC_INSERT_THREADS;  // one head-list atomic per 1024 pieces (a per-wave atomic on the one
                                           // counter serialised 2048 waves: 26 of the kernel's 31 us)
 __global__ __launch_bounds__(kInsertThreads) void log_insert_kernel(LogLaunch a) {
     __shared__ uint32_t wcount[kInsertThreads / 64], bbase;
@@ -951,7 +966,7 @@ __device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint
     for (int j = 0; j < M; j++) {
         const bool full = pl.o + 256u * j < pl.l3;
         r.S[j] = __builtin_amdgcn_raw_buffer_load_b32(
-            rw, (full && CC_LOG_ABLATE != 2 && CC_LOG_ABLATE != 5 ? l4 : kBufOOB) + 256u * j, 0, 0);
+            rw, (full && CC_LOG_ABLATE != 2 && CC_LOG_ABLATE != 5 ? l4 : kBufOOB) + 256u * j, 0, CC_LOG_SRC_AUX);
     }
     uint32_t e[2];
     piece_edges(p, e);
@@ -961,8 +976,9 @@ __device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint
         const bool mine = e[k] != 0xffffffffu && lane == (e[k] & 63u);
         const uint32_t k0 = p.rlo > b ? p.rlo - b : 0u;
         const uint32_t k1 = p.rhi < b + 4 ? p.rhi - b : 4u;
-        r.ea[k] = __builtin_amdgcn_raw_buffer_load_b32(re, (mine && k0 < 4u - sh) ? b : kBufOOB, 0, 0);
-        r.eb[k] = __builtin_amdgcn_raw_buffer_load_b32(re, (mine && sh && k1 > 4u - sh) ? b + 4 : kBufOOB, 0, 0);
+        r.ea[k] = __builtin_amdgcn_raw_buffer_load_b32(re, (mine && k0 < 4u - sh) ? b : kBufOOB, 0, CC_LOG_SRC_AUX);
+        r.eb[k] =
+            __builtin_amdgcn_raw_buffer_load_b32(re, (mine && sh && k1 > 4u - sh) ? b + 4 : kBufOOB, 0, CC_LOG_SRC_AUX);
     }
 }
 
@@ -1087,6 +1103,13 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
                 ocy = a.page_crcs[pgy + vz];
             } else if constexpr (CC_LOG_ABLATE == 3 || CC_LOG_ABLATE == 5) {
                 load_rows<M>(Y, a.pool + (uint64_t)pgy * pb, 0u, lane);  // timing ablation: no page reads
+            } else if constexpr (CC_LOG_SKIP_COVERED) {
+                // rows the page's only piece covers whole come from the source:
+                // not read (out-of-range offset, no memory traffic)
+                const uint32_t f0 = (py.rlo + 255u) >> 8, f1 = py.rhi >> 8;  // whole rows [f0, f1)
+                const uint32_t full =
+                    f1 > f0 ? ((f1 >= 32u ? 0xFFFFFFFFu : (1u << f1) - 1u) & ~((1u << f0) - 1u)) : 0u;
+                load_rows<M>(Y, a.pool + (uint64_t)pgy * pb, ((singles >> h) & 1ull) ? ~full : 0xFFFFFFFFu, lane);
             } else {
                 load_page<M>(Y, pages + (uint64_t)pgy * (64u * M));
             }
@@ -1145,7 +1168,7 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
                                                                ? 4u * lane
                                                                : kBufOOB) +
                                                               256u * j,
-                                                          0, 0);
+                                                          0, CC_LOG_STORE_AUX);
             }
             uint32_t crc;
             if constexpr (Delta) {
@@ -1160,7 +1183,13 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
             } else {
                 crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
             }
-            if (lane == 0 && !hot) a.page_crcs[pg] = crc;
+            if (lane == 0 && !hot) {
+#if CC_LOG_CRC_NT
+                __builtin_nontemporal_store(crc, a.page_crcs + pg);
+#else
+                a.page_crcs[pg] = crc;
+#endif
+            }
             return more;
         };
         // the two register sets alternate (no copies): page k in one while page
