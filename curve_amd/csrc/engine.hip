@@ -502,9 +502,25 @@ int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, u
     const uint64_t need = (n + wpb - 1) / wpb;
     const uint64_t cap = (uint64_t)c->cus * CC_RANGE_GRID_MULT;
     const int blocks = (int)(need < cap ? need : cap);
-    return map_err(launch_range_crc(static_cast<const unsigned char*>(d_buf),
-                                    reinterpret_cast<const RangeDesc*>(d_ranges), n, c->image, d_out, blocks,
-                                    static_cast<hipStream_t>(stream)));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const RangeDesc* rd = reinterpret_cast<const RangeDesc*>(d_ranges);
+#ifndef CC_RANGE_ORDER_MIN
+#define CC_RANGE_ORDER_MIN 8192  // batches this large are dealt out in decreasing-size order
+#endif
+    if (n < (uint64_t)CC_RANGE_ORDER_MIN || n > 0xFFFFFFFFull)
+        return map_err(launch_range_crc(static_cast<const unsigned char*>(d_buf), rd, nullptr, n, c->image, d_out,
+                                        blocks, s));
+    // stream-ordered scratch of this call (calls on different streams may overlap)
+    const size_t hist_bytes = (size_t)kOrderBins * kOrderBlocks * 4;
+    unsigned char* scratch = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&scratch), hist_bytes + n * 4, s);
+    if (e != hipSuccess) return map_err(e);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(scratch);
+    uint32_t* perm = reinterpret_cast<uint32_t*>(scratch + hist_bytes);
+    if ((e = launch_range_order(rd, n, hist, perm, s)) == hipSuccess)
+        e = launch_range_crc(static_cast<const unsigned char*>(d_buf), rd, perm, n, c->image, d_out, blocks, s);
+    const hipError_t f = hipFreeAsync(scratch, s);
+    return map_err(e != hipSuccess ? e : f);
 }
 
 int cc_crc_bufs_host(const void* const* h_bufs, const uint64_t* h_lens, uint64_t n, uint32_t* h_out) {
@@ -591,8 +607,8 @@ int cc_crc_bufs_host(const void* const* h_bufs, const uint64_t* h_lens, uint64_t
         const uint64_t wpb = (uint64_t)range_waves();
         const uint64_t need = (k + wpb - 1) / wpb;
         const int blocks = (int)(need < (uint64_t)c->cus ? need : (uint64_t)c->cus);
-        if ((e = launch_range_crc(static_cast<const unsigned char*>(st.dev[s]), drecs, k, c->image, st.dcrc[s],
-                                  blocks, strm)) != hipSuccess)
+        if ((e = launch_range_crc(static_cast<const unsigned char*>(st.dev[s]), drecs, nullptr, k, c->image,
+                                  st.dcrc[s], blocks, strm)) != hipSuccess)
             return ring.fail(map_err(e));
         if ((e = hipMemcpyAsync(st.hcrc[s], st.dcrc[s], k * 4, hipMemcpyDeviceToHost, strm)) != hipSuccess)
             return ring.fail(map_err(e));

@@ -153,8 +153,14 @@ hipError_t launch_read_verify(const ReadVerifyLaunch& a, hipStream_t s);
 // CRC32C (butil Value) of arbitrary byte ranges of one device buffer; one
 // wave per range descriptor batch, range_waves() waves per workgroup.
 int range_waves();
-hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, const void* image,
-                            uint32_t* out, int blocks, hipStream_t s);
+// perm: NULL, or the order in which the static schedule deals the ranges out
+// (launch_range_order: decreasing 4 KiB-block count)
+hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, const uint32_t* perm, uint64_t n,
+                            const void* image, uint32_t* out, int blocks, hipStream_t s);
+// perm[0..n) = range indices by decreasing 4 KiB-block count (counting sort,
+// two launches); hist: kOrderBins * kOrderBlocks uint32 of scratch; n < 2^32
+constexpr uint32_t kOrderBins = 64, kOrderBlocks = 128;
+hipError_t launch_range_order(const RangeDesc* ranges, uint64_t n, uint32_t* hist, uint32_t* perm, hipStream_t s);
 // x^(-8t) mod P for t = 0..kXinvEntries-1 (undoing the zero pad after a range in its last 4 KiB block)
 constexpr uint32_t kXinvEntries = 4100;  // x^(-8t), t < 4096 + 4: the zero pad after a range in its last 4 KiB block
 hipError_t upload_xinv(const uint32_t* table);

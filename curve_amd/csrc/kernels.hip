@@ -480,7 +480,8 @@ constexpr int kRangeWaves = CC_RANGE_WAVES;
 #define CC_RANGE_DEPTH 3  // 4 KiB blocks in flight behind the one being folded (A/B: 3 ~3 % over 2 on WAL sizes)
 #endif
 __global__ __launch_bounds__(64 * kRangeWaves) void range_crc_kernel(const unsigned char* __restrict__ buf,
-                                                                  const RangeDesc* __restrict__ ranges, uint64_t n,
+                                                                  const RangeDesc* __restrict__ ranges,
+                                                                  const uint32_t* __restrict__ perm, uint64_t n,
                                                                   const uint4* __restrict__ image,
                                                                   uint32_t* __restrict__ out) {
     __shared__ uint32_t tab[kLdsBytes / 4];
@@ -494,8 +495,12 @@ __global__ __launch_bounds__(64 * kRangeWaves) void range_crc_kernel(const unsig
     for (uint64_t base = (uint64_t)blockIdx.x * kRangeWaves + wave; base < n; base += 64u * W) {
         const uint64_t ri = base + (uint64_t)lane * W;
         const bool valid = ri < n;
-        const RangeDesc rd = ranges[valid ? ri : base];
-        if (valid && rd.len == 0) out[ri] = 0u;  // V(empty) = 0
+        // position ri of the batch's order: the range itself, or perm[ri]
+        // (decreasing size, launch_range_order) so the stride deals the
+        // largest ranges out first, one per wave (LPT-like balance)
+        const uint64_t ix = perm ? (uint64_t)perm[valid ? ri : base] : (valid ? ri : base);
+        const RangeDesc rd = ranges[ix];
+        if (valid && rd.len == 0) out[ix] = 0u;  // V(empty) = 0
         uint64_t bits = __ballot(valid && rd.len != 0);
         if (!bits) continue;
         auto geo = [&](uint32_t h) {
@@ -566,7 +571,8 @@ __global__ __launch_bounds__(64 * kRangeWaves) void range_crc_kernel(const unsig
                 } else {
                     v ^= ~mulmod_dev(xpow_wave(gx.len << 3, lane), 0xFFFFFFFFu);
                 }
-                if (lane == 0) out[base + (uint64_t)px.h * W] = v;
+                const uint64_t oi = readlane64(ix, px.h);
+                if (lane == 0) out[oi] = v;
             }
         };
 #if CC_RANGE_DEPTH == 3
@@ -1497,11 +1503,106 @@ hipError_t upload_xinv(const uint32_t* table) { return hipMemcpyToSymbol(HIP_SYM
 
 int range_waves() { return kRangeWaves; }
 
-hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, const void* image,
-                            uint32_t* out, int blocks, hipStream_t s) {
+hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, const uint32_t* perm, uint64_t n,
+                            const void* image, uint32_t* out, int blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(range_crc_kernel, dim3(blocks), dim3(64 * kRangeWaves), 0, s, buf, ranges, n,
+    hipLaunchKernelGGL(range_crc_kernel, dim3(blocks), dim3(64 * kRangeWaves), 0, s, buf, ranges, perm, n,
                        static_cast<const uint4*>(image), out);
+    return hipGetLastError();
+}
+
+// Decreasing-size order of a range batch: a counting sort of the ranges by
+// 4 KiB-block count (kOrderBins bins, bin 0 = the largest), in two launches.
+// Block b of kOrderBlocks owns ranges [n*b/B, n*(b+1)/B).  Stable: within a
+// bin the ranges keep their batch order, so neighbours in memory stay
+// neighbours in the schedule (an unstable scatter cost ~25 us of locality).
+__device__ __forceinline__ uint32_t range_bin(const RangeDesc& d) {
+    if (d.len == 0) return kOrderBins - 1;
+    const uint32_t nb = range_geo(d.off, d.len).nb;  // >= 1
+    return nb >= kOrderBins ? 0u : kOrderBins - nb;
+}
+
+constexpr uint32_t kOrderThreads = 256;
+__global__ __launch_bounds__(kOrderThreads) void range_hist_kernel(const RangeDesc* __restrict__ ranges, uint64_t n,
+                                                                   uint32_t* __restrict__ hist) {
+    __shared__ uint32_t cnt[kOrderBins];
+    if (threadIdx.x < kOrderBins) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t lo = n * blockIdx.x / kOrderBlocks, hi = n * (blockIdx.x + 1) / kOrderBlocks;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += kOrderThreads) atomicAdd(&cnt[range_bin(ranges[i])], 1u);
+    __syncthreads();
+    if (threadIdx.x < kOrderBins) hist[threadIdx.x * kOrderBlocks + blockIdx.x] = cnt[threadIdx.x];  // bin-major
+}
+
+__global__ __launch_bounds__(kOrderThreads) void range_scatter_kernel(const RangeDesc* __restrict__ ranges, uint64_t n,
+                                                                      const uint32_t* __restrict__ hist,
+                                                                      uint32_t* __restrict__ perm) {
+    constexpr uint32_t kAll = kOrderBins * kOrderBlocks, kPer = kAll / kOrderThreads, kW = kOrderThreads / 64;
+    __shared__ uint32_t part[kOrderThreads], cur[kOrderBins], wcnt[kW][kOrderBins];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    // exclusive scan of the bin-major histogram; keep this block's column
+    uint32_t v[kPer], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) sum += (v[j] = hist[t * kPer + j]);
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < kOrderThreads; d <<= 1) {  // inclusive Hillis-Steele scan of the partials
+        const uint32_t x = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    uint32_t acc = part[t] - sum;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t e = t * kPer + j;  // = bin * kOrderBlocks + block
+        if (e % kOrderBlocks == blockIdx.x) cur[e / kOrderBlocks] = acc;
+        acc += v[j];
+    }
+    if (t < kOrderBins)
+        for (uint32_t w = 0; w < kW; w++) wcnt[w][t] = 0;
+    __syncthreads();
+    // stable within a bin: chunks of kOrderThreads ranges in index order, a
+    // lane's rank among the earlier lanes of its wave with the same bin
+    const uint64_t lo = n * blockIdx.x / kOrderBlocks, hi = n * (blockIdx.x + 1) / kOrderBlocks;
+    for (uint64_t c = lo; c < hi; c += kOrderThreads) {
+        const uint64_t i = c + t;
+        const bool valid = i < hi;
+        const uint32_t bin = valid ? range_bin(ranges[i]) : 0u;
+        uint64_t same = __ballot(valid);
+#pragma unroll
+        for (uint32_t k = 0; k < 6; k++) {
+            const uint64_t x = __ballot((bin >> k) & 1u);
+            same &= ((bin >> k) & 1u) ? x : ~x;
+        }
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(same >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)same, 0u));
+        if (valid && rank == 0) wcnt[wv][bin] = (uint32_t)__popcll(same);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = cur[bin] + rank;
+            for (uint32_t w = 0; w < wv; w++) pos += wcnt[w][bin];
+            perm[pos] = (uint32_t)i;
+        }
+        __syncthreads();
+        if (t < kOrderBins) {
+            uint32_t add = 0;
+            for (uint32_t w = 0; w < kW; w++) {
+                add += wcnt[w][t];
+                wcnt[w][t] = 0;
+            }
+            cur[t] += add;
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_range_order(const RangeDesc* ranges, uint64_t n, uint32_t* hist, uint32_t* perm, hipStream_t s) {
+    if (n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(range_hist_kernel, dim3(kOrderBlocks), dim3(kOrderThreads), 0, s, ranges, n, hist);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(range_scatter_kernel, dim3(kOrderBlocks), dim3(kOrderThreads), 0, s, ranges, n,
+                       static_cast<const uint32_t*>(hist), perm);
     return hipGetLastError();
 }
 

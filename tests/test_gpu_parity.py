@@ -620,7 +620,8 @@ def test_write_log_delta_keeps_latent_corruption(dev, oracle, page_bytes):
 
 def test_crc_ranges_large_batch(dev, oracle):
     """cc_crc_ranges_dev over a batch larger than the grid (several 64-range
-    descriptor batches per wave): 10,000 ranges of every shape (empty, 1-3
+    descriptor batches per wave; >= 8192 ranges, so dealt out in decreasing-size
+    order through launch_range_order): 10,000 ranges of every shape (empty, 1-3
     bytes, unaligned, multi-block, one 3 MiB giant) == the oracle."""
     from curve_amd import crc as C
     rng = np.random.default_rng(4096)
