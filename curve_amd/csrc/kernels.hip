@@ -25,6 +25,8 @@
 // src/chunkserver/copyset_node.cpp:964), all of which call
 // curve::common::CRC32 (src/common/crc32.h:40-55).
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <stdint.h>
 
 #include "kernels.h"
@@ -341,6 +343,9 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
 #endif
 #ifndef CC_LOG_CRC_NT
 #define CC_LOG_CRC_NT 0  // nontemporal page-CRC stores in the write-log kernels
+#endif
+#ifndef CC_LOG_ROWSEL
+#define CC_LOG_ROWSEL 1  // full mode: one-piece pages through the per-row source/page select (merge_edges)
 #endif
 #ifndef CC_LOG_STORE_AUX
 #define CC_LOG_STORE_AUX 2  // cache policy bits of the write-log row stores (2 = nontemporal: -20 us a batch)
@@ -1022,6 +1027,103 @@ __device__ __forceinline__ void merge_piece(uint32_t (&w)[M], uint32_t& dirty, c
 }
 
 
+// Full-mode fast path for a page with ONE piece (the common case).  Every row
+// is, uniformly, untouched (read from the page), covered whole by the piece
+// (read from the source: that row's buffer descriptor is the source's, chosen
+// by a scalar select, with the same vector offset), or an edge row -- the
+// first / last touched row when the piece starts / ends inside it (read from
+// the page; its source dwords are fetched on their own and merged).  So no row
+// but the <= 2 edge rows costs a vector compare or select (the generic path
+// spends ~12 VALU a row on them: 411 VALU a page, the kernel's issue bound).
+struct PieceEdges {
+    uint32_t r[2];          // edge rows (uniform; kNoRow = none)
+    uint32_t s[2];          // the lane's source dword in edge row q, if wholly inside the piece
+    uint32_t ea[2], eb[2];  // the partially covered dwords' aligned source dwords (as PieceSrc)
+};
+constexpr uint32_t kNoRow = 0xFFFFu;
+
+__device__ __forceinline__ void edge_rows(const Piece& p, uint32_t (&r)[2]) {
+    const uint32_t row0 = p.rlo >> 8, row1 = (p.rhi - 1) >> 8;
+    r[0] = (p.rlo & 255u) ? row0 : kNoRow;
+    r[1] = ((p.rhi & 255u) && row1 != r[0]) ? row1 : kNoRow;
+}
+
+__device__ __forceinline__ uint32_t covered_rows(const Piece& p) {  // rows [f0, f1) the piece covers whole
+    const uint32_t f0 = (p.rlo + 255u) >> 8, f1 = p.rhi >> 8;
+    return f1 > f0 ? ((f1 >= 32u ? 0xFFFFFFFFu : (1u << f1) - 1u) & ~((1u << f0) - 1u)) : 0u;
+}
+
+template <int M>
+__device__ __forceinline__ void load_rows_sel(uint32_t (&w)[M], const unsigned char* page, const unsigned char* sp,
+                                              uint32_t cov, uint32_t lane) {
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(page), 0, 256u * M,
+                                                                         kBufFlags);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(sp), 0, 256u * M,
+                                                                         kBufFlags);
+#pragma unroll
+    for (int j = 0; j < M; j++)
+        w[j] = __builtin_amdgcn_raw_buffer_load_b32(((cov >> j) & 1u) ? rs : rp, 4u * lane + 256u * j, 0, 2);
+}
+
+template <int M>
+__device__ __forceinline__ void fetch_edges(PieceEdges& r, const Piece& p, uint32_t lane) {
+    const uint32_t sh = (uint32_t)(uintptr_t)p.sp & 3u;
+    const __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(p.sp), 0, 64u * 4u * M + 8u, kBufFlags);
+    const __amdgpu_buffer_rsrc_t re =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(p.sp - sh), 0, 64u * 4u * M + 8u, kBufFlags);
+    edge_rows(p, r.r);
+    const PieceLane pl = piece_lane(p, lane);
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const bool in = r.r[q] != kNoRow && pl.o + 256u * r.r[q] < pl.l3;
+        r.s[q] = __builtin_amdgcn_raw_buffer_load_b32(rw, in ? 4u * lane + 256u * r.r[q] : kBufOOB, 0, 0);
+    }
+    uint32_t e[2];
+    piece_edges(p, e);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const uint32_t b = 4 * (e[k] & 0x3fffffffu);
+        const bool mine = e[k] != 0xffffffffu && lane == (e[k] & 63u);
+        const uint32_t k0 = p.rlo > b ? p.rlo - b : 0u;
+        const uint32_t k1 = p.rhi < b + 4 ? p.rhi - b : 4u;
+        r.ea[k] = __builtin_amdgcn_raw_buffer_load_b32(re, (mine && k0 < 4u - sh) ? b : kBufOOB, 0, 0);
+        r.eb[k] = __builtin_amdgcn_raw_buffer_load_b32(re, (mine && sh && k1 > 4u - sh) ? b + 4 : kBufOOB, 0, 0);
+    }
+}
+
+// w: rows loaded by load_rows_sel (covered rows already hold the new bytes)
+template <int M>
+__device__ __forceinline__ void merge_edges(uint32_t (&w)[M], uint32_t& dirty, const PieceEdges& r, const Piece& p,
+                                            uint32_t lane) {
+    const PieceLane pl = piece_lane(p, lane);
+    uint32_t e[2];
+    piece_edges(p, e);
+    const uint32_t sh = (uint32_t)(uintptr_t)p.sp & 3u;
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const uint32_t rq = r.r[q];
+        if (rq == kNoRow) continue;  // uniform
+        uint32_t v = w[rq];          // uniform dynamic row index
+        v = pl.o + 256u * rq < pl.l3 ? r.s[q] : v;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (e[k] == 0xffffffffu || (e[k] >> 6) != rq) continue;  // uniform
+            const uint32_t spl = sh ? __builtin_amdgcn_alignbyte(r.eb[k], r.ea[k], sh) : r.ea[k];
+            const uint32_t b = 4 * e[k];
+            const uint32_t k0 = p.rlo > b ? p.rlo - b : 0u;
+            const uint32_t k1 = p.rhi < b + 4 ? p.rhi - b : 4u;
+            const uint32_t mhi = k1 >= 4u ? 0xFFFFFFFFu : (1u << (8u * k1)) - 1u;
+            const uint32_t mask = mhi & ~((1u << (8u * (k0 & 3u))) - 1u);
+            v = lane == (e[k] & 63u) ? (spl & mask) | (v & ~mask) : v;
+        }
+        w[rq] = v;
+    }
+    const PieceRows pr = piece_rows(p);
+    const uint32_t top = pr.row1 >= 31 ? 0xFFFFFFFFu : (2u << pr.row1) - 1u;
+    dirty |= top & ~((1u << pr.row0) - 1u);
+}
+
 // One wave per touched page, balanced: wave w owns heads w, w + W, w + 2W, ...
 // (W = waves in the grid), ~pages/W each.  Its lanes load the metadata of up to
 // 64 of its heads at once (table entry: page + one piece, that piece's list
@@ -1088,7 +1190,16 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
         // loads, 20 source loads, 17 stores -- and gfx950's 6-bit vmcnt cannot
         // count two iterations' worth, so the waits stop being exact.)
         uint32_t A[M], B[M];
-        PieceSrc<M> S0, S1;
+        constexpr bool kRowSel = CC_LOG_ROWSEL && !Delta && CC_LOG_ABLATE == 0;
+        using Src = typename std::conditional<kRowSel, PieceEdges, PieceSrc<M>>::type;
+        Src S0, S1;
+        auto fetch = [&](Src& r, const Piece& p) {
+            if constexpr (kRowSel) {
+                fetch_edges<M>(r, p, lane);
+            } else {
+                fetch_piece<M>(r, p, lane);
+            }
+        };
         auto head_piece = [&](uint32_t k, uint32_t pg) {
             return piece_in_page((uint64_t)pg * pb, pb, readlane64(ddst, k), readlane64(dsrc, k),
                                  __builtin_amdgcn_readlane(dlen, k), a.src);
@@ -1107,6 +1218,10 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
                 uint32_t vz = 0;
                 asm volatile("" : "+v"(vz));
                 ocy = a.page_crcs[pgy + vz];
+            } else if constexpr (kRowSel) {
+                // rows the page's only piece covers whole come straight from the source
+                load_rows_sel<M>(Y, a.pool + (uint64_t)pgy * pb, py.sp, ((singles >> h) & 1ull) ? covered_rows(py) : 0u,
+                                 lane);
             } else if constexpr (CC_LOG_ABLATE == 3 || CC_LOG_ABLATE == 5) {
                 load_rows<M>(Y, a.pool + (uint64_t)pgy * pb, 0u, lane);  // timing ablation: no page reads
             } else if constexpr (CC_LOG_SKIP_COVERED) {
@@ -1120,8 +1235,8 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
                 load_page<M>(Y, pages + (uint64_t)pgy * (64u * M));
             }
         };
-        auto step = [&](uint32_t (&X)[M], PieceSrc<M>& SX, const Piece& px, uint32_t pg, uint32_t hh, uint32_t ocx,
-                        uint32_t (&Y)[M], PieceSrc<M>& SY, Piece& py, uint32_t& pgy, uint32_t& ocy) {
+        auto step = [&](uint32_t (&X)[M], Src& SX, const Piece& px, uint32_t pg, uint32_t hh, uint32_t ocx,
+                        uint32_t (&Y)[M], Src& SY, Piece& py, uint32_t& pgy, uint32_t& ocy) {
             const bool more = hh + 1 < cnt;
             // next page + its first piece's source bytes in flight (clamped to the
             // last page: a harmless re-read, so every step issues the same loads
@@ -1130,7 +1245,7 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
             pgy = __builtin_amdgcn_readlane(key, h1);
             py = head_piece(h1, pgy);
             load_next(Y, py, pgy, h1, ocy);
-            fetch_piece<M>(SY, py, lane);
+            fetch(SY, py);
             const uint64_t pbase = (uint64_t)pg * pb;
             uint32_t dirty = 0;
             uint32_t O[Delta ? M : 1];
@@ -1140,7 +1255,11 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
             }
             bool hot = false;
             if ((singles >> hh) & 1ull) {
-                merge_piece<M>(X, dirty, SX, px, lane);
+                if constexpr (kRowSel) {
+                    merge_edges<M>(X, dirty, SX, px, lane);
+                } else {
+                    merge_piece<M>(X, dirty, SX, px, lane);
+                }
             } else {  // several pieces: collect the list, apply in log (update index) order
                 uint32_t q = __builtin_amdgcn_readlane(pfirst, hh), cnt = 0, mine = kNoPiece;
                 while (q != kNoPiece && cnt < 64u) {
@@ -1159,8 +1278,14 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
                         const uint32_t l = (uint32_t)__builtin_ctzll(__ballot(rank == r));
                         const UpdateDesc dq = a.upd[__builtin_amdgcn_readlane(idx, l)];
                         const Piece pq = piece_in_page(pbase, pb, dq.dst, dq.src, dq.len, a.src);
-                        fetch_piece<M>(SX, pq, lane);  // SX (the prefetched head piece) is not used: reuse it
-                        merge_piece<M>(X, dirty, SX, pq, lane);
+                        if constexpr (kRowSel) {
+                            PieceSrc<M> T;
+                            fetch_piece<M>(T, pq, lane);
+                            merge_piece<M>(X, dirty, T, pq, lane);
+                        } else {
+                            fetch_piece<M>(SX, pq, lane);  // SX (the prefetched head piece) is not used: reuse it
+                            merge_piece<M>(X, dirty, SX, pq, lane);
+                        }
                     }
                 }
             }
@@ -1204,7 +1329,7 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
         uint32_t ocA = 0, ocB = 0;
         Piece pA = head_piece(0, pgA), pB = pA;
         load_next(A, pA, pgA, 0, ocA);
-        fetch_piece<M>(S0, pA, lane);
+        fetch(S0, pA);
         for (uint32_t h = 0;; h += 2) {
             if (!step(A, S0, pA, pgA, h, ocA, B, S1, pB, pgB, ocB)) break;
             if (!step(B, S1, pB, pgB, h + 1, ocB, A, S0, pA, pgA, ocA)) break;
