@@ -95,6 +95,11 @@ constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
 #define CC_LOG_WAVES 12  // waves per CU of the write-log page kernel (A/B: 12 beats 8 by ~6 %; 16 forces <= 128 VGPRs and spills in delta mode)
 #endif
 constexpr int kLogWaves = CC_LOG_WAVES;
+#ifndef CC_LOG_WAVES_FULL
+#define CC_LOG_WAVES_FULL 16  // full mode, pages <= 4 KiB: 127 VGPRs since the row-select merge, so 16 fit (A/B ~1.5 %)
+#endif
+// waves per workgroup of log_pages_kernel<M, Delta>
+constexpr int log_waves(int m, bool delta) { return (!delta && m <= 16) ? CC_LOG_WAVES_FULL : CC_LOG_WAVES; }
 struct LogLaunch {
     unsigned char* pool;
     uint64_t pool_bytes;

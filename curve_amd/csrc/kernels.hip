@@ -1158,9 +1158,10 @@ __device__ __forceinline__ void load_rows(uint32_t (&w)[M], const unsigned char*
 }
 
 template <int M, bool Delta>
-__global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
+__global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(LogLaunch a) {
+    constexpr int WV = log_waves(M, Delta);
     __shared__ uint32_t tab[kLdsBytes / 4];
-    fill_lds<64 * kLogWaves>(tab, static_cast<const uint4*>(a.image));
+    fill_lds<64 * WV>(tab, static_cast<const uint4*>(a.image));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t c0 = lane << 2 & 0x7Cu;
@@ -1169,8 +1170,8 @@ __global__ CC_LOG_ATTR void log_pages_kernel(LogLaunch a) {
     const uint32_t* pages = reinterpret_cast<const uint32_t*>(a.pool) + lane;
     const uint32_t pb = a.page_bytes;
     const uint32_t H = *a.head_count;
-    const uint32_t W = gridDim.x * kLogWaves;
-    for (uint32_t base = blockIdx.x * kLogWaves + wave; base < H; base += 64u * W) {
+    const uint32_t W = gridDim.x * WV;
+    for (uint32_t base = blockIdx.x * WV + wave; base < H; base += 64u * W) {
         // lane k <- head base + k*W (clamped loads: no branches around them)
         const uint64_t ih = (uint64_t)base + (uint64_t)lane * W;
         const bool hv = ih < H;
@@ -1776,9 +1777,11 @@ hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s) {
 #define CC_GCASE(MM)                                                                                        \
     case MM:                                                                                                \
         if (a.delta)                                                                                        \
-            hipLaunchKernelGGL((log_pages_kernel<MM, true>), dim3(a.blocks), dim3(64 * kLogWaves), 0, s, a);  \
+            hipLaunchKernelGGL((log_pages_kernel<MM, true>), dim3(a.blocks), dim3(64 * log_waves(MM, true)), 0, s,  \
+                               a);                                                                          \
         else                                                                                                \
-            hipLaunchKernelGGL((log_pages_kernel<MM, false>), dim3(a.blocks), dim3(64 * kLogWaves), 0, s, a); \
+            hipLaunchKernelGGL((log_pages_kernel<MM, false>), dim3(a.blocks), dim3(64 * log_waves(MM, false)), 0, \
+                               s, a);                                                                       \
         break;
     switch (a.page_bytes / kWaveBytes) {
         CC_GCASE(1)
