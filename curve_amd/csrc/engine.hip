@@ -10,6 +10,7 @@
 // submission lock.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <errno.h>
@@ -74,6 +75,7 @@ struct Staging {
     void* dev[2] = {nullptr, nullptr};
     uint32_t* dcrc[2] = {nullptr, nullptr};
     uint32_t* hcrc[2] = {nullptr, nullptr};
+    uint64_t* tiles[2] = {nullptr, nullptr};  // range batches: per-tile block counts (kRangeTiles)
     hipStream_t stream[2] = {nullptr, nullptr};
     hipEvent_t done[2] = {nullptr, nullptr};
     SlotSignal sig[2];
@@ -133,6 +135,8 @@ void staging_free(Staging& st) {
         if (st.dev[i]) hipFree(st.dev[i]);
         if (st.dcrc[i]) hipFree(st.dcrc[i]);
         if (st.hcrc[i]) hipHostFree(st.hcrc[i]);
+        if (st.tiles[i]) hipFree(st.tiles[i]);
+        st.tiles[i] = nullptr;
         if (st.stream[i]) hipStreamDestroy(st.stream[i]);
         if (st.done[i]) hipEventDestroy(st.done[i]);
         st.host[i] = st.dev[i] = nullptr;
@@ -190,13 +194,18 @@ int get_ctx(CtxRef* out) {
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     std::vector<uint32_t> img(kLdsBytes / 4);
     build_lds_image(img.data());
-    if ((e = hipMalloc(&c->image, kLdsBytes)) != hipSuccess) return map_err(e);
-    if ((e = hipMemcpy(c->image, img.data(), kLdsBytes, hipMemcpyHostToDevice)) != hipSuccess) return map_err(e);
-    if ((e = upload_x2k(x2k().t)) != hipSuccess) return map_err(e);
-    static uint32_t xinv[kXinvEntries];
+    // device image: the LDS image, then for t < kXinvEntries the 32 products
+    // x^(-8t) * x^i, i = 0..31 (range kernel: a lane-parallel multiply by x^(-8t))
+    img.resize(kLdsBytes / 4 + kXinvEntries * 32);
     uint32_t r = xinv_bytes(0);
-    for (uint32_t t = 0; t < kXinvEntries; t++, r = div_x8(r)) xinv[t] = r;  // x^(-8t)
-    if ((e = upload_xinv(xinv)) != hipSuccess) return map_err(e);
+    for (uint32_t t = 0; t < kXinvEntries; t++, r = div_x8(r)) {  // r = x^(-8t)
+        uint32_t b = r;
+        for (uint32_t i = 0; i < 32; i++, b = (b >> 1) ^ (kPoly & (0u - (b & 1u))))  // b *= x
+            img[kLdsBytes / 4 + t * 32 + i] = b;
+    }
+    if ((e = hipMalloc(&c->image, img.size() * 4)) != hipSuccess) return map_err(e);
+    if ((e = hipMemcpy(c->image, img.data(), img.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return map_err(e);
+    if ((e = upload_x2k(x2k().t)) != hipSuccess) return map_err(e);
     c->ready = true;
     std::atomic_store(&g_ctx[dev], c);
     *out = std::move(c);
@@ -242,6 +251,7 @@ int staging_init(DevCtx* c) {
         if ((e = hipMalloc(&st.dev[i], per)) != hipSuccess) return map_err(e);
         if ((e = hipMalloc(&st.dcrc[i], per / 256 * 4)) != hipSuccess) return map_err(e);
         if ((e = hipHostMalloc(&st.hcrc[i], per / 256 * 4, hipHostMallocDefault)) != hipSuccess) return map_err(e);
+        if ((e = hipMalloc(&st.tiles[i], (kRangeTiles + 1) * sizeof(uint64_t))) != hipSuccess) return map_err(e);
         if ((e = hipStreamCreateWithFlags(&st.stream[i], hipStreamNonBlocking)) != hipSuccess) return map_err(e);
         if ((e = hipEventCreateWithFlags(&st.done[i], hipEventDisableTiming)) != hipSuccess) return map_err(e);
     }
@@ -376,6 +386,10 @@ int cc_hbm_read_probe_dev(const void* d_buf, uint64_t bytes, uint32_t* d_sink, v
     return map_err(launch_read_probe(d_buf, bytes, d_sink, 2 * c->cus, static_cast<hipStream_t>(stream)));
 }
 
+#if CC_RANGE_TRACE
+int cc_debug_range_trace(uint64_t* host) { return map_err(range_trace_read(host)); }
+#endif
+
 int cc_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -493,33 +507,15 @@ int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, u
     CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
-#ifndef CC_RANGE_GRID_MULT
-#define CC_RANGE_GRID_MULT 1  // workgroups per CU launched for a range batch (> 1: hardware re-balances waves)
-#endif
-    // one descriptor per wave: enough workgroups of range_waves() waves to give
-    // every range its wave, capped at CC_RANGE_GRID_MULT workgroups per CU
-    const uint64_t wpb = (uint64_t)range_waves();
-    const uint64_t need = (n + wpb - 1) / wpb;
-    const uint64_t cap = (uint64_t)c->cus * CC_RANGE_GRID_MULT;
-    const int blocks = (int)(need < cap ? need : cap);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const RangeDesc* rd = reinterpret_cast<const RangeDesc*>(d_ranges);
-#ifndef CC_RANGE_ORDER_MIN
-#define CC_RANGE_ORDER_MIN 8192  // batches this large are dealt out in decreasing-size order
-#endif
-    if (n < (uint64_t)CC_RANGE_ORDER_MIN || n > 0xFFFFFFFFull)
-        return map_err(launch_range_crc(static_cast<const unsigned char*>(d_buf), rd, nullptr, n, c->image, d_out,
-                                        blocks, s));
-    // stream-ordered scratch of this call (calls on different streams may overlap)
-    const size_t hist_bytes = (size_t)kOrderBins * kOrderBlocks * 4;
-    unsigned char* scratch = nullptr;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&scratch), hist_bytes + n * 4, s);
+    // every wave an equal share of the batch's 4 KiB blocks; stream-ordered
+    // scratch of this call for the tile counts (calls on different streams may overlap)
+    uint64_t* tiles = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&tiles), (kRangeTiles + 1) * sizeof(uint64_t), s);
     if (e != hipSuccess) return map_err(e);
-    uint32_t* hist = reinterpret_cast<uint32_t*>(scratch);
-    uint32_t* perm = reinterpret_cast<uint32_t*>(scratch + hist_bytes);
-    if ((e = launch_range_order(rd, n, hist, perm, s)) == hipSuccess)
-        e = launch_range_crc(static_cast<const unsigned char*>(d_buf), rd, perm, n, c->image, d_out, blocks, s);
-    const hipError_t f = hipFreeAsync(scratch, s);
+    e = launch_range_flat(static_cast<const unsigned char*>(d_buf), rd, n, tiles, c->image, d_out, c->cus, s);
+    const hipError_t f = hipFreeAsync(tiles, s);
     return map_err(e != hipSuccess ? e : f);
 }
 
@@ -604,11 +600,8 @@ int cc_crc_bufs_host(const void* const* h_bufs, const uint64_t* h_lens, uint64_t
             return ring.fail(map_err(e));
         if ((e = hipMemcpyAsync(drecs, recs, k * sizeof(RangeDesc), hipMemcpyHostToDevice, strm)) != hipSuccess)
             return ring.fail(map_err(e));
-        const uint64_t wpb = (uint64_t)range_waves();
-        const uint64_t need = (k + wpb - 1) / wpb;
-        const int blocks = (int)(need < (uint64_t)c->cus ? need : (uint64_t)c->cus);
-        if ((e = launch_range_crc(static_cast<const unsigned char*>(st.dev[s]), drecs, nullptr, k, c->image,
-                                  st.dcrc[s], blocks, strm)) != hipSuccess)
+        if ((e = launch_range_flat(static_cast<const unsigned char*>(st.dev[s]), drecs, k, st.tiles[s], c->image,
+                                   st.dcrc[s], c->cus, strm)) != hipSuccess)
             return ring.fail(map_err(e));
         if ((e = hipMemcpyAsync(st.hcrc[s], st.dcrc[s], k * 4, hipMemcpyDeviceToHost, strm)) != hipSuccess)
             return ring.fail(map_err(e));

@@ -8,6 +8,8 @@ namespace cc {
 
 // LDS image geometry of the page kernel (see DESIGN.md "LDS image").
 constexpr uint32_t kLdsBytes = 163840;  // all 160 KiB of a CU's LDS
+// The device image is the LDS image followed by the x^(-8t) * x^i product table
+// (kXinvEntries x 32 words).
 constexpr uint32_t kFinBase = 131072;   // per-lane final-shift nibble tables [128K, 160K)
 constexpr uint32_t kWordsPerWaveStep = 64;  // one dword per lane per step
 constexpr uint32_t kWaveBytes = 256;        // bytes consumed per wave step
@@ -155,20 +157,19 @@ size_t scan_temp_bytes(uint64_t n);
 hipError_t exclusive_scan_u64(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
                               hipStream_t s);
 hipError_t launch_read_verify(const ReadVerifyLaunch& a, hipStream_t s);
-// CRC32C (butil Value) of arbitrary byte ranges of one device buffer; one
-// wave per range descriptor batch, range_waves() waves per workgroup.
-int range_waves();
-// perm: NULL, or the order in which the static schedule deals the ranges out
-// (launch_range_order: decreasing 4 KiB-block count)
-hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, const uint32_t* perm, uint64_t n,
-                            const void* image, uint32_t* out, int blocks, hipStream_t s);
-// perm[0..n) = range indices by decreasing 4 KiB-block count (counting sort,
-// two launches); hist: kOrderBins * kOrderBlocks uint32 of scratch; n < 2^32
-constexpr uint32_t kOrderBins = 64, kOrderBlocks = 128;
-hipError_t launch_range_order(const RangeDesc* ranges, uint64_t n, uint32_t* hist, uint32_t* perm, hipStream_t s);
+// CRC32C (butil Value) of arbitrary byte ranges of one device buffer, on the
+// flat block schedule: range_tiles_kernel writes the 4 KiB-block
+// count of each of kRangeTiles contiguous tiles of the batch (and zeroes
+// out[]); range_flat_kernel gives every wave an equal share of the blocks,
+// ranges cut by a share boundary XOR their segments into out[].
+// tile_blocks: kRangeTiles + 1 uint64 of stream-ordered scratch (the last: the
+// dynamic-tail chunk counter).
+constexpr uint32_t kRangeTiles = 1024;
+hipError_t range_trace_read(uint64_t* host);  // CC_RANGE_TRACE builds only: [4][8192]
+hipError_t launch_range_flat(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, uint64_t* tile_blocks,
+                             const void* image, uint32_t* out, int blocks, hipStream_t s);
 // x^(-8t) mod P for t = 0..kXinvEntries-1 (undoing the zero pad after a range in its last 4 KiB block)
 constexpr uint32_t kXinvEntries = 4100;  // x^(-8t), t < 4096 + 4: the zero pad after a range in its last 4 KiB block
-hipError_t upload_xinv(const uint32_t* table);
 
 // Fused scan epilogue: one 256-thread block per chunk.
 struct EpilogueLaunch {

@@ -384,10 +384,23 @@ __device__ __forceinline__ uint32_t xpow_dev(uint64_t n) {
     return r;
 }
 
-struct XInv {
-    uint32_t t[kXinvEntries];
-};
-__constant__ XInv c_xinv;  // x^(-8t) mod P, t = 0 .. kXinvEntries-1
+// Compact forms for once-per-range code inside unrolled block loops (keeps
+// the kernel's instruction footprint small; the unrolled ones are 6x larger).
+__device__ __forceinline__ uint32_t mulmod_small(uint32_t a, uint32_t b) {
+    uint32_t prod = 0;
+#pragma unroll 4
+    for (int i = 0; i < 32; i++) {
+        prod ^= b & (0u - ((a >> (31 - i)) & 1u));
+        b = (b >> 1) ^ (kPolyDev & (0u - (b & 1u)));
+    }
+    return prod;
+}
+__device__ __forceinline__ uint32_t xpow_wave_small(uint64_t n, uint32_t lane) {
+    uint32_t f = ((n >> lane) & 1u) ? c_x2k.t[lane] : 0x80000000u;
+#pragma unroll 1
+    for (int t = 1; t < 64; t <<= 1) f = mulmod_small(f, __shfl_xor(f, t, 64));
+    return f;
+}
 
 // Product over the wave of per-lane GF(2)[x]/P factors (lane k: x^(2^k) if bit k
 // of n is set, else 1) = x^n mod P; result in every lane.
@@ -409,12 +422,9 @@ __device__ __forceinline__ uint32_t xpow_wave(uint64_t n, uint32_t lane) {
 // raw(M ^ (~0 || 0...)) ^ ~0, so the first four bytes of the range are XORed
 // with 0xFF as they are loaded.  (len < 4: K(len) = ~shift(~0, len) instead.)
 //
-// Schedule: wave w owns ranges w, w+W, ... (W = waves in the grid); its lanes
-// load 64 range descriptors at once, and the wave walks their 4 KiB blocks (16
-// rows) as one stream: block k+1 -- of the same range or the next one -- is
-// loaded while block k is masked and chained, so a range of any length keeps
-// a block of loads in flight.  Loads are buffer loads with an out-of-range
-// offset for rows past the range (no branches around them: exact vmcnt waits).
+// Blocks are loaded as buffer loads with an out-of-range offset for rows past
+// the range (no branches around them: exact vmcnt waits); the schedule is the
+// flat block stream below (range_flat_kernel).
 // ---------------------------------------------------------------------------
 struct RangeGeo {
     uint64_t a;      // 256-byte-aligned start
@@ -435,24 +445,33 @@ __device__ __forceinline__ RangeGeo range_geo(uint64_t off, uint64_t len) {
     return g;
 }
 
-// Block k of range g (16 rows, lane l holds dwords l + 64j of the block).
-__device__ __forceinline__ void load_range_block(uint32_t (&w)[16], const unsigned char* buf, const RangeGeo& g,
-                                                 uint32_t k, uint32_t lane) {
+// Block k of range g (16 rows, lane l holds dwords l + 64j of the block) into
+// w[0..15]; when k is the range's last block, w[16] of lane i < 32 =
+// x^(-8t) * x^i, t = the zero pad after the range (the table behind the LDS
+// image; one 128-byte load in flight with the block), so the pad is removed by
+// a lane-parallel multiply (mul_xinv) instead of a 32-step serial one.
+__device__ __forceinline__ void load_range_block(uint32_t (&w)[17], const unsigned char* buf, const RangeGeo& g,
+                                                 uint32_t k, uint32_t lane, __amdgpu_buffer_rsrc_t xr,
+                                                 bool live = true) {
     // the descriptor's record count ends the block at the range's last dword
     // (rounded up to 4 bytes: a dword that starts inside the range is in
     // bounds, the next one is not, whether the unit tests the dword's start or
     // its end), so rows past the range read 0 with no per-row select
+    // (a stream position past the wave's last block -- `live` false -- loads nothing)
     const uint64_t rem = g.lim - ((uint64_t)k << 12);  // > 0 for every block of the range
-    const uint32_t nr = rem >= 4096u ? 4096u : (((uint32_t)rem + 3u) & ~3u);
+    const uint32_t nr = !live ? 0u : rem >= 4096u ? 4096u : (((uint32_t)rem + 3u) & ~3u);
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(buf + g.a + ((uint64_t)k << 12)), 0, nr, kBufFlags);
 #pragma unroll
     for (int j = 0; j < 16; j++) w[j] = __builtin_amdgcn_raw_buffer_load_b32(r, 4u * lane + 256u * j, 0, 2);
+    const uint32_t xo = (live && k + 1 == g.nb) ? 128u * (uint32_t)(((uint64_t)g.nb << 12) - g.lim) + 4u * (lane & 31u)
+                                                : kBufOOB;
+    w[16] = __builtin_amdgcn_raw_buffer_load_b32(xr, xo, 0, 0);
 }
 
 // Zero the bytes outside the range (first / last dword) and fold butil's init
 // into the first four bytes.  Block k; the row/lane tests are per-lane compares.
-__device__ __forceinline__ void mask_range_block(uint32_t (&w)[16], const RangeGeo& g, uint32_t k, uint32_t lane) {
+__device__ __forceinline__ void mask_range_block(uint32_t (&w)[17], const RangeGeo& g, uint32_t k, uint32_t lane) {
     const uint64_t last = g.lim - 1;  // byte offset (from a) of the range's last byte
     const uint32_t tail = (uint32_t)(g.lim & 3u);
     if (tail && k + 1 == g.nb) {  // uniform: only a range's last block has bytes after its end
@@ -477,138 +496,286 @@ __device__ __forceinline__ void mask_range_block(uint32_t (&w)[16], const RangeG
     }
 }
 
-#ifndef CC_RANGE_WAVES
-#define CC_RANGE_WAVES 12  // waves per CU of the range kernel (A/B: 12 ~3 % over 8, 16 equal)
+// ---------------------------------------------------------------------------
+// Flat block schedule of a range batch (WAL replay, raw-file hashes).  The
+// batch is one stream of 4 KiB blocks (range 0's blocks, then range 1's, ...),
+// B blocks in all.  The first Bs = B - B/kDynDiv are dealt out statically:
+// rounds * W equal pieces, wave w taking pieces w, w + W, ... whatever the
+// range sizes.  The last B/kDynDiv blocks are kDynBlocks-block chunks handed
+// out through an atomic counter to whichever waves finish first (per-wave
+// rates differ by ~7 % -- some XCDs run slower -- so a purely static split
+// waits for the slowest wave).  A range cut by a piece or chunk boundary is
+// hashed in segments: segment [kb, ke) of the range contributes
+// raw(segment || 0-pad) * x^(8 * (lim - 4096*ke)) (x^(-8t) for the one that
+// ends the range), XORed into out[] (zeroed by the tile pass); a range hashed
+// whole by one wave is stored directly.  Where a piece starts comes from
+// kRangeTiles per-tile block counts (range_tiles_kernel, one launch before),
+// held in registers by every wave.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void range_tiles_kernel(const RangeDesc* __restrict__ ranges, uint64_t n,
+                                                          uint64_t* __restrict__ tile_blocks,
+                                                          uint32_t* __restrict__ out) {
+    __shared__ uint64_t part[4];
+    const uint64_t lo = n * blockIdx.x / kRangeTiles, hi = n * (blockIdx.x + 1) / kRangeTiles;
+    uint64_t sum = 0;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += 256) {
+        const RangeDesc d = ranges[i];
+        sum += d.len ? range_geo(d.off, d.len).nb : 0u;
+        out[i] = 0u;  // V(empty) = 0; split ranges XOR their segments into it
+    }
+#pragma unroll
+    for (int d = 32; d; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        tile_blocks[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+        if (blockIdx.x == 0) tile_blocks[kRangeTiles] = 0;  // the dynamic chunk counter
+    }
+}
+
+__device__ __forceinline__ uint64_t wave_scan_incl(uint64_t v, uint32_t lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(v, d, 64);
+        if (lane >= (uint32_t)d) v += o;
+    }
+    return v;
+}
+
+#ifndef CC_RANGE_ABLATE
+#define CC_RANGE_ABLATE 0  // timing ablations (wrong CRCs): 1 no per-range multiply, 2 no per-range finish
 #endif
-constexpr int kRangeWaves = CC_RANGE_WAVES;
-#ifndef CC_RANGE_DEPTH
-#define CC_RANGE_DEPTH 3  // 4 KiB blocks in flight behind the one being folded (A/B: 3 ~3 % over 2 on WAL sizes)
+#ifndef CC_RANGE_TRACE
+#define CC_RANGE_TRACE 0  // diagnostic builds: per-wave start/end wall clock of range_flat_kernel
 #endif
-__global__ __launch_bounds__(64 * kRangeWaves) void range_crc_kernel(const unsigned char* __restrict__ buf,
-                                                                  const RangeDesc* __restrict__ ranges,
-                                                                  const uint32_t* __restrict__ perm, uint64_t n,
-                                                                  const uint4* __restrict__ image,
-                                                                  uint32_t* __restrict__ out) {
+#if CC_RANGE_TRACE
+__device__ uint64_t g_rtrace[4][8192];  // start, end, block, cu
+#endif
+#ifndef CC_FLAT_WAVES
+#define CC_FLAT_WAVES 8  // waves per CU of the flat range kernel (A/B on WAL sizes: 8 beats 12 by ~4 %, 16 by ~10 %)
+#endif
+constexpr int kFlatWaves = CC_FLAT_WAVES;
+#ifndef CC_RANGE_ROUNDS
+#define CC_RANGE_ROUNDS 2  // static pieces per wave (A/B: 2 best; 1 loses on equal sizes, 8 on random)
+#endif
+#ifndef CC_RANGE_DYN_DIV
+#define CC_RANGE_DYN_DIV 32  // 1/32 of the blocks go to the dynamic tail (0: none; A/B: 1/8 and 1/16 lose to
+                             // the one counter's atomics, 1/64 leaves tail)
+#endif
+#ifndef CC_RANGE_DYN_BLOCKS
+#define CC_RANGE_DYN_BLOCKS 16  // blocks per dynamic chunk (A/B: 8 slower, 16 = 32)
+#endif
+__global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsigned char* __restrict__ buf,
+                                                                   const RangeDesc* __restrict__ ranges, uint64_t n,
+                                                                   uint64_t* __restrict__ tile_blocks,
+                                                                   const uint4* __restrict__ image,
+                                                                   uint32_t* __restrict__ out) {
+    constexpr uint32_t rounds = CC_RANGE_ROUNDS;
     __shared__ uint32_t tab[kLdsBytes / 4];
-    fill_lds<64 * kRangeWaves>(tab, image);
+    fill_lds<64 * kFlatWaves>(tab, image);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t c0 = lane << 2 & 0x7Cu;
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
-    const uint64_t W = (uint64_t)gridDim.x * kRangeWaves;
-    for (uint64_t base = (uint64_t)blockIdx.x * kRangeWaves + wave; base < n; base += 64u * W) {
-        const uint64_t ri = base + (uint64_t)lane * W;
-        const bool valid = ri < n;
-        // position ri of the batch's order: the range itself, or perm[ri]
-        // (decreasing size, launch_range_order) so the stride deals the
-        // largest ranges out first, one per wave (LPT-like balance)
-        const uint64_t ix = perm ? (uint64_t)perm[valid ? ri : base] : (valid ? ri : base);
-        const RangeDesc rd = ranges[ix];
-        if (valid && rd.len == 0) out[ix] = 0u;  // V(empty) = 0
-        uint64_t bits = __ballot(valid && rd.len != 0);
-        if (!bits) continue;
-        auto geo = [&](uint32_t h) {
-            return range_geo(readlane64(rd.off, h), readlane64(rd.len, h));
+    const uint64_t W = (uint64_t)gridDim.x * kFlatWaves;
+    const uint64_t w = (uint64_t)blockIdx.x * kFlatWaves + wave;
+#if CC_RANGE_TRACE
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint4*>(image) + kLdsBytes / 16, 0, kXinvEntries * 128u, kBufFlags);
+
+    // tile block counts: lane l holds tiles kTpl*l .. kTpl*l + kTpl-1, cum = inclusive prefix of the lane sums
+    constexpr int kTpl = kRangeTiles / 64;
+    uint64_t tb[kTpl], lsum = 0;
+#pragma unroll
+    for (int j = 0; j < kTpl; j++) lsum += (tb[j] = tile_blocks[kTpl * lane + j]);
+    const uint64_t cum = wave_scan_incl(lsum, lane);
+    const uint64_t B = readlane64(cum, 63);
+    const uint64_t Bs = CC_RANGE_DYN_DIV ? B - B / CC_RANGE_DYN_DIV : B;  // statically dealt blocks
+    const uint64_t n_dyn = (B - Bs + CC_RANGE_DYN_BLOCKS - 1) / CC_RANGE_DYN_BLOCKS;
+    unsigned long long* dyn_ctr = reinterpret_cast<unsigned long long*>(tile_blocks + kRangeTiles);
+
+    // work items: static pieces item < rounds, then dynamic chunks until the counter runs out
+#pragma unroll 1
+    for (uint32_t item = 0;; item++) {
+        uint64_t b0, b1;
+        if (item < rounds) {
+            const uint64_t RW = (uint64_t)rounds * W, c = (uint64_t)item * W + w;
+            b0 = Bs * c / RW;
+            b1 = Bs * (c + 1) / RW;
+            if (b0 >= b1) continue;
+        } else {
+            uint64_t c = 0;
+            if (lane == 0) c = atomicAdd(dyn_ctr, 1ull);
+            c = readlane64(c, 0);
+            if (c >= n_dyn) break;
+            b0 = Bs + c * CC_RANGE_DYN_BLOCKS;
+            b1 = b0 + CC_RANGE_DYN_BLOCKS < B ? b0 + CC_RANGE_DYN_BLOCKS : B;
+        }
+        // tile holding block b0: lane tl's tiles, then the first of them whose running count passes b0
+        const uint32_t tl = (uint32_t)__builtin_ctzll(__ballot(cum > b0));
+        uint64_t before = tl ? readlane64(cum, tl - 1) : 0;
+        uint32_t tile = kTpl * tl;
+        bool found = false;
+#pragma unroll
+        for (int j = 0; j < kTpl; j++) {
+            const uint64_t v = readlane64(tb[j], tl);
+            if (!found) {
+                if (before + v > b0) {
+                    found = true;
+                    tile = kTpl * tl + j;
+                } else {
+                    before += v;
+                }
+            }
+        }
+        // range holding block b0: the tile's ranges 64 at a time
+        uint64_t r = n * tile / kRangeTiles;
+        uint64_t rel = b0 - before;
+        uint32_t k0 = 0;
+        for (;;) {
+            const uint64_t ri = r + lane;
+            const RangeDesc d = ranges[ri < n ? ri : n - 1];
+            const uint64_t nbl = (ri < n && d.len) ? range_geo(d.off, d.len).nb : 0u;
+            const uint64_t c = wave_scan_incl(nbl, lane);
+            const uint64_t tot = readlane64(c, 63);
+            if (rel < tot) {
+                const uint32_t h = (uint32_t)__builtin_ctzll(__ballot(c > rel));
+                k0 = (uint32_t)(rel - (h ? readlane64(c, h - 1) : 0));
+                r += h;
+                break;
+            }
+            rel -= tot;
+            r += 64;
+        }
+
+        // window of 64 descriptors (ranges wb + lane), refilled when passed
+        uint64_t wb = r;
+        RangeDesc wd;
+        uint64_t wbits;  // lanes of the window holding a range with blocks
+        auto load_window = [&]() {
+            const uint64_t ri = wb + lane;
+            wd = ranges[ri < n ? ri : n - 1];
+            wbits = __ballot(ri < n && wd.len != 0);
         };
-        // stream position: block k of the range in lane slot h; `real` false
-        // once the wave's blocks are exhausted (then the last block is re-read:
-        // every step issues the same loads, so the vmcnt waits stay exact)
+        load_window();
+        uint64_t left = b1 - b0;  // blocks not yet issued
         struct Pos {
             RangeGeo g;
-            uint32_t h, k;
-            bool real;
+            uint64_t r;              // range index
+            uint32_t k;              // block of the range
+            bool real, first, last;  // issued block / first and last block of the item
+        };
+        auto at = [&](uint64_t ri, uint32_t k) -> Pos {
+            Pos p;
+            const uint32_t h = (uint32_t)(ri - wb);
+            p.g = range_geo(readlane64(wd.off, h), readlane64(wd.len, h));
+            p.r = ri;
+            p.k = k;
+            p.real = true;
+            p.first = false;
+            p.last = --left == 0;
+            return p;
         };
         auto adv = [&](const Pos& p) -> Pos {
-            Pos q = p;
-            if (p.real && p.k + 1 < p.g.nb) {
-                q.k = p.k + 1;
-            } else if (p.real && bits) {
-                q.h = (uint32_t)__builtin_ctzll(bits);
-                bits &= bits - 1;
-                q.g = geo(q.h);
-                q.k = 0;
-            } else {
+            if (!p.real || p.last) {
+                Pos q = p;
                 q.real = false;
+                q.first = q.last = false;
+                return q;
             }
-            return q;
+            if (p.k + 1 < p.g.nb) {
+                Pos q = p;
+                q.k = p.k + 1;
+                q.first = false;
+                q.last = --left == 0;
+                return q;
+            }
+            uint32_t h = (uint32_t)(p.r - wb);
+            uint64_t nx = h < 63 ? (wbits & (~0ull << (h + 1))) : 0ull;
+            while (!nx) {  // window passed (rare): the next 64 descriptors
+                wb += 64;
+                load_window();
+                nx = wbits;
+            }
+            return at(wb + (uint64_t)__builtin_ctzll(nx), 0);
         };
-#if CC_RANGE_DEPTH == 3
-        uint32_t A[16], B[16], Cq[16], Dq[16];
-#else
-        uint32_t A[16], B[16], Cq[16];
-#endif
-        Pos pA;
-        pA.h = (uint32_t)__builtin_ctzll(bits);
-        bits &= bits - 1;
-        pA.g = geo(pA.h);
-        pA.k = 0;
-        pA.real = true;
-        load_range_block(A, buf, pA.g, pA.k, lane);
+        // ring of 4 blocks: three blocks of loads in flight behind the one being folded
+        uint32_t A[17], B4[17], Cq[17], Dq[17];
+        Pos pA = at(r, k0);
+        pA.first = true;
+        load_range_block(A, buf, pA.g, pA.k, lane, xr);
         Pos pB = adv(pA);
-        load_range_block(B, buf, pB.g, pB.k, lane);
-#if CC_RANGE_DEPTH == 3
+        load_range_block(B4, buf, pB.g, pB.k, lane, xr, pB.real);
         Pos pC = adv(pB);
-        load_range_block(Cq, buf, pC.g, pC.k, lane);
+        load_range_block(Cq, buf, pC.g, pC.k, lane, xr, pC.real);
         Pos pD = pC;
-#else
-        Pos pC = pB;
-#endif
         uint32_t s = 0;
-        // consume X (two blocks of loads in flight behind it) after issuing the
-        // loads of position py into Y
-        auto step = [&](uint32_t (&X)[16], const Pos& px, uint32_t (&Y)[16], const Pos& py) {
-            load_range_block(Y, buf, py.g, py.k, lane);
+        bool seg0 = false;  // the current segment began at block 0 of its range
+        auto step = [&](uint32_t (&X)[17], const Pos& px, uint32_t (&Y)[17], const Pos& py) {
+            load_range_block(Y, buf, py.g, py.k, lane, xr, py.real);
             const RangeGeo& gx = px.g;
             const uint32_t kx = px.k;
             mask_range_block(X, gx, kx, lane);
-            // all 16 rows of every block: rows past the range are zeros (loaded
-            // out of range), i.e. a trailing pad the x^(-8t) below removes
-            s = kx == 0 ? X[0] : apply_g_xor(tab, s, X[0], c0, c1);
+            const bool start = kx == 0 || px.first;
+            if (start) seg0 = kx == 0;
+            s = start ? X[0] : apply_g_xor(tab, s, X[0], c0, c1);
 #pragma unroll
             for (int j = 1; j < 16; j++) s = apply_g_xor(tab, s, X[j], c0, c1);
-            if (kx + 1 == gx.nb) {  // range done
+            const bool end = kx + 1 == gx.nb;
+            if (end || px.last) {
+#if CC_RANGE_ABLATE == 2
+                const uint32_t raw_pad = __builtin_amdgcn_readfirstlane(s);
+#else
                 const uint32_t raw_pad = wave_xor(apply_fin(tab, s, cf));
-                const uint32_t t = (uint32_t)(((uint64_t)gx.nb << 12) - gx.lim);  // zero pad in the last block
-                uint32_t v = mulmod_dev(c_xinv.t[t], raw_pad);
-                if (gx.len >= 4) {
-                    v ^= 0xFFFFFFFFu;
-                } else {
-                    v ^= ~mulmod_dev(xpow_wave(gx.len << 3, lane), 0xFFFFFFFFu);
+#endif
+#if CC_RANGE_ABLATE
+                const uint32_t v = raw_pad ^ gx.nb;
+#else
+                // the item ends inside the range: shift over the range's bytes
+                // after this block; a range of < 4 bytes: its K(len) (no folded init)
+                const bool pw_needed = !end || gx.len < 4;
+                const uint32_t pw =
+                    pw_needed ? xpow_wave_small(end ? gx.len << 3 : (gx.lim - ((uint64_t)(kx + 1) << 12)) << 3, lane)
+                              : 0u;
+                // x^(-8t) * raw_pad = XOR over i of bit (31 - i) of raw_pad ? x^(-8t) x^i : 0
+                const uint32_t bit = lane < 32u ? (raw_pad >> (31u - lane)) & 1u : 0u;
+                uint32_t v = end ? wave_xor(bit ? X[16] : 0u) : mulmod_small(pw, raw_pad);
+                if (end) v ^= gx.len >= 4 ? 0xFFFFFFFFu : ~mulmod_small(pw, 0xFFFFFFFFu);
+#endif
+                if (lane == 0) {
+                    if (end && seg0)
+                        out[px.r] = v;
+                    else
+                        atomicXor(out + px.r, v);
                 }
-                const uint64_t oi = readlane64(ix, px.h);
-                if (lane == 0) out[oi] = v;
             }
         };
-#if CC_RANGE_DEPTH == 3
         for (;;) {
             if (!pA.real) break;
             pD = adv(pC);
             step(A, pA, Dq, pD);
             if (!pB.real) break;
             pA = adv(pD);
-            step(B, pB, A, pA);
+            step(B4, pB, A, pA);
             if (!pC.real) break;
             pB = adv(pA);
-            step(Cq, pC, B, pB);
+            step(Cq, pC, B4, pB);
             if (!pD.real) break;
             pC = adv(pB);
             step(Dq, pD, Cq, pC);
         }
-#else
-        for (;;) {
-            if (!pA.real) break;
-            pC = adv(pB);
-            step(A, pA, Cq, pC);
-            if (!pB.real) break;
-            pA = adv(pC);
-            step(B, pB, A, pA);
-            if (!pC.real) break;
-            pB = adv(pA);
-            step(Cq, pC, B, pB);
-        }
-#endif
     }
+#if CC_RANGE_TRACE
+    if (lane == 0 && w < 8192) {
+        g_rtrace[0][w] = t_start;
+        g_rtrace[1][w] = __builtin_amdgcn_s_memrealtime();
+        g_rtrace[2][w] = blockIdx.x;
+        g_rtrace[3][w] = __smid();
+    }
+#endif
 }
 
 // Fast path: per_group = 64*q.  One wave per group, grid-stride over groups;
@@ -1625,110 +1792,19 @@ hipError_t launch_fold(const FoldLaunch& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t upload_xinv(const uint32_t* table) { return hipMemcpyToSymbol(HIP_SYMBOL(c_xinv), table, sizeof(XInv)); }
 
-int range_waves() { return kRangeWaves; }
+#if CC_RANGE_TRACE
+hipError_t range_trace_read(uint64_t* host) { return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rtrace), sizeof(g_rtrace)); }
+#endif
 
-hipError_t launch_range_crc(const unsigned char* buf, const RangeDesc* ranges, const uint32_t* perm, uint64_t n,
-                            const void* image, uint32_t* out, int blocks, hipStream_t s) {
+hipError_t launch_range_flat(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, uint64_t* tile_blocks,
+                             const void* image, uint32_t* out, int blocks, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(range_crc_kernel, dim3(blocks), dim3(64 * kRangeWaves), 0, s, buf, ranges, perm, n,
-                       static_cast<const uint4*>(image), out);
-    return hipGetLastError();
-}
-
-// Decreasing-size order of a range batch: a counting sort of the ranges by
-// 4 KiB-block count (kOrderBins bins, bin 0 = the largest), in two launches.
-// Block b of kOrderBlocks owns ranges [n*b/B, n*(b+1)/B).  Stable: within a
-// bin the ranges keep their batch order, so neighbours in memory stay
-// neighbours in the schedule (an unstable scatter cost ~25 us of locality).
-__device__ __forceinline__ uint32_t range_bin(const RangeDesc& d) {
-    if (d.len == 0) return kOrderBins - 1;
-    const uint32_t nb = range_geo(d.off, d.len).nb;  // >= 1
-    return nb >= kOrderBins ? 0u : kOrderBins - nb;
-}
-
-constexpr uint32_t kOrderThreads = 256;
-__global__ __launch_bounds__(kOrderThreads) void range_hist_kernel(const RangeDesc* __restrict__ ranges, uint64_t n,
-                                                                   uint32_t* __restrict__ hist) {
-    __shared__ uint32_t cnt[kOrderBins];
-    if (threadIdx.x < kOrderBins) cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const uint64_t lo = n * blockIdx.x / kOrderBlocks, hi = n * (blockIdx.x + 1) / kOrderBlocks;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += kOrderThreads) atomicAdd(&cnt[range_bin(ranges[i])], 1u);
-    __syncthreads();
-    if (threadIdx.x < kOrderBins) hist[threadIdx.x * kOrderBlocks + blockIdx.x] = cnt[threadIdx.x];  // bin-major
-}
-
-__global__ __launch_bounds__(kOrderThreads) void range_scatter_kernel(const RangeDesc* __restrict__ ranges, uint64_t n,
-                                                                      const uint32_t* __restrict__ hist,
-                                                                      uint32_t* __restrict__ perm) {
-    constexpr uint32_t kAll = kOrderBins * kOrderBlocks, kPer = kAll / kOrderThreads, kW = kOrderThreads / 64;
-    __shared__ uint32_t part[kOrderThreads], cur[kOrderBins], wcnt[kW][kOrderBins];
-    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    // exclusive scan of the bin-major histogram; keep this block's column
-    uint32_t v[kPer], sum = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++) sum += (v[j] = hist[t * kPer + j]);
-    part[t] = sum;
-    __syncthreads();
-    for (uint32_t d = 1; d < kOrderThreads; d <<= 1) {  // inclusive Hillis-Steele scan of the partials
-        const uint32_t x = t >= d ? part[t - d] : 0u;
-        __syncthreads();
-        part[t] += x;
-        __syncthreads();
-    }
-    uint32_t acc = part[t] - sum;
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++) {
-        const uint32_t e = t * kPer + j;  // = bin * kOrderBlocks + block
-        if (e % kOrderBlocks == blockIdx.x) cur[e / kOrderBlocks] = acc;
-        acc += v[j];
-    }
-    if (t < kOrderBins)
-        for (uint32_t w = 0; w < kW; w++) wcnt[w][t] = 0;
-    __syncthreads();
-    // stable within a bin: chunks of kOrderThreads ranges in index order, a
-    // lane's rank among the earlier lanes of its wave with the same bin
-    const uint64_t lo = n * blockIdx.x / kOrderBlocks, hi = n * (blockIdx.x + 1) / kOrderBlocks;
-    for (uint64_t c = lo; c < hi; c += kOrderThreads) {
-        const uint64_t i = c + t;
-        const bool valid = i < hi;
-        const uint32_t bin = valid ? range_bin(ranges[i]) : 0u;
-        uint64_t same = __ballot(valid);
-#pragma unroll
-        for (uint32_t k = 0; k < 6; k++) {
-            const uint64_t x = __ballot((bin >> k) & 1u);
-            same &= ((bin >> k) & 1u) ? x : ~x;
-        }
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(same >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)same, 0u));
-        if (valid && rank == 0) wcnt[wv][bin] = (uint32_t)__popcll(same);
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = cur[bin] + rank;
-            for (uint32_t w = 0; w < wv; w++) pos += wcnt[w][bin];
-            perm[pos] = (uint32_t)i;
-        }
-        __syncthreads();
-        if (t < kOrderBins) {
-            uint32_t add = 0;
-            for (uint32_t w = 0; w < kW; w++) {
-                add += wcnt[w][t];
-                wcnt[w][t] = 0;
-            }
-            cur[t] += add;
-        }
-        __syncthreads();
-    }
-}
-
-hipError_t launch_range_order(const RangeDesc* ranges, uint64_t n, uint32_t* hist, uint32_t* perm, hipStream_t s) {
-    if (n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(range_hist_kernel, dim3(kOrderBlocks), dim3(kOrderThreads), 0, s, ranges, n, hist);
+    hipLaunchKernelGGL(range_tiles_kernel, dim3(kRangeTiles), dim3(256), 0, s, ranges, n, tile_blocks, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(range_scatter_kernel, dim3(kOrderBlocks), dim3(kOrderThreads), 0, s, ranges, n,
-                       static_cast<const uint32_t*>(hist), perm);
+    hipLaunchKernelGGL(range_flat_kernel, dim3(blocks), dim3(64 * kFlatWaves), 0, s, buf, ranges, n,
+                       tile_blocks, static_cast<const uint4*>(image), out);
     return hipGetLastError();
 }
 

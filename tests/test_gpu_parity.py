@@ -619,10 +619,9 @@ def test_write_log_delta_keeps_latent_corruption(dev, oracle, page_bytes):
 
 
 def test_crc_ranges_large_batch(dev, oracle):
-    """cc_crc_ranges_dev over a batch larger than the grid (several 64-range
-    descriptor batches per wave; >= 8192 ranges, so dealt out in decreasing-size
-    order through launch_range_order): 10,000 ranges of every shape (empty, 1-3
-    bytes, unaligned, multi-block, one 3 MiB giant) == the oracle."""
+    """cc_crc_ranges_dev over a batch larger than the grid: 10,000 ranges of
+    every shape (empty, 1-3 bytes, unaligned, multi-block, one 3 MiB giant cut
+    over several waves' block shares) == the oracle."""
     from curve_amd import crc as C
     rng = np.random.default_rng(4096)
     buf = rng.integers(0, 256, 8 << 20, dtype=np.uint8)
@@ -632,6 +631,37 @@ def test_crc_ranges_large_batch(dev, oracle):
     lens[:40] = [0, 1, 2, 3, 4, 5, 255, 256, 257, 4095, 4096, 4097] + list(range(28))
     lens[5000] = 3 << 20
     offs = rng.integers(0, (8 << 20) - lens - 1)
+    got = u32(C.crc_ranges(d, offs, lens))
+    want = np.array([oracle.crc32c(buf[o:o + l].tobytes()) for o, l in zip(offs, lens)], dtype=np.uint32)
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, (bad[:10], offs[bad[:3]], lens[bad[:3]])
+
+
+@pytest.mark.parametrize("shape", ["tiny_many", "giants"])
+def test_crc_ranges_flat_schedule(dev, oracle, shape):
+    """Large batches through cc_crc_ranges_dev's flat block schedule (every
+    wave an equal share of the batch's 4 KiB blocks, in 2 pieces).
+    tiny_many: 300,000 ranges of 0-300 bytes, so a wave's piece spans more than
+    one 64-descriptor window, plus empty ranges at tile edges.  giants: ranges of
+    up to 24 MiB cut into segments by many wave pieces (segments that start and
+    end inside one range: shift-and-XOR combine) next to 0-3 byte ranges."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(len(shape) * 7)
+    size = 32 << 20
+    buf = rng.integers(0, 256, size, dtype=np.uint8)
+    d = to_dev(buf, dev)
+    if shape == "tiny_many":
+        n = 300000
+        lens = rng.integers(0, 301, n)
+        lens[::97] = 0
+        lens[:3] = [0, 0, 0]
+        lens[-3:] = [0, 1, 0]
+    else:
+        n = 9000
+        lens = rng.integers(0, 4, n)
+        lens[::500] = rng.integers(1 << 20, 24 << 20, lens[::500].size)
+        lens[-1] = 24 << 20
+    offs = rng.integers(0, size - lens)
     got = u32(C.crc_ranges(d, offs, lens))
     want = np.array([oracle.crc32c(buf[o:o + l].tobytes()) for o, l in zip(offs, lens)], dtype=np.uint32)
     bad = np.flatnonzero(got != want)
