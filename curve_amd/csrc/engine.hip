@@ -238,6 +238,30 @@ void geometry_for(const DevCtx* c, uint64_t n_pages, PageLaunch* a) {
     a->tile_shift = ts;
 }
 
+#ifndef CC_PAGE_DYN_DIV
+#define CC_PAGE_DYN_DIV 8  // 1/8 of a large launch's tiles form the dynamic tail (0: static only)
+#endif
+// Page kernel launch with the dynamic tail (kernels.hip, page_crc_kernel) when
+// the batch is large: a stream-ordered, zeroed 8-byte chunk counter per call.
+hipError_t launch_page_tail(const DevCtx* c, PageLaunch& a, bool verify, hipStream_t s) {
+    geometry_for(c, a.n_pages, &a);
+    const uint32_t m = a.words_per_lane;
+    const uint64_t tiles = (a.n_pages + (1ull << a.tile_shift) - 1) >> a.tile_shift;
+    const uint64_t waves = (uint64_t)a.blocks * kWavesPerBlock;
+    if (!CC_PAGE_DYN_DIV || m > 32 || (m & (m - 1)) || tiles < waves * 8)
+        return verify ? launch_page_verify(a, s) : launch_page_crc(a, s);
+    unsigned long long* ctr = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(*ctr), s);
+    if (e != hipSuccess) return e;
+    if ((e = hipMemsetAsync(ctr, 0, sizeof(*ctr), s)) == hipSuccess) {
+        a.dyn_ctr = ctr;
+        a.static_tiles = tiles - tiles / CC_PAGE_DYN_DIV;
+        e = verify ? launch_page_verify(a, s) : launch_page_crc(a, s);
+    }
+    const hipError_t f = hipFreeAsync(ctr, s);
+    return e != hipSuccess ? e : f;
+}
+
 int staging_init(DevCtx* c) {
     Staging& st = c->st;
     if (st.ready) return CC_OK;
@@ -386,8 +410,8 @@ int cc_hbm_read_probe_dev(const void* d_buf, uint64_t bytes, uint32_t* d_sink, v
     return map_err(launch_read_probe(d_buf, bytes, d_sink, 2 * c->cus, static_cast<hipStream_t>(stream)));
 }
 
-#if CC_RANGE_TRACE
-int cc_debug_range_trace(uint64_t* host) { return map_err(range_trace_read(host)); }
+#if CC_WAVE_TRACE
+int cc_debug_wave_trace(uint64_t* host) { return map_err(wave_trace_read(host)); }
 #endif
 
 int cc_device_count(void) {
@@ -439,8 +463,7 @@ int cc_page_crc_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes, 
     a.image = c->image;
     a.kconst = kconst_for(page_bytes);
     a.out = d_out;
-    geometry_for(c.get(), n_pages, &a);
-    return map_err(launch_page_crc(a, static_cast<hipStream_t>(stream)));
+    return map_err(launch_page_tail(c.get(), a, false, static_cast<hipStream_t>(stream)));
 }
 
 int cc_page_verify_list_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes, const uint32_t* d_expected,
@@ -464,8 +487,7 @@ int cc_page_verify_list_dev(const void* d_pages, uint64_t n_pages, uint32_t page
     a.sink.first_bad = reinterpret_cast<unsigned long long*>(d_first_bad);
     a.sink.list = max_bad_pages ? reinterpret_cast<unsigned long long*>(d_bad_pages) : nullptr;
     a.sink.max_list = max_bad_pages;
-    geometry_for(c.get(), n_pages, &a);
-    return map_err(launch_page_verify(a, static_cast<hipStream_t>(stream)));
+    return map_err(launch_page_tail(c.get(), a, true, static_cast<hipStream_t>(stream)));
 }
 
 int cc_page_verify_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes, const uint32_t* d_expected,

@@ -42,6 +42,10 @@ struct PageLaunch {
     VerifySink sink;          // verify only
     int blocks;
     uint32_t tile_shift;      // 2^tile_shift consecutive pages per wave tile (0..6)
+    // dynamic tail: null = every tile in the strided static walk; else tiles
+    // [static_tiles, all) are handed out through this zeroed counter
+    unsigned long long* dyn_ctr;
+    uint64_t static_tiles;
 };
 
 hipError_t launch_page_crc(const PageLaunch& a, hipStream_t s);
@@ -165,7 +169,7 @@ hipError_t launch_read_verify(const ReadVerifyLaunch& a, hipStream_t s);
 // tile_blocks: kRangeTiles + 1 uint64 of stream-ordered scratch (the last: the
 // dynamic-tail chunk counter).
 constexpr uint32_t kRangeTiles = 1024;
-hipError_t range_trace_read(uint64_t* host);  // CC_RANGE_TRACE builds only: [4][8192]
+hipError_t wave_trace_read(uint64_t* host);  // CC_WAVE_TRACE builds only: [4][8192]
 hipError_t launch_range_flat(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, uint64_t* tile_blocks,
                              const void* image, uint32_t* out, int blocks, hipStream_t s);
 // x^(-8t) mod P for t = 0..kXinvEntries-1 (undoing the zero pad after a range in its last 4 KiB block)

@@ -46,6 +46,21 @@ constexpr uint32_t kPolyDev = 0x82F63B78u;
 #define CC_ABLATE 0  // diagnostic builds only (wrong CRCs): 1 no G lookups, 2 no final map, 3 no loads
 #endif
 
+#ifndef CC_WAVE_TRACE
+#define CC_WAVE_TRACE 0  // diagnostic builds: per-wave start/end wall clock of the page and range kernels
+#endif
+#if CC_WAVE_TRACE
+__device__ uint64_t g_rtrace[4][8192];  // start, end, block, cu
+__device__ __forceinline__ void wave_trace(uint64_t w, uint64_t t_start) {
+    if ((threadIdx.x & 63u) == 0 && w < 8192) {
+        g_rtrace[0][w] = t_start;
+        g_rtrace[1][w] = __builtin_amdgcn_s_memrealtime();
+        g_rtrace[2][w] = blockIdx.x;
+        g_rtrace[3][w] = __smid();
+    }
+}
+#endif
+
 __device__ __forceinline__ uint32_t lds_u32(const uint32_t* tab, uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + byte_addr);
 }
@@ -81,6 +96,12 @@ __device__ __forceinline__ uint32_t apply_fin(const uint32_t* tab, uint32_t s, u
         r ^= lds_u32(tab, ((v << 8) | cf) + 4096u * n);
     }
     return r;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+    // readlane returns int: go through uint32_t so the low half is not sign-extended
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
 }
 
 // XOR over the 64 lanes, result wave-uniform (SGPR).
@@ -247,64 +268,94 @@ __device__ __forceinline__ void chains(const uint32_t* tab, const uint32_t (&w)[
 // Wave w walks tiles w, w+W, w+2W, ... (W = waves in the grid) of 2^ts pages,
 // P pages per step.  CC_PREFETCH+1 register buffers rotate so CC_PREFETCH
 // steps' loads are in flight while the current step is hashed.  Loads are
-// unconditional (index clamped to the last page) so hipcc counts vmcnt exactly.
+// unconditional (index clamped to the item's last page) so hipcc counts vmcnt
+// exactly.
+// Dynamic tail (dyn_ctr != null): the strided walk covers tiles [0, static_tiles)
+// only; the remaining tiles are handed out CC_PAGE_DYN_TILES at a time through
+// the atomic counter *dyn_ctr (zeroed by the caller) to whichever waves finish
+// first.  Per-wave rates differ by XCD (a kernel trace shows odd XCDs ~10 %
+// slower on the same work), so a purely static split waits for the slowest.
+#ifndef CC_PAGE_DYN_PAGES
+#define CC_PAGE_DYN_PAGES 64  // pages per dynamic chunk (A/B: 64 beats 128)
+#endif
 template <int M, int MODE>
 __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
     const uint32_t* __restrict__ pages, uint64_t n_pages, const uint4* __restrict__ image,
     uint32_t kconst, uint32_t* __restrict__ out, const uint32_t* __restrict__ expected, VerifySink vs,
-    uint32_t tshift) {
+    uint32_t tshift, unsigned long long* __restrict__ dyn_ctr, uint64_t static_tiles) {
     __shared__ uint32_t tab[kLdsBytes / 4];
     fill_lds(tab, image);
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    Walk W;
-    W.tshift = tshift;
-    W.tmask = (1u << tshift) - 1u;
-    W.wstride = ((uint64_t)gridDim.x * kWavesPerBlock) << tshift;
-    W.wfirst = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) << tshift;
-    if (W.wfirst >= n_pages) return;
-    const uint64_t last = n_pages - 1;
+#if CC_WAVE_TRACE
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t c0 = lane << 2 & 0x7Cu;
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
     const uint32_t* base = pages + lane;
     constexpr int D = CC_PREFETCH;
     constexpr int P = (M <= 16) ? CC_PAIR : 1;  // register budget: P*(D+1)*M data VGPRs
-    uint32_t acc = 0;
-
-    // ring of D+1 register buffers; after full unrolling every index is a
-    // compile-time constant, so the ring lives in VGPRs (no scratch)
-    uint32_t ring[D + 1][P][M];
+    // item 0: the strided static walk over tiles [0, static_tiles); then dynamic chunks
+    Walk W;
+    W.tshift = tshift;
+    W.tmask = (1u << tshift) - 1u;
+    W.wstride = ((uint64_t)gridDim.x * kWavesPerBlock) << tshift;
+    W.wfirst = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) << tshift;
+    uint64_t lim = dyn_ctr ? (static_tiles << tshift < n_pages ? static_tiles << tshift : n_pages) : n_pages;
+#pragma unroll 1
+    for (;;) {
+        if (W.wfirst < lim) {
+            const uint64_t last = lim - 1;
+            uint32_t acc = 0;
+            // ring of D+1 register buffers; after full unrolling every index is a
+            // compile-time constant, so the ring lives in VGPRs (no scratch)
+            uint32_t ring[D + 1][P][M];
 #pragma unroll
-    for (int st = 0; st < D; st++) load_pages<M, P>(ring[st], base, W, (uint64_t)st * P, last);
-    // Every step's loads are unconditional (clamped) and termination is tested
-    // once per ring revolution: path-insensitive waitcnt dataflow then sees the
-    // same D stages outstanding on every edge into a step and keeps each wait
-    // at its exact count (a per-step early exit made hipcc over-wait a stage).
-    for (uint64_t k = 0;; k += (uint64_t)(D + 1) * P) {
+            for (int st = 0; st < D; st++) load_pages<M, P>(ring[st], base, W, (uint64_t)st * P, last);
+            // Every step's loads are unconditional (clamped) and termination is tested
+            // once per ring revolution: path-insensitive waitcnt dataflow then sees the
+            // same D stages outstanding on every edge into a step and keeps each wait
+            // at its exact count (a per-step early exit made hipcc over-wait a stage).
+            for (uint64_t k = 0;; k += (uint64_t)(D + 1) * P) {
 #pragma unroll
-        for (int st = 0; st <= D; st++) {
-            const uint64_t kk = k + (uint64_t)st * P;
-            load_pages<M, P>(ring[(st + D) % (D + 1)], base, W, kk + (uint64_t)D * P, last);
-            uint32_t s[P];
-            chains<M, P>(tab, ring[st], c0, c1, s);
+                for (int st = 0; st <= D; st++) {
+                    const uint64_t kk = k + (uint64_t)st * P;
+                    load_pages<M, P>(ring[(st + D) % (D + 1)], base, W, kk + (uint64_t)D * P, last);
+                    uint32_t s[P];
+                    chains<M, P>(tab, ring[st], c0, c1, s);
 #pragma unroll
-            for (int q = 0; q < P; q++) {
-                const uint64_t kq = kk + q;
-                const uint64_t pc = W.page(kq);
-                if (pc < n_pages) {
-                    const uint64_t pn = W.page(kq + 1);
-                    const uint32_t crc = wave_xor(apply_fin(tab, s[q], cf)) ^ kconst;
-                    const uint32_t slot = (uint32_t)(kq & W.tmask);
-                    acc = lane == slot ? crc : acc;
-                    if (slot == W.tmask || pn >= n_pages)
-                        flush_tile<MODE>(acc, pc - slot, slot + 1u, lane, out, expected, vs);
+                    for (int q = 0; q < P; q++) {
+                        const uint64_t kq = kk + q;
+                        const uint64_t pc = W.page(kq);
+                        if (pc < lim) {
+                            const uint64_t pn = W.page(kq + 1);
+                            const uint32_t crc = wave_xor(apply_fin(tab, s[q], cf)) ^ kconst;
+                            const uint32_t slot = (uint32_t)(kq & W.tmask);
+                            acc = lane == slot ? crc : acc;
+                            if (slot == W.tmask || pn >= lim)
+                                flush_tile<MODE>(acc, pc - slot, slot + 1u, lane, out, expected, vs);
+                        }
+                    }
                 }
+                if (W.page(k + (uint64_t)(D + 1) * P) >= lim) break;
             }
         }
-        if (W.page(k + (uint64_t)(D + 1) * P) >= n_pages) break;
+        if (!dyn_ctr) break;
+        // next dynamic chunk: CC_PAGE_DYN_PAGES consecutive pages
+        unsigned long long c = 0;
+        if (lane == 0) c = atomicAdd(dyn_ctr, 1ull);
+        c = readlane64(c, 0);
+        const uint64_t p0 = (static_tiles << tshift) + c * CC_PAGE_DYN_PAGES;
+        if (p0 >= n_pages) break;
+        W.wfirst = p0;
+        W.wstride = 1ull << tshift;  // consecutive tiles: page(k) = p0 + k
+        lim = p0 + CC_PAGE_DYN_PAGES < n_pages ? p0 + CC_PAGE_DYN_PAGES : n_pages;
     }
+#if CC_WAVE_TRACE
+    wave_trace((uint64_t)blockIdx.x * kWavesPerBlock + wave, t_start);
+#endif
 }
 
 // Any M (page_bytes = 256*M): no register prefetch, dynamic chain length.
@@ -353,11 +404,6 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
 constexpr uint32_t kBufOOB = 0x80000000u;   // offset past num_records: load 0 / store dropped
 constexpr uint32_t kBufFlags = 0x00020000u;  // buffer resource dword 3 for gfx9-family (CDNA)
 
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
-    // readlane returns int: go through uint32_t so the low half is not sign-extended
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
-           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
-}
 
 // ---------------------------------------------------------------------------
 // GF(2) helpers for the fold / shift kernels (tiny volume: 4 B per page).
@@ -545,12 +591,6 @@ __device__ __forceinline__ uint64_t wave_scan_incl(uint64_t v, uint32_t lane) {
 #ifndef CC_RANGE_ABLATE
 #define CC_RANGE_ABLATE 0  // timing ablations (wrong CRCs): 1 no per-range multiply, 2 no per-range finish
 #endif
-#ifndef CC_RANGE_TRACE
-#define CC_RANGE_TRACE 0  // diagnostic builds: per-wave start/end wall clock of range_flat_kernel
-#endif
-#if CC_RANGE_TRACE
-__device__ uint64_t g_rtrace[4][8192];  // start, end, block, cu
-#endif
 #ifndef CC_FLAT_WAVES
 #define CC_FLAT_WAVES 8  // waves per CU of the flat range kernel (A/B on WAL sizes: 8 beats 12 by ~4 %, 16 by ~10 %)
 #endif
@@ -580,7 +620,7 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsig
     const uint32_t cf = kFinBase + (lane << 2);
     const uint64_t W = (uint64_t)gridDim.x * kFlatWaves;
     const uint64_t w = (uint64_t)blockIdx.x * kFlatWaves + wave;
-#if CC_RANGE_TRACE
+#if CC_WAVE_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
@@ -768,13 +808,8 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsig
             step(Dq, pD, Cq, pC);
         }
     }
-#if CC_RANGE_TRACE
-    if (lane == 0 && w < 8192) {
-        g_rtrace[0][w] = t_start;
-        g_rtrace[1][w] = __builtin_amdgcn_s_memrealtime();
-        g_rtrace[2][w] = blockIdx.x;
-        g_rtrace[3][w] = __smid();
-    }
+#if CC_WAVE_TRACE
+    wave_trace(w, t_start);
 #endif
 }
 
@@ -1727,7 +1762,7 @@ hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
 #define CC_CASE(MM)                                                                                     \
     case MM:                                                                                            \
         hipLaunchKernelGGL((page_crc_kernel<MM, MODE>), grid, block, 0, s, a.pages, a.n_pages, img,    \
-                           a.kconst, a.out, a.expected, a.sink, a.tile_shift);                         \
+                           a.kconst, a.out, a.expected, a.sink, a.tile_shift, a.dyn_ctr, a.static_tiles); \
         break;
     switch (a.words_per_lane) {
         CC_CASE(1)
@@ -1749,7 +1784,9 @@ hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
 hipError_t launch_page_crc(const PageLaunch& a, hipStream_t s) { return launch_page<0>(a, s); }
 
 // Read-only probe (diagnostic): dwordx4 nt loads, 4 in flight per lane, the
-// fastest pure-read shape found by scripts/hbm_probe.hip.
+// fastest pure-read shape found by scripts/hbm_probe.hip.  Static strided
+// schedule: it waits for the slowest XCD as the page kernel did before its
+// dynamic tail (a dynamic-tail version of this probe measured slower, 6.7 TB/s).
 __global__ __launch_bounds__(1024) void read_probe_kernel(const uint4* __restrict__ p, uint64_t n16,
                                                           uint32_t* __restrict__ sink) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -1793,8 +1830,8 @@ hipError_t launch_fold(const FoldLaunch& a, hipStream_t s) {
 }
 
 
-#if CC_RANGE_TRACE
-hipError_t range_trace_read(uint64_t* host) { return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rtrace), sizeof(g_rtrace)); }
+#if CC_WAVE_TRACE
+hipError_t wave_trace_read(uint64_t* host) { return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rtrace), sizeof(g_rtrace)); }
 #endif
 
 hipError_t launch_range_flat(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, uint64_t* tile_blocks,
