@@ -987,7 +987,7 @@ uint64_t cc_verify_reads_work_bytes(uint64_t n_reads) {
     if (n_reads == 0 || n_reads >= (1ull << 31)) return 0;
     const size_t temp = scan_temp_bytes(n_reads);
     if (!temp) return 0;
-    return 2 * align256(n_reads * 8) + align256(temp);
+    return 2 * align256(n_reads * 8) + align256(temp) + 256;  // + the dynamic-tail counter
 }
 
 int cc_verify_reads_dev(const void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const cc_range* d_reads,
@@ -1013,6 +1013,8 @@ int cc_verify_reads_dev(const void* d_pool, uint64_t pool_bytes, uint32_t page_b
     a.counts = reinterpret_cast<uint64_t*>(w);
     a.start = reinterpret_cast<uint64_t*>(w + align256(n_reads * 8));
     void* temp = w + 2 * align256(n_reads * 8);
+    const size_t temp_bytes = align256(scan_temp_bytes(n_reads));
+    a.dyn_ctr = reinterpret_cast<unsigned long long*>(w + 2 * align256(n_reads * 8) + temp_bytes);
     a.page_crcs = d_page_crcs;
     a.bad_per_read = d_bad_per_read;
     a.bad_total = reinterpret_cast<unsigned long long*>(d_bad_total);
@@ -1021,8 +1023,7 @@ int cc_verify_reads_dev(const void* d_pool, uint64_t pool_bytes, uint32_t page_b
     a.blocks = c->cus;  // every wave takes an equal share of the (device-computed) page slots
     hipError_t e;
     if ((e = launch_read_counts(a, s)) != hipSuccess) return map_err(e);
-    if ((e = exclusive_scan_u64(temp, work_bytes - 2 * align256(n_reads * 8), a.counts, a.start, n_reads, s)) !=
-        hipSuccess)
+    if ((e = exclusive_scan_u64(temp, temp_bytes, a.counts, a.start, n_reads, s)) != hipSuccess)
         return map_err(e);
     return map_err(launch_read_verify(a, s));
 }

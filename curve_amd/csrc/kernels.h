@@ -152,6 +152,7 @@ struct ReadVerifyLaunch {
     const uint32_t* page_crcs;  // stored CRC per pool page
     uint32_t* bad_per_read;     // [n_reads] += mismatching pages; UINT32_MAX for a read beyond the pool
     unsigned long long* bad_total;
+    unsigned long long* dyn_ctr;  // dynamic-tail chunk counter (zeroed by the count kernel)
     const void* image;
     uint32_t kconst;
     int blocks;

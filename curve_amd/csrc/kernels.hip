@@ -1606,6 +1606,7 @@ __global__ CC_LOG_ATTR void log_hot_kernel(LogLaunch a) {
 // Pages each read touches (a read past the pool touches none and is marked).
 __global__ void read_counts_kernel(ReadVerifyLaunch a) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *a.dyn_ctr = 0;  // read_verify_kernel's dynamic-tail counter
     if (i >= a.n_reads) return;
     const RangeDesc r = a.reads[i];
     uint64_t c = 0;
@@ -1634,6 +1635,12 @@ __global__ void read_counts_kernel(ReadVerifyLaunch a) {
 #define CC_RV_WAVES 8  // waves per CU of the verify-on-read kernel
 #endif
 constexpr int kRvWaves = CC_RV_WAVES;
+#ifndef CC_RV_DYN_DIV
+#define CC_RV_DYN_DIV 16  // 1/16 of the slots form the dynamic tail (A/B: 2-3 % over none; 1/8, 1/32 less)
+#endif
+#ifndef CC_RV_DYN_SLOTS
+#define CC_RV_DYN_SLOTS 32  // slots (pages) per dynamic chunk (64: -1 %, 128: -5 %, 256: -18 % -- too coarse)
+#endif
 template <int M>
 __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLaunch a) {
     __shared__ uint32_t tab[kLdsBytes / 4];
@@ -1670,57 +1677,71 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
         }
         return lo;
     };
-    const uint64_t rb = lower_bound(T * w / W), re = lower_bound(T * (w + 1) / W);
     auto stored_crc = [&](uint64_t g) { return a.page_crcs[g + vz]; };
-    for (uint64_t base = rb; base < re; base += 64) {
-        const uint64_t ri = base + lane;
-        const bool valid = ri < re;
-        const RangeDesc r = a.reads[(valid ? ri : base) + vz];
-        const uint32_t cnt = valid ? (uint32_t)a.counts[ri] : 0u;  // 0 also for reads past the pool
-        const uint64_t p0 = r.off / a.page_bytes;
-        uint32_t cum = cnt;  // inclusive prefix sum over the lanes
+    // static shares of the first Ts slots, then dynamic chunks of CC_RV_DYN_SLOTS
+    // slots (the page kernel's tail: the XCDs run at different rates)
+    const uint64_t Ts = T - T / CC_RV_DYN_DIV;
+    uint64_t lo_slot = Ts * w / W, hi_slot = Ts * (w + 1) / W;
+#pragma unroll 1
+    for (;;) {
+        const uint64_t rb = lower_bound(lo_slot), re = lower_bound(hi_slot);
+        for (uint64_t base = rb; base < re; base += 64) {
+            const uint64_t ri = base + lane;
+            const bool valid = ri < re;
+            const RangeDesc r = a.reads[(valid ? ri : base) + vz];
+            const uint32_t cnt = valid ? (uint32_t)a.counts[ri] : 0u;  // 0 also for reads past the pool
+            const uint64_t p0 = r.off / a.page_bytes;
+            uint32_t cum = cnt;  // inclusive prefix sum over the lanes
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(cum, d, 64);
-            if (lane >= (uint32_t)d) cum += o;
-        }
-        const uint32_t P = __builtin_amdgcn_readlane(cum, 63);
-        if (P == 0) continue;
-        auto page_at = [&](uint32_t k, uint32_t& owner) -> uint64_t {
-            owner = (uint32_t)__builtin_ctzll(__ballot(cum > k));
-            const uint32_t before = owner ? (uint32_t)__builtin_amdgcn_readlane(cum, owner - 1) : 0u;
-            const uint64_t first = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(p0 >> 32), owner) << 32) |
-                                   (uint32_t)__builtin_amdgcn_readlane((uint32_t)p0, owner);
-            return first + (k - before);
-        };
-        uint32_t A[M], B[M], Cq[M];
-        uint32_t oA, oB, oC;
-        uint64_t gA = page_at(0, oA), gB = page_at(P > 1 ? 1 : 0, oB), gC = gB;
-        oC = oB;
-        uint32_t sA = stored_crc(gA), sB = stored_crc(gB), sC = sB;
-        load_page<M>(A, pages + gA * (64u * M));
-        load_page<M>(B, pages + gB * (64u * M));
-        // hash X (page k: stored CRC sx, owner lane ox); page k+2's loads go into Y
-        auto step = [&](uint32_t (&X)[M], uint32_t sx, uint32_t ox, uint32_t k, uint32_t (&Y)[M], uint64_t& gy,
-                        uint32_t& sy, uint32_t& oy) {
-            const bool more = k + 1 < P;
-            gy = page_at(k + 2 < P ? k + 2 : P - 1, oy);  // clamped: same loads every step
-            sy = stored_crc(gy);
-            load_page<M>(Y, pages + gy * (64u * M));
-            const uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
-            if (crc != sx && lane == 0) {
-                atomicAdd(a.bad_per_read + base + ox, 1u);
-                atomicAdd(a.bad_total, 1ull);
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(cum, d, 64);
+                if (lane >= (uint32_t)d) cum += o;
             }
-            return more;
-        };
-        for (uint32_t k = 0;; k += 3) {
-            if (!step(A, sA, oA, k, Cq, gC, sC, oC)) break;
-            if (!step(B, sB, oB, k + 1, A, gA, sA, oA)) break;
-            if (!step(Cq, sC, oC, k + 2, B, gB, sB, oB)) break;
+            const uint32_t P = __builtin_amdgcn_readlane(cum, 63);
+            if (P == 0) continue;
+            auto page_at = [&](uint32_t k, uint32_t& owner) -> uint64_t {
+                owner = (uint32_t)__builtin_ctzll(__ballot(cum > k));
+                const uint32_t before = owner ? (uint32_t)__builtin_amdgcn_readlane(cum, owner - 1) : 0u;
+                const uint64_t first = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(p0 >> 32), owner) << 32) |
+                                       (uint32_t)__builtin_amdgcn_readlane((uint32_t)p0, owner);
+                return first + (k - before);
+            };
+            uint32_t A[M], B[M], Cq[M];
+            uint32_t oA, oB, oC;
+            uint64_t gA = page_at(0, oA), gB = page_at(P > 1 ? 1 : 0, oB), gC = gB;
+            oC = oB;
+            uint32_t sA = stored_crc(gA), sB = stored_crc(gB), sC = sB;
+            load_page<M>(A, pages + gA * (64u * M));
+            load_page<M>(B, pages + gB * (64u * M));
+            // hash X (page k: stored CRC sx, owner lane ox); page k+2's loads go into Y
+            auto step = [&](uint32_t (&X)[M], uint32_t sx, uint32_t ox, uint32_t k, uint32_t (&Y)[M], uint64_t& gy,
+                            uint32_t& sy, uint32_t& oy) {
+                const bool more = k + 1 < P;
+                gy = page_at(k + 2 < P ? k + 2 : P - 1, oy);  // clamped: same loads every step
+                sy = stored_crc(gy);
+                load_page<M>(Y, pages + gy * (64u * M));
+                const uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
+                if (crc != sx && lane == 0) {
+                    atomicAdd(a.bad_per_read + base + ox, 1u);
+                    atomicAdd(a.bad_total, 1ull);
+                }
+                return more;
+            };
+            for (uint32_t k = 0;; k += 3) {
+                if (!step(A, sA, oA, k, Cq, gC, sC, oC)) break;
+                if (!step(B, sB, oB, k + 1, A, gA, sA, oA)) break;
+                if (!step(Cq, sC, oC, k + 2, B, gB, sB, oB)) break;
+            }
         }
+        unsigned long long c = 0;
+        if (lane == 0) c = atomicAdd(a.dyn_ctr, 1ull);
+        c = readlane64(c, 0);
+        lo_slot = Ts + c * CC_RV_DYN_SLOTS;
+        if (lo_slot >= T) break;
+        hi_slot = lo_slot + CC_RV_DYN_SLOTS < T ? lo_slot + CC_RV_DYN_SLOTS : T;
     }
 }
+
 
 __global__ void combine_kernel(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t m,
                                uint64_t n, uint32_t* __restrict__ out) {
