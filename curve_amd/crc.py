@@ -597,16 +597,18 @@ def apply_updates_batched(pool, page_crcs, src, dst_off, src_off, lens, page_byt
     n_pages = _nbytes(pool) // page_bytes
     max_len = int(lens.max()) if lens.size else 1
     need = int(lib().cc_update_work_bytes(n_pages, dst_off.size, max_len, page_bytes))
-    key = (pool.device, need)
+    # scratch per (device, stream), as apply_log: calls on different streams may overlap
+    key = _stream_key(pool.device, stream)
     work = _work_cache.get(key)
-    if work is None:
-        work = torch.empty(need, dtype=torch.uint8, device=pool.device)
-        _work_cache.clear()
+    if work is None or work.numel() < need:
+        with _on_stream(stream):
+            work = torch.empty(need, dtype=torch.uint8, device=pool.device)
         _work_cache[key] = work
     rec_in = np.zeros(dst_off.size, dtype=_update_dtype())
     rec_in["dst"], rec_in["src"], rec_in["len"] = dst_off, src_off, lens
     rec, ends, nb = plan_updates(rec_in)
-    d_upd = torch.from_numpy(rec.view(np.uint8)).to(pool.device, non_blocking=False)
+    with _on_stream(stream):
+        d_upd = torch.from_numpy(rec.view(np.uint8)).to(pool.device, non_blocking=False)
     with torch.cuda.device(pool.device):
         check(lib().cc_apply_updates_dev(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, _dev_ptr(src, "src"),
                                          _dev_ptr(d_upd, "updates"), rec.size,
@@ -614,8 +616,9 @@ def apply_updates_batched(pool, page_crcs, src, dst_off, src_off, lens, page_byt
                                          _dev_ptr(page_crcs, "page_crcs"), _dev_ptr(work, "work"), work.numel(),
                                          _stream_handle(stream)),
               "cc_apply_updates_dev")
-    if stream is not None:  # temp descriptor buffer must outlive the kernels on `stream`
+    if stream is not None:  # buffers must outlive the kernels on `stream`
         d_upd.record_stream(stream)
+        work.record_stream(stream)
     return nb
 
 

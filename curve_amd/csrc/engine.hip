@@ -893,11 +893,11 @@ inline uint32_t log_slots(uint32_t max_len, uint32_t page_bytes) { return (max_l
 }  // namespace
 
 namespace {
-// Work layout of the write log: counters (head_count, hot_count) | page table |
-// next links | head slots | hot slots.  Only the counters and the table are
+// Work layout of the write log: counter (head_count) | page table | next links |
+// head slots.  Only the counter and the table are
 // cleared per call (one memset).
 struct LogWork {
-    uint64_t n_pieces, table_entries, table_off, next_off, heads_off, hot_off, bytes;
+    uint64_t n_pieces, table_entries, table_off, next_off, heads_off, bytes;
 };
 bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork* w) {
     if (!log_page_ok(page_bytes) || max_len == 0 || n_updates == 0) return false;
@@ -909,8 +909,7 @@ bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork
     w->table_off = 256;
     w->next_off = w->table_off + te * 8;
     w->heads_off = w->next_off + align256(w->n_pieces * 4);
-    w->hot_off = w->heads_off + align256(w->n_pieces * 4);
-    w->bytes = w->hot_off + align256(w->n_pieces * 4);
+    w->bytes = w->heads_off + align256(w->n_pieces * 4);
     return true;
 }
 }  // namespace
@@ -948,12 +947,10 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
     a.slots = log_slots(max_len, page_bytes);
     a.n_pieces = lw.n_pieces;
     a.head_count = reinterpret_cast<uint32_t*>(w);
-    a.hot_count = reinterpret_cast<uint32_t*>(w + 4);
     a.table = reinterpret_cast<uint64_t*>(w + lw.table_off);
     a.table_mask = (uint32_t)(lw.table_entries - 1);
     a.next = reinterpret_cast<uint32_t*>(w + lw.next_off);
     a.heads = reinterpret_cast<uint32_t*>(w + lw.heads_off);
-    a.hot = reinterpret_cast<uint32_t*>(w + lw.hot_off);
     a.image = c->image;
     a.kconst = kconst_for(page_bytes);
     a.page_crcs = d_page_crcs;
@@ -964,8 +961,7 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
     hipError_t e;
     if ((e = hipMemsetAsync(w, 0, lw.next_off, s)) != hipSuccess) return map_err(e);  // counters + table
     if ((e = launch_log_insert(a, s)) != hipSuccess) return map_err(e);
-    if ((e = launch_log_pages(a, s)) != hipSuccess) return map_err(e);
-    return map_err(launch_log_hot(a, s));
+    return map_err(launch_log_pages(a, s));
 }
 }  // namespace
 

@@ -95,7 +95,7 @@ hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s);
 // page groups them (each entry heads a linked list of the page's pieces) with
 // no sort; one wave per touched page (balanced over the grid) then applies its
 // pieces in log order in registers, stores the changed rows and rehashes it.
-// Pages with more than 64 pieces are finished by a log-replay kernel.
+// A page with more than 64 pieces is finished by its wave replaying the log.
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
 #ifndef CC_LOG_WAVES
 #define CC_LOG_WAVES 12  // waves per CU of the write-log page kernel (A/B: 12 beats 8 by ~6 %; 16 forces <= 128 VGPRs and spills in delta mode)
@@ -121,8 +121,6 @@ struct LogLaunch {
     uint32_t* next;             // [n_pieces] next piece of the same page (kNoPiece = end)
     uint32_t* heads;            // [n_pieces] table slots of the touched pages (unordered)
     uint32_t* head_count;       // number of them
-    uint32_t* hot;              // [n_pieces] table slots of pages with > 64 pieces
-    uint32_t* hot_count;
     const void* image;
     uint32_t kconst;
     uint32_t* page_crcs;        // out; in delta mode also in (the CRCs before the batch)
@@ -131,7 +129,6 @@ struct LogLaunch {
 };
 hipError_t launch_log_insert(const LogLaunch& a, hipStream_t s);
 hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s);
-hipError_t launch_log_hot(const LogLaunch& a, hipStream_t s);
 
 struct RangeDesc {
     uint64_t off, len;

@@ -1333,14 +1333,10 @@ __device__ __forceinline__ void merge_edges(uint32_t (&w)[M], uint32_t& dirty, c
 // software-pipelines them: while page k's pieces are merged, stored and
 // hashed, page k+1's data AND the source bytes of its piece are in flight.  A
 // page with several pieces (overlapping / neighbouring writes: rare) walks its
-// list, ranks the pieces by update index and applies them in log order; a
-// page with more than 64 goes to the hot list (log_hot_kernel).  Every page is
-// owned by exactly one wave: no write races, no flags, no atomics on the data.
-#if CC_LOG_WAVES == 16
-#define CC_LOG_ATTR __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 4)))
-#else
-#define CC_LOG_ATTR __launch_bounds__(64 * CC_LOG_WAVES)
-#endif
+// list, ranks the pieces by update index and applies them in log order; for
+// a page with more than 64 (a log hammering it) the wave replays the whole log
+// in place.  Every page is owned by exactly one wave: no write races, no
+// flags, no atomics on the data.
 // Delta mode (cc_apply_log_delta_dev): the stored CRC of each touched page is
 // taken as the CRC of its bytes before the batch and updated through
 // linearity, V(new) = V(old) ^ raw0(old ^ new) (equal lengths: the init and
@@ -1373,6 +1369,9 @@ __global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(Log
     const uint32_t pb = a.page_bytes;
     const uint32_t H = *a.head_count;
     const uint32_t W = gridDim.x * WV;
+    // static shares only: a dynamic tail (the last 1/8 or 1/16 of the heads in
+    // chunks of 4-16 through one atomic counter, as the page kernel does) measured
+    // 7-19 % slower here (0.177-0.197 vs 0.165 ms a batch)
     for (uint32_t base = blockIdx.x * WV + wave; base < H; base += 64u * W) {
         // lane k <- head base + k*W (clamped loads: no branches around them)
         const uint64_t ih = (uint64_t)base + (uint64_t)lane * W;
@@ -1456,7 +1455,6 @@ __global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(Log
 #pragma unroll
                 for (int j = 0; j < M; j++) O[j] = X[j];
             }
-            bool hot = false;
             if ((singles >> hh) & 1ull) {
                 if constexpr (kRowSel) {
                     merge_edges<M>(X, dirty, SX, px, lane);
@@ -1470,9 +1468,24 @@ __global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(Log
                     cnt++;
                     q = a.next[q];
                 }
-                if (q != kNoPiece) {  // > 64 pieces: the hot-page kernel replays the log for it
-                    hot = true;
-                    if (lane == 0) a.hot[atomicAdd(a.hot_count, 1u)] = __builtin_amdgcn_readlane(hslot, hh);
+                if (q != kNoPiece) {  // > 64 pieces (a log hammering this page: rare)
+                    // its own wave replays the whole log for this page, 64 records per round
+                    // (a ballot of the records touching it), in log order
+                    for (uint64_t b = 0; b < a.n_updates; b += 64) {
+                        const uint64_t i = b + lane;
+                        const UpdateDesc dr = a.upd[i < a.n_updates ? i : b];
+                        const bool ok = i < a.n_updates && dr.len >= 1 && dr.len <= a.max_len &&
+                                        dr.dst < a.pool_bytes && dr.len <= a.pool_bytes - dr.dst &&
+                                        dr.dst < pbase + pb && dr.dst + dr.len > pbase;
+                        for (uint64_t m = __ballot(ok); m; m &= m - 1) {
+                            const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                            const Piece pq = piece_in_page(pbase, pb, readlane64(dr.dst, l), readlane64(dr.src, l),
+                                                           __builtin_amdgcn_readlane(dr.len, l), a.src);
+                            PieceSrc<M> T;
+                            fetch_piece<M>(T, pq, lane);
+                            merge_piece<M>(X, dirty, T, pq, lane);
+                        }
+                    }
                 } else {
                     const uint32_t idx = lane < cnt ? mine / a.slots : 0xFFFFFFFFu;
                     uint32_t rank = lane < cnt ? 0u : 0xFFFFu;
@@ -1517,7 +1530,7 @@ __global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(Log
             } else {
                 crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
             }
-            if (lane == 0 && !hot) {
+            if (lane == 0) {
 #if CC_LOG_CRC_NT
                 __builtin_nontemporal_store(crc, a.page_crcs + pg);
 #else
@@ -1537,66 +1550,6 @@ __global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(Log
             if (!step(A, S0, pA, pgA, h, ocA, B, S1, pB, pgB, ocB)) break;
             if (!step(B, S1, pB, pgB, h + 1, ocB, A, S0, pA, pgA, ocA)) break;
         }
-    }
-}
-
-// Pages with more than 64 pieces (a write log hammering a few pages): one wave
-// per hot page replays the whole log in order, 64 records per round trip (a
-// ballot of the records that touch the page), merging their pieces into the
-// page in registers -- log order by construction, any number of pieces.  A
-// grid with no hot page returns before filling its LDS.
-template <int M, bool Delta>
-__global__ CC_LOG_ATTR void log_hot_kernel(LogLaunch a) {
-    __shared__ uint32_t tab[kLdsBytes / 4];
-    const uint32_t HC = *a.hot_count;
-    if ((uint64_t)blockIdx.x * kLogWaves >= HC) return;  // uniform per block: no hot page for it
-    fill_lds<64 * kLogWaves>(tab, static_cast<const uint4*>(a.image));
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t c0 = lane << 2 & 0x7Cu;
-    const uint32_t c1 = c0 | 0x10000u;
-    const uint32_t cf = kFinBase + (lane << 2);
-    const uint32_t* pages = reinterpret_cast<const uint32_t*>(a.pool) + lane;
-    const uint32_t pb = a.page_bytes;
-    const uint32_t W = gridDim.x * kLogWaves;
-    for (uint32_t h = blockIdx.x * kLogWaves + wave; h < HC; h += W) {
-        const unsigned long long ent = reinterpret_cast<const unsigned long long*>(a.table)[a.hot[h]];
-        const uint32_t pg = (uint32_t)(ent >> 32) - 1u;
-        const uint64_t pbase = (uint64_t)pg * pb;
-        uint32_t X[M], O[Delta ? M : 1];
-        load_page<M>(X, pages + (uint64_t)pg * (64u * M));
-        if constexpr (Delta) {
-#pragma unroll
-            for (int j = 0; j < M; j++) O[j] = X[j];
-        }
-        uint32_t dirty = 0;
-        PieceSrc<M> S;
-        for (uint64_t b = 0; b < a.n_updates; b += 64) {
-            const uint64_t i = b + lane;
-            const UpdateDesc d = a.upd[i < a.n_updates ? i : b];
-            const bool ok = i < a.n_updates && d.len >= 1 && d.len <= a.max_len && d.dst < a.pool_bytes &&
-                            d.len <= a.pool_bytes - d.dst && d.dst < pbase + pb && d.dst + d.len > pbase;
-            for (uint64_t m = __ballot(ok); m; m &= m - 1) {  // this round's writes to the page, in log order
-                const uint32_t l = (uint32_t)__builtin_ctzll(m);
-                const Piece pq = piece_in_page(pbase, pb, readlane64(d.dst, l), readlane64(d.src, l),
-                                               __builtin_amdgcn_readlane(d.len, l), a.src);
-                fetch_piece<M>(S, pq, lane);
-                merge_piece<M>(X, dirty, S, pq, lane);
-            }
-        }
-        const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(a.pool + pbase, 0, 256u * M, kBufFlags);
-#pragma unroll
-        for (int j = 0; j < M; j++)
-            __builtin_amdgcn_raw_buffer_store_b32(X[j], rp, (((dirty >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j, 0, 0);
-        uint32_t crc;
-        if constexpr (Delta) {
-#pragma unroll
-            for (int j = 0; j < M; j++) O[j] ^= X[j];
-            crc = wave_xor(apply_fin(tab, chain<M>(tab, O, c0, c1), cf)) ^ a.page_crcs[pg];
-        } else {
-            crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
-        }
-        if (lane == 0) a.page_crcs[pg] = crc;
     }
 }
 
@@ -1927,28 +1880,6 @@ hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s) {
         default: return hipErrorInvalidValue;
     }
 #undef CC_GCASE
-    return hipGetLastError();
-}
-
-hipError_t launch_log_hot(const LogLaunch& a, hipStream_t s) {
-    if (a.n_pieces == 0) return hipSuccess;
-#define CC_HCASE(MM)                                                                                      \
-    case MM:                                                                                              \
-        if (a.delta)                                                                                      \
-            hipLaunchKernelGGL((log_hot_kernel<MM, true>), dim3(a.blocks), dim3(64 * kLogWaves), 0, s, a);  \
-        else                                                                                              \
-            hipLaunchKernelGGL((log_hot_kernel<MM, false>), dim3(a.blocks), dim3(64 * kLogWaves), 0, s, a); \
-        break;
-    switch (a.page_bytes / kWaveBytes) {
-        CC_HCASE(1)
-        CC_HCASE(2)
-        CC_HCASE(4)
-        CC_HCASE(8)
-        CC_HCASE(16)
-        CC_HCASE(32)
-        default: return hipErrorInvalidValue;
-    }
-#undef CC_HCASE
     return hipGetLastError();
 }
 

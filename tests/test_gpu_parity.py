@@ -543,21 +543,29 @@ def test_partial_writes(dev, oracle, page_bytes, n_upd, overlap, mode):
     assert (u32(crcs) == oracle.page_crcs(want, page_bytes, threads=8)).all()
 
 
+@pytest.mark.parametrize("spread", [0, 4000])
 @pytest.mark.parametrize("delta", [False, True])
-def test_write_log_hot_pages_and_contract(dev, oracle, delta):
-    """cc_apply_log_dev with every write piled on a few pages (long per-page
-    piece lists that cross sort tiles, applied strictly in log order), plus
+def test_write_log_hot_pages_and_contract(dev, oracle, delta, spread):
+    """cc_apply_log_dev with 700 writes piled on a few pages (piece lists longer
+    than 64: the owning wave replays the log, strictly in log order), plus
     entries that break the contract (len 0, len > max_len, beyond the pool):
-    those are skipped whole, everything else lands as in-order application."""
+    those are skipped whole, everything else lands as in-order application.
+    spread > 0 interleaves that many writes scattered over the pool, so the
+    hot pages sit among thousands of touched pages (static shares and the
+    dynamic tail of the page kernel)."""
     from curve_amd import crc as C
-    rng = np.random.default_rng(77)
-    pool_bytes, pb = 1 << 20, 4096
+    rng = np.random.default_rng(77 + spread)
+    pool_bytes, pb = 16 << 20 if spread else 1 << 20, 4096
     host = rng.integers(0, 256, pool_bytes, dtype=np.uint8)
     d_pool = to_dev(host, dev)
     crcs = C.page_crc(d_pool, pb)
-    n = 700
+    n = 700 + spread
     lens = rng.integers(1, 3000, n).astype(np.uint32)
     dst = (rng.integers(0, 3 * pb, n) + 5 * pb).astype(np.uint64)  # pages 5..8
+    if spread:
+        far = rng.permutation(n)[:spread]
+        far = far[~np.isin(far, [3, 100, 101, 650])]
+        dst[far] = rng.integers(16 * pb, pool_bytes - 4096, far.size).astype(np.uint64)
     src_off = rng.integers(0, 1 << 16, n).astype(np.uint64)
     src_data = rng.integers(0, 256, (1 << 16) + 4096, dtype=np.uint8)
     bad = [3, 100, 101, 650]
