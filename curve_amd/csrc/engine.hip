@@ -959,7 +959,9 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
     const uint64_t blocks = (lw.n_pieces + kLogWaves - 1) / kLogWaves;
     a.blocks = (int)(blocks < (uint64_t)c->cus ? (blocks ? blocks : 1) : (uint64_t)c->cus);
     hipError_t e;
-    if ((e = hipMemsetAsync(w, 0, lw.next_off, s)) != hipSuccess) return map_err(e);  // counters + table
+    // (memset + insert + pages as ONE cooperative launch with two grid barriers
+    // measured 0.221 vs 0.162 ms a batch: not kept)
+    if ((e = hipMemsetAsync(w, 0, lw.next_off, s)) != hipSuccess) return map_err(e);  // counter + table
     if ((e = launch_log_insert(a, s)) != hipSuccess) return map_err(e);
     return map_err(launch_log_pages(a, s));
 }

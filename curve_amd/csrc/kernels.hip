@@ -1040,10 +1040,11 @@ __device__ __forceinline__ uint32_t page_hash(uint32_t page, uint32_t mask) {
 #endif
 constexpr uint32_t kInsertThreads = CC_INSERT_THREADS;  // one head-list atomic per 1024 pieces (a per-wave atomic on the one
                                           // counter serialised 2048 waves: 26 of the kernel's 31 us)
-__global__ __launch_bounds__(kInsertThreads) void log_insert_kernel(LogLaunch a) {
-    __shared__ uint32_t wcount[kInsertThreads / 64], bbase;
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+// Piece t of the log (t >= n_pieces: none) into the table.  Every thread of
+// the block calls it; `wcount` = LDS scratch of blockDim/64 + 1 words, free
+// again after the block's next __syncthreads.
+__device__ __forceinline__ void insert_piece(const LogLaunch& a, uint64_t t, uint32_t* wcount) {
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
     bool fresh = false;
     uint32_t slot = 0;
     if (t < a.n_pieces) {
@@ -1089,13 +1090,18 @@ __global__ __launch_bounds__(kInsertThreads) void log_insert_kernel(LogLaunch a)
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t tot = 0;
-        for (uint32_t w = 0; w < blockDim.x / 64; w++) tot += wcount[w];
-        bbase = tot ? atomicAdd(a.head_count, tot) : 0u;
+        for (uint32_t w = 0; w < nw; w++) tot += wcount[w];
+        wcount[nw] = tot ? atomicAdd(a.head_count, tot) : 0u;
     }
     __syncthreads();
-    uint32_t base = bbase;
+    uint32_t base = wcount[nw];
     for (uint32_t w = 0; w < wv; w++) base += wcount[w];
     if (fresh) a.heads[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = slot;
+}
+
+__global__ __launch_bounds__(kInsertThreads) void log_insert_kernel(LogLaunch a) {
+    __shared__ uint32_t wcount[kInsertThreads / 64 + 1];
+    insert_piece(a, (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, wcount);
 }
 
 // The bytes of one update that fall inside one page, page-relative: page bytes
@@ -1356,9 +1362,8 @@ __device__ __forceinline__ void load_rows(uint32_t (&w)[M], const unsigned char*
 }
 
 template <int M, bool Delta>
-__global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(LogLaunch a) {
+__device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab) {
     constexpr int WV = log_waves(M, Delta);
-    __shared__ uint32_t tab[kLdsBytes / 4];
     fill_lds<64 * WV>(tab, static_cast<const uint4*>(a.image));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1551,6 +1556,12 @@ __global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(Log
             if (!step(B, S1, pB, pgB, h + 1, ocB, A, S0, pA, pgA, ocA)) break;
         }
     }
+}
+
+template <int M, bool Delta>
+__global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(LogLaunch a) {
+    __shared__ uint32_t tab[kLdsBytes / 4];
+    log_pages_body<M, Delta>(a, tab);
 }
 
 // ---------------------------------------------------------------------------
