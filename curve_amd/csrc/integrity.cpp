@@ -206,14 +206,22 @@ int cc_pcrc_load(const char* table_path, cc_pcrc_header* h, uint32_t* page_crcs,
     return cc_pcrc_decode(buf.data(), buf.size(), h, page_crcs, max_pages);
 }
 
-int cc_pcrc_store(const char* chunk_path, uint32_t meta_bytes, const char* table_path, const uint32_t* page_crcs,
-                  uint32_t n_pages, uint32_t page_bytes) {
+}  // extern "C"
+
+namespace {
+// The store behind cc_pcrc_store.  With `expect`, the chunk's identity read here
+// must still be the one the CRCs were computed under (else CC_ESTALE, nothing
+// written): a write landing between a job's read and its table refresh must not
+// get a table of the bytes before it.
+int store_table(const char* chunk_path, uint32_t meta_bytes, const char* table_path, const uint32_t* page_crcs,
+                uint32_t n_pages, uint32_t page_bytes, const ChunkId* expect) {
     if (!chunk_path || !table_path || (n_pages && !page_crcs) || page_bytes == 0 || meta_bytes == 0)
         return CC_EINVAL;
     ChunkId id;
     int rc = chunk_identity(chunk_path, meta_bytes, &id);
     if (rc) return rc;
     if (id.size != (uint64_t)meta_bytes + (uint64_t)n_pages * page_bytes) return CC_EINVAL;
+    if (expect && (id.sn != expect->sn || id.mtime != expect->mtime || id.size != expect->size)) return CC_ESTALE;
     cc_pcrc_header h = {page_bytes, n_pages, id.sn, id.mtime, id.size};
     std::vector<unsigned char> buf(cc_pcrc_encoded_bytes(n_pages));
     if ((rc = cc_pcrc_encode(&h, page_crcs, buf.data(), buf.size()))) return rc;
@@ -228,6 +236,14 @@ int cc_pcrc_store(const char* chunk_path, uint32_t meta_bytes, const char* table
     if (!rc && rename(tmp.c_str(), table_path) != 0) rc = -errno;
     if (rc) unlink(tmp.c_str());
     return rc;
+}
+}  // namespace
+
+extern "C" {
+
+int cc_pcrc_store(const char* chunk_path, uint32_t meta_bytes, const char* table_path, const uint32_t* page_crcs,
+                  uint32_t n_pages, uint32_t page_bytes) {
+    return store_table(chunk_path, meta_bytes, table_path, page_crcs, n_pages, page_bytes, nullptr);
 }
 
 int cc_integrity_check(const char* const* chunk_paths, const char* const* table_paths, uint64_t n,
@@ -277,7 +293,13 @@ int cc_integrity_check(const char* const* chunk_paths, const char* const* table_
                 r.table_state = CC_TABLE_STALE;
                 return;
             }
-            const int s = cc_pcrc_store(chunk_paths[i], o->meta_bytes, table_paths[i], got, n_pages, o->page_bytes);
+            // the chunk must still be the one read in step 2 (identity before)
+            const int s =
+                store_table(chunk_paths[i], o->meta_bytes, table_paths[i], got, n_pages, o->page_bytes, &before[i]);
+            if (s == CC_ESTALE) {
+                r.table_state = CC_TABLE_STALE;
+                return;
+            }
             if (s) r.status = s;
             r.table_state = state_ok;
         };

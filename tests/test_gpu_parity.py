@@ -306,6 +306,38 @@ def test_large_pool_properties(dev, oracle):
     assert int(cnt[0]) == 0
 
 
+@pytest.mark.parametrize("page_bytes", [256, 1024])
+def test_page_kernel_dynamic_tail(dev, oracle, page_bytes):
+    """Launches large enough for the page kernel's dynamic tail (>= 8 tiles per
+    wave: the last 1/8 of the tiles go out in 64-page chunks through an atomic
+    counter): every CRC equals the oracle's, and verify-with-list finds exactly
+    the corrupted pages, in the static shares, at the static/dynamic boundary,
+    inside the tail and at the very last page (1M + 77 pages: a partial chunk)."""
+    from curve_amd import crc as C
+    n_pages = (1 << 20) + 77
+    d = torch.empty(n_pages * page_bytes, dtype=torch.uint8, device=dev).random_(0, 256)
+    pc = C.page_crc(d, page_bytes)
+    host = d.cpu().numpy()
+    assert (u32(pc) == oracle.page_crcs(host, page_bytes, threads=16)).all()
+    tiles = (n_pages + 63) // 64
+    first_dyn = (tiles - tiles // 8) * 64
+    bad = sorted({0, 12345, first_dyn - 1, first_dyn, first_dyn + 64 * 37 + 5, n_pages - 64, n_pages - 1})
+    for p in bad:
+        d[p * page_bytes + 3] ^= 0x80
+    cnt, lst = C.page_verify_list(d, pc, page_bytes, max_bad=64)
+    torch.cuda.synchronize()
+    assert int(cnt[0]) == len(bad) and int(cnt[1]) == bad[0]
+    assert sorted(int(x) for x in lst[:len(bad)].cpu()) == bad
+    # repeated launches on one stream: the per-call tail counter starts from 0 each time
+    for _ in range(3):
+        again = C.page_crc(d, page_bytes)
+    torch.cuda.synchronize()
+    for p in bad:
+        d[p * page_bytes + 3] ^= 0x80
+    assert torch.equal(C.page_crc(d, page_bytes), pc)
+    assert not torch.equal(again, pc)
+
+
 def test_write_log_full_size_config3(dev, oracle):
     """BASELINE config 3 at full size: a 16 GiB pool (1024 chunks), 65,536 random
     512 B-4 KiB writes in one log (unaligned, straddling, some overlapping).
