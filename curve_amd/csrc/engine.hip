@@ -242,20 +242,27 @@ void geometry_for(const DevCtx* c, uint64_t n_pages, PageLaunch* a) {
 #define CC_PAGE_DYN_DIV 8  // 1/8 of a large launch's tiles form the dynamic tail (0: static only)
 #endif
 // Page kernel launch with the dynamic tail (kernels.hip, page_crc_kernel) when
-// the batch is large: a stream-ordered, zeroed 8-byte chunk counter per call.
-hipError_t launch_page_tail(const DevCtx* c, PageLaunch& a, bool verify, hipStream_t s) {
+// the batch is large: a stream-ordered, zeroed 8-byte chunk counter per call --
+// `zeroed_ctr` if the caller has one (zeroed on the stream before this launch:
+// cc_pool_scan_dev has the metapage launch clear it), else allocated + memset.
+hipError_t launch_page_tail(const DevCtx* c, PageLaunch& a, bool verify, hipStream_t s,
+                            unsigned long long* zeroed_ctr = nullptr) {
     geometry_for(c, a.n_pages, &a);
     const uint32_t m = a.words_per_lane;
     const uint64_t tiles = (a.n_pages + (1ull << a.tile_shift) - 1) >> a.tile_shift;
     const uint64_t waves = (uint64_t)a.blocks * kWavesPerBlock;
     if (!CC_PAGE_DYN_DIV || m > 32 || (m & (m - 1)) || tiles < waves * 8)
         return verify ? launch_page_verify(a, s) : launch_page_crc(a, s);
+    a.static_tiles = tiles - tiles / CC_PAGE_DYN_DIV;
+    if (zeroed_ctr) {
+        a.dyn_ctr = zeroed_ctr;
+        return verify ? launch_page_verify(a, s) : launch_page_crc(a, s);
+    }
     unsigned long long* ctr = nullptr;
     hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(*ctr), s);
     if (e != hipSuccess) return e;
     if ((e = hipMemsetAsync(ctr, 0, sizeof(*ctr), s)) == hipSuccess) {
         a.dyn_ctr = ctr;
-        a.static_tiles = tiles - tiles / CC_PAGE_DYN_DIV;
         e = verify ? launch_page_verify(a, s) : launch_page_crc(a, s);
     }
     const hipError_t f = hipFreeAsync(ctr, s);
@@ -465,6 +472,55 @@ int cc_page_crc_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes, 
     a.out = d_out;
     return map_err(launch_page_tail(c.get(), a, false, static_cast<hipStream_t>(stream)));
 }
+
+extern "C++" {  // engine-internal (C++ linkage), used by pool.hip
+namespace cc {
+// cc_pool_scan_dev's page launches (pool.hip): the metapage launch (static
+// walk) clears the data launch's tail counter and the digest partials as its
+// block 0 starts, so the scan step needs no memset launches; the data launch
+// then runs with that counter.
+int pool_page_launches(const void* d_data, uint64_t n_data_pages, uint32_t page_bytes, uint32_t* d_page_crcs,
+                       const void* d_meta, uint64_t n_meta, uint32_t meta_bytes, uint32_t* d_meta_crcs,
+                       uint32_t* d_digest, uint64_t digest_words, hipStream_t s, void* ev_begin, void* ev_end) {
+    if (!page_size_ok(page_bytes) || !page_size_ok(meta_bytes)) return CC_EINVAL;
+    if (!d_data || !d_page_crcs || !d_meta || !d_meta_crcs || ((uintptr_t)d_data & 3u) || ((uintptr_t)d_meta & 3u))
+        return CC_EINVAL;
+    CtxRef c;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    unsigned long long* ctr = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(*ctr), s);
+    if (e != hipSuccess) return map_err(e);
+    PageLaunch m = {};
+    m.pages = static_cast<const uint32_t*>(d_meta);
+    m.n_pages = n_meta;
+    m.words_per_lane = meta_bytes / kWaveBytes;
+    m.image = c->image;
+    m.kconst = kconst_for(meta_bytes);
+    m.out = d_meta_crcs;
+    m.zero[0] = reinterpret_cast<uint32_t*>(ctr);
+    m.zero_words[0] = sizeof(*ctr) / 4;
+    m.zero[1] = d_digest;
+    m.zero_words[1] = d_digest ? digest_words : 0;
+    geometry_for(c.get(), n_meta, &m);  // static walk (a tail would need a counter of its own)
+    e = launch_page_crc(m, s);
+    if (e == hipSuccess && ev_begin) e = hipEventRecord(static_cast<hipEvent_t>(ev_begin), s);
+    if (e == hipSuccess) {
+        PageLaunch a = {};
+        a.pages = static_cast<const uint32_t*>(d_data);
+        a.n_pages = n_data_pages;
+        a.words_per_lane = page_bytes / kWaveBytes;
+        a.image = c->image;
+        a.kconst = kconst_for(page_bytes);
+        a.out = d_page_crcs;
+        e = launch_page_tail(c.get(), a, false, s, ctr);
+    }
+    if (e == hipSuccess && ev_end) e = hipEventRecord(static_cast<hipEvent_t>(ev_end), s);
+    const hipError_t f = hipFreeAsync(ctr, s);
+    return map_err(e != hipSuccess ? e : f);
+}
+}  // namespace cc
+}  // extern "C++"
 
 int cc_page_verify_list_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes, const uint32_t* d_expected,
                             uint64_t* d_bad_count, uint64_t* d_first_bad, uint64_t* d_bad_pages,

@@ -46,9 +46,18 @@ struct PageLaunch {
     // [static_tiles, all) are handed out through this zeroed counter
     unsigned long long* dyn_ctr;
     uint64_t static_tiles;
+    // block 0 zeroes these word ranges before its walk (stream-ordered for the
+    // kernels after it: the next launch's tail counter, a digest to XOR into)
+    uint32_t* zero[2];
+    uint64_t zero_words[2];
 };
 
 hipError_t launch_page_crc(const PageLaunch& a, hipStream_t s);
+// engine.hip, for cc_pool_scan_dev: metapage launch (clears the data launch's
+// tail counter and the digest) then the data launch, bracketed by the events
+int pool_page_launches(const void* d_data, uint64_t n_data_pages, uint32_t page_bytes, uint32_t* d_page_crcs,
+                       const void* d_meta, uint64_t n_meta, uint32_t meta_bytes, uint32_t* d_meta_crcs,
+                       uint32_t* d_digest, uint64_t digest_words, hipStream_t s, void* ev_begin, void* ev_end);
 hipError_t launch_read_probe(const void* buf, uint64_t bytes, uint32_t* sink, int blocks, hipStream_t s);
 hipError_t launch_page_verify(const PageLaunch& a, hipStream_t s);
 

@@ -278,12 +278,22 @@ __device__ __forceinline__ void chains(const uint32_t* tab, const uint32_t (&w)[
 #ifndef CC_PAGE_DYN_PAGES
 #define CC_PAGE_DYN_PAGES 64  // pages per dynamic chunk (A/B: 64 beats 128)
 #endif
+struct ZeroRanges {
+    uint32_t* p[2];
+    uint64_t n[2];
+    __device__ __forceinline__ void clear() const {
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+            for (uint64_t i = threadIdx.x; i < n[k]; i += blockDim.x) p[k][i] = 0u;
+    }
+};
 template <int M, int MODE>
 __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
     const uint32_t* __restrict__ pages, uint64_t n_pages, const uint4* __restrict__ image,
     uint32_t kconst, uint32_t* __restrict__ out, const uint32_t* __restrict__ expected, VerifySink vs,
-    uint32_t tshift, unsigned long long* __restrict__ dyn_ctr, uint64_t static_tiles) {
+    uint32_t tshift, unsigned long long* __restrict__ dyn_ctr, uint64_t static_tiles, ZeroRanges zr) {
     __shared__ uint32_t tab[kLdsBytes / 4];
+    if (blockIdx.x == 0) zr.clear();
     fill_lds(tab, image);
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -362,8 +372,10 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
 template <int MODE>
 __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
     const uint32_t* __restrict__ pages, uint64_t n_pages, uint32_t M, const uint4* __restrict__ image,
-    uint32_t kconst, uint32_t* __restrict__ out, const uint32_t* __restrict__ expected, VerifySink vs) {
+    uint32_t kconst, uint32_t* __restrict__ out, const uint32_t* __restrict__ expected, VerifySink vs,
+    ZeroRanges zr) {
     __shared__ uint32_t tab[kLdsBytes / 4];
+    if (blockIdx.x == 0) zr.clear();
     fill_lds(tab, image);
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -1744,10 +1756,11 @@ template <int MODE>
 hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
     const dim3 grid(a.blocks), block(kBlockThreads);
     const uint4* img = static_cast<const uint4*>(a.image);
+    const ZeroRanges zr = {{a.zero[0], a.zero[1]}, {a.zero[0] ? a.zero_words[0] : 0, a.zero[1] ? a.zero_words[1] : 0}};
 #define CC_CASE(MM)                                                                                     \
     case MM:                                                                                            \
         hipLaunchKernelGGL((page_crc_kernel<MM, MODE>), grid, block, 0, s, a.pages, a.n_pages, img,    \
-                           a.kconst, a.out, a.expected, a.sink, a.tile_shift, a.dyn_ctr, a.static_tiles); \
+                           a.kconst, a.out, a.expected, a.sink, a.tile_shift, a.dyn_ctr, a.static_tiles, zr); \
         break;
     switch (a.words_per_lane) {
         CC_CASE(1)
@@ -1758,7 +1771,7 @@ hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
         CC_CASE(32)
         default:
             hipLaunchKernelGGL((page_crc_kernel_dyn<MODE>), grid, block, 0, s, a.pages, a.n_pages,
-                               a.words_per_lane, img, a.kconst, a.out, a.expected, a.sink);
+                               a.words_per_lane, img, a.kconst, a.out, a.expected, a.sink, zr);
     }
 #undef CC_CASE
     return hipGetLastError();

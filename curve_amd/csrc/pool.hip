@@ -137,15 +137,13 @@ int cc_pool_scan_dev(const cc_pool_shard* p, cc_comm* comm, void* stream) {
         if (dig && (e = hipMemsetAsync(p->d_digest, 0, p->n_groups * 4, s)) != hipSuccess) return map_hip(e);
         return comm ? cc_digest_allreduce_dev(comm, p->d_digest, p->n_groups, stream) : CC_OK;
     }
-    if (p->ev_pages_begin && (e = hipEventRecord(static_cast<hipEvent_t>(p->ev_pages_begin), s)) != hipSuccess)
-        return map_hip(e);
-    // the hot kernel: every 4 KiB data page of the shard
-    if ((rc = cc_page_crc_dev(p->d_data, pages, p->page_bytes, p->d_page_crcs, stream))) return rc;
-    if (p->ev_pages_end && (e = hipEventRecord(static_cast<hipEvent_t>(p->ev_pages_end), s)) != hipSuccess)
-        return map_hip(e);
-    // readMetaPage ops: one "page" of meta_bytes per chunk
-    if ((rc = cc_page_crc_dev(p->d_meta, p->n_chunks, p->meta_bytes, p->d_meta_crcs, stream))) return rc;
-    if (dig && (e = hipMemsetAsync(p->d_digest, 0, p->n_groups * 4, s)) != hipSuccess) return map_hip(e);
+    // readMetaPage ops (one "page" of meta_bytes per chunk; this launch also
+    // zeroes the digest partials and the next launch's tail counter), then the
+    // hot kernel over every data page of the shard, bracketed by the caller's events
+    if ((rc = cc::pool_page_launches(p->d_data, pages, p->page_bytes, p->d_page_crcs, p->d_meta, p->n_chunks,
+                                     p->meta_bytes, p->d_meta_crcs, dig ? p->d_digest : nullptr,
+                                     dig ? p->n_groups : 0, s, p->ev_pages_begin, p->ev_pages_end)))
+        return rc;
     // slices + file CRCs + digest partials in one launch
     if ((rc = cc_scan_epilogue_dev(p->d_page_crcs, p->d_meta_crcs, p->n_chunks, p->chunk_bytes / p->page_bytes,
                                    p->page_bytes, p->slice_bytes / p->page_bytes, p->d_slice_crcs, p->d_file_crcs,
