@@ -883,11 +883,31 @@ __global__ __launch_bounds__(256) void epilogue_kernel(EpilogueLaunch a) {
     const uint32_t* chk = a.mtab + 9 * 1024;
     for (uint64_t c = blockIdx.x; c < a.n_chunks; c += gridDim.x) {
         const uint32_t* p = a.page_crcs + c * a.pages_per_chunk + (uint64_t)t * a.q;
-        uint32_t s = p[0];
-        for (uint32_t i = 1; i < a.q; i++) {
+        auto horner = [&](uint32_t s, uint32_t w) {
             const uint32_t u = __builtin_amdgcn_bitop3_b32(mt[s & 255u], mt[256 + ((s >> 8) & 255u)],
                                                            mt[512 + ((s >> 16) & 255u)], 0x96);
-            s = __builtin_amdgcn_bitop3_b32(u, mt[768 + (s >> 24)], p[i], 0x96);
+            return __builtin_amdgcn_bitop3_b32(u, mt[768 + (s >> 24)], w, 0x96);
+        };
+        uint32_t s;
+        if (a.q == 16 && ((uintptr_t)a.page_crcs & 15u) == 0) {
+            // 16 MiB chunks of 4 KiB pages: the thread's 64 B in four 16-byte loads, all in flight
+            uint4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = reinterpret_cast<const uint4*>(p)[k];
+            s = v[0].x;
+            s = horner(s, v[0].y);
+            s = horner(s, v[0].z);
+            s = horner(s, v[0].w);
+#pragma unroll
+            for (int k = 1; k < 4; k++) {
+                s = horner(s, v[k].x);
+                s = horner(s, v[k].y);
+                s = horner(s, v[k].z);
+                s = horner(s, v[k].w);
+            }
+        } else {
+            s = p[0];
+            for (uint32_t i = 1; i < a.q; i++) s = horner(s, p[i]);
         }
         if (a.slice_shift == 0) a.slice_crcs[c * 256 + t] = s;  // one thread per slice
         // levels 0..5 inside the wave
