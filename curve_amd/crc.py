@@ -175,7 +175,8 @@ def page_crc(pages, page_bytes: int = PAGE_SIZE, out=None, stream=None):
         raise CurveCrcError(_lib.CC_EINVAL, "pages size is not a multiple of page_bytes")
     n = nb // page_bytes
     if out is None:
-        out = torch.empty(n, dtype=torch.int32, device=pages.device)
+        with _on_stream(stream):  # created on the stream the kernel writes it on
+            out = torch.empty(n, dtype=torch.int32, device=pages.device)
     elif out.numel() < n or out.element_size() != 4:
         raise CurveCrcError(_lib.CC_EINVAL, "out too small or not 32-bit")
     with torch.cuda.device(pages.device):
@@ -244,7 +245,8 @@ def fold(crcs, per_group: int, unit_bytes: int, out=None, stream=None):
         raise CurveCrcError(_lib.CC_EINVAL, "crcs count is not a multiple of per_group")
     g = n // per_group
     if out is None:
-        out = torch.empty(g, dtype=torch.int32, device=crcs.device)
+        with _on_stream(stream):  # created on the stream the kernel writes it on
+            out = torch.empty(g, dtype=torch.int32, device=crcs.device)
     with torch.cuda.device(crcs.device):
         check(lib().cc_fold_dev(_dev_ptr(crcs, "crcs"), g, per_group, int(unit_bytes), _dev_ptr(out, "out"),
                                 _stream_handle(stream)), "cc_fold_dev")
@@ -258,7 +260,8 @@ def shift_dev(crcs, shift_bytes, out=None, stream=None):
     if shift_bytes.numel() != n or shift_bytes.element_size() != 8:
         raise CurveCrcError(_lib.CC_EINVAL, "shift_bytes must be int64, one per crc")
     if out is None:
-        out = torch.empty(n, dtype=torch.int32, device=crcs.device)
+        with _on_stream(stream):  # created on the stream the kernel writes it on
+            out = torch.empty(n, dtype=torch.int32, device=crcs.device)
     with torch.cuda.device(crcs.device):
         check(lib().cc_shift_dev(_dev_ptr(crcs, "crcs"), _dev_ptr(shift_bytes, "shift_bytes"), n,
                                  _dev_ptr(out, "out"), _stream_handle(stream)), "cc_shift_dev")
@@ -294,7 +297,8 @@ def xpow8(nbytes, out=None, stream=None):
     """x^(8*n) mod P per element (cc_xpow8_dev): the shift multipliers of a static layout."""
     torch = _torch()
     if out is None:
-        out = torch.empty(nbytes.numel(), dtype=torch.int32, device=nbytes.device)
+        with _on_stream(stream):  # created on the stream the kernel writes it on
+            out = torch.empty(nbytes.numel(), dtype=torch.int32, device=nbytes.device)
     with torch.cuda.device(nbytes.device):
         check(lib().cc_xpow8_dev(_dev_ptr(nbytes, "nbytes"), nbytes.numel(), _dev_ptr(out, "out"),
                                  _stream_handle(stream)), "cc_xpow8_dev")
@@ -324,7 +328,8 @@ def combine_dev(a, b, len_b: int, out=None, stream=None):
     if b.numel() != n:
         raise CurveCrcError(_lib.CC_EINVAL, "a / b length mismatch")
     if out is None:
-        out = torch.empty(n, dtype=torch.int32, device=a.device)
+        with _on_stream(stream):  # created on the stream the kernel writes it on
+            out = torch.empty(n, dtype=torch.int32, device=a.device)
     with torch.cuda.device(a.device):
         check(lib().cc_combine_dev(_dev_ptr(a, "a"), _dev_ptr(b, "b"), int(len_b), n, _dev_ptr(out, "out"),
                                    _stream_handle(stream)), "cc_combine_dev")
@@ -338,7 +343,8 @@ def digest_fold_dev(gathered, nranks: int, out=None, stream=None):
         raise CurveCrcError(_lib.CC_EINVAL, "gathered size is not a multiple of nranks")
     n = gathered.numel() // nranks
     if out is None:
-        out = torch.empty(n, dtype=torch.int32, device=gathered.device)
+        with _on_stream(stream):  # created on the stream the kernel writes it on
+            out = torch.empty(n, dtype=torch.int32, device=gathered.device)
     with torch.cuda.device(gathered.device):
         check(lib().cc_digest_fold_dev(_dev_ptr(gathered, "gathered"), nranks, n, _dev_ptr(out, "out"),
                                        _stream_handle(stream)), "cc_digest_fold_dev")
@@ -352,7 +358,8 @@ def digest_dev(file_crcs, after_bytes, group, n_groups: int, out=None, stream=No
     if after_bytes.numel() != n or group.numel() != n:
         raise CurveCrcError(_lib.CC_EINVAL, "file_crcs / after_bytes / group length mismatch")
     if out is None:
-        out = torch.zeros(n_groups, dtype=torch.int32, device=file_crcs.device)
+        with _on_stream(stream):  # created on the stream the kernel writes it on
+            out = torch.zeros(n_groups, dtype=torch.int32, device=file_crcs.device)
     with torch.cuda.device(file_crcs.device):
         check(lib().cc_digest_dev(_dev_ptr(file_crcs, "file_crcs"), _dev_ptr(after_bytes, "after_bytes"),
                                   _dev_ptr(group, "group"), n, _dev_ptr(out, "out"), _stream_handle(stream)),
