@@ -393,7 +393,7 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
 }
 
 #ifndef CC_INSERT_ABLATE
-#define CC_INSERT_ABLATE 0  // timing ablation of log_insert_kernel (wrong results): 1 no atomics
+#define CC_INSERT_ABLATE 0  // timing ablations of log_insert_kernel (wrong results): 1 no CAS, 2 no head append
 #endif
 #ifndef CC_LOG_ABLATE
 #define CC_LOG_ABLATE 0  // timing ablations of log_pages_kernel (wrong results): 1 no stores, 2 no source loads, 3 no page loads, 4 no CRC chain, 5 no loads/stores of data
@@ -1094,7 +1094,7 @@ __device__ __forceinline__ void insert_piece(const LogLaunch& a, uint64_t t, uin
             // CAS first (one atomic for a page seen first, the common case);
             // next[] is only read by later kernels, so it can follow the CAS
             unsigned long long cur = 0ull;
-#if CC_INSERT_ABLATE  // timing only (wrong grouping): a plain store instead of the CAS
+#if CC_INSERT_ABLATE == 1  // timing only (wrong grouping): a plain store instead of the CAS
             tab[slot] = tag | (unsigned long long)(t + 1);
             a.next[t] = kNoPiece;
             fresh = true;
@@ -1118,6 +1118,10 @@ __device__ __forceinline__ void insert_piece(const LogLaunch& a, uint64_t t, uin
         }
     }
     const uint64_t m = __ballot(fresh);
+#if CC_INSERT_ABLATE == 2  // timing only: heads written at the table slot, no block aggregation or counter
+    if (fresh) a.heads[slot] = slot;
+    return;
+#endif
     if (lane == 0) wcount[wv] = (uint32_t)__popcll(m);
     __syncthreads();
     if (threadIdx.x == 0) {
