@@ -239,7 +239,7 @@ void geometry_for(const DevCtx* c, uint64_t n_pages, PageLaunch* a) {
 }
 
 #ifndef CC_PAGE_DYN_DIV
-#define CC_PAGE_DYN_DIV 8  // 1/8 of a large launch's tiles form the dynamic tail (0: static only)
+#define CC_PAGE_DYN_DIV 16  // 1/16 of a large launch's tiles form the dynamic tail (0: static only; A/B 2.464 ms vs 2.474-2.478 at 1/8, 2.474 at 1/12, 2.51 at 1/24 and 1/32)
 #endif
 // Page kernel launch with the dynamic tail (kernels.hip, page_crc_kernel) when
 // the batch is large: a stream-ordered, zeroed 8-byte chunk counter per call --

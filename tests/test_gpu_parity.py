@@ -309,7 +309,7 @@ def test_large_pool_properties(dev, oracle):
 @pytest.mark.parametrize("page_bytes", [256, 1024])
 def test_page_kernel_dynamic_tail(dev, oracle, page_bytes):
     """Launches large enough for the page kernel's dynamic tail (>= 8 tiles per
-    wave: the last 1/8 of the tiles go out in 64-page chunks through an atomic
+    wave: the last 1/16 of the tiles go out in 64-page chunks through an atomic
     counter): every CRC equals the oracle's, and verify-with-list finds exactly
     the corrupted pages, in the static shares, at the static/dynamic boundary,
     inside the tail and at the very last page (1M + 77 pages: a partial chunk)."""
@@ -320,8 +320,11 @@ def test_page_kernel_dynamic_tail(dev, oracle, page_bytes):
     host = d.cpu().numpy()
     assert (u32(pc) == oracle.page_crcs(host, page_bytes, threads=16)).all()
     tiles = (n_pages + 63) // 64
-    first_dyn = (tiles - tiles // 8) * 64
-    bad = sorted({0, 12345, first_dyn - 1, first_dyn, first_dyn + 64 * 37 + 5, n_pages - 64, n_pages - 1})
+    bad = {0, 12345, n_pages - 64, n_pages - 1}
+    for div in (8, 16):  # the static/dynamic boundary for a 1/8 and a 1/16 tail (engine.hip CC_PAGE_DYN_DIV)
+        first_dyn = (tiles - tiles // div) * 64
+        bad |= {first_dyn - 1, first_dyn, first_dyn + 64 * 37 + 5}
+    bad = sorted(bad)
     for p in bad:
         d[p * page_bytes + 3] ^= 0x80
     cnt, lst = C.page_verify_list(d, pc, page_bytes, max_bad=64)
