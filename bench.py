@@ -658,6 +658,20 @@ def main():
         if r:
             probe_ms.append(pe0.elapsed_time(pe1))
     probe_gbs = pool.data.numel() / (float(np.mean(probe_ms)) * 1e-3) / 1e9
+    # the page kernel itself with its CRC arithmetic removed (same tiles, prefetch
+    # ring, dynamic tail, loads and CRC-sized stores): the ceiling for THIS schedule
+    lo_out = torch.empty(pool.data.numel() // 4096, dtype=torch.int32, device=dev)
+    lo_ms = []
+    for r in range(6):
+        pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        pe0.record(stream)
+        C.page_load_probe(pool.data, lo_out, stream=stream)
+        pe1.record(stream)
+        torch.cuda.synchronize()
+        if r:
+            lo_ms.append(pe0.elapsed_time(pe1))
+    del lo_out
+    load_only_gbs = pool.data.numel() // 4096 * ALG_BYTES_PER_PAGE / (float(np.mean(lo_ms)) * 1e-3) / 1e9
 
     n_pages = n * chunk // pb
     per_step_bytes = n * chunk * world
@@ -691,7 +705,9 @@ def main():
                      "alg_bytes_per_launch": n_pages * ALG_BYTES_PER_PAGE,
                      "traffic_source": traffic_src,
                      "read_probe_GBps": round(probe_gbs, 1),
-                     "frac_of_read_probe": round(achieved / probe_gbs, 4)},
+                     "frac_of_read_probe": round(achieved / probe_gbs, 4),
+                     "load_only_probe_GBps": round(load_only_gbs, 1),
+                     "frac_of_load_only_probe": round(achieved / load_only_gbs, 4)},
         "verify": {"GiBps": round(n * chunk / GiB / (verify_ms * 1e-3), 2), "bad_pages": bad},
     }
     if world > 1:

@@ -98,6 +98,7 @@ SIGNATURES = {
     "cc_page_crc_dev": (_int, [_vp, _u64, _u32, _vp, _vp]),
     "cc_page_verify_dev": (_int, [_vp, _u64, _u32, _vp, _vp, _vp, _vp]),
     "cc_hbm_read_probe_dev": (_int, [_vp, _u64, _vp, _vp]),
+    "cc_page_load_probe_dev": (_int, [_vp, _u64, _vp, _vp]),
     "cc_page_verify_list_dev": (_int, [_vp, _u64, _u32, _vp, _vp, _vp, _vp, _u64, _vp]),
     "cc_fold_dev": (_int, [_vp, _u64, _u32, _u64, _vp, _vp]),
     "cc_shift_dev": (_int, [_vp, _vp, _u64, _vp, _vp]),

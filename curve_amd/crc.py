@@ -213,6 +213,17 @@ def hbm_read_probe(buf, sink, stream=None):
                                       _stream_handle(stream)), "cc_hbm_read_probe_dev")
 
 
+def page_load_probe(pages, out, stream=None):
+    """cc_page_load_probe_dev (diagnostic): the page kernel's schedule and
+    traffic over the 4 KiB pages of `pages` without the CRC arithmetic; `out`
+    (one int32 per page) receives meaningless words."""
+    n = _nbytes(pages) // PAGE_SIZE
+    if out.numel() < n or out.element_size() != 4:
+        raise CurveCrcError(_lib.CC_EINVAL, "out too small or not 32-bit")
+    check(lib().cc_page_load_probe_dev(_dev_ptr(pages, "pages"), n, _dev_ptr(out, "out"), _stream_handle(stream)),
+          "cc_page_load_probe_dev")
+
+
 def page_verify_list(pages, expected, page_bytes: int = PAGE_SIZE, max_bad: int = 4096, stream=None):
     """cc_page_verify_list_dev: -> (counters [bad_count, first_bad] int64 device
     tensor, bad page indices int64 device tensor of max_bad slots; the first

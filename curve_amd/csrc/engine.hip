@@ -246,24 +246,26 @@ void geometry_for(const DevCtx* c, uint64_t n_pages, PageLaunch* a) {
 // `zeroed_ctr` if the caller has one (zeroed on the stream before this launch:
 // cc_pool_scan_dev has the metapage launch clear it), else allocated + memset.
 hipError_t launch_page_tail(const DevCtx* c, PageLaunch& a, bool verify, hipStream_t s,
-                            unsigned long long* zeroed_ctr = nullptr) {
+                            unsigned long long* zeroed_ctr = nullptr, bool load_probe = false) {
     geometry_for(c, a.n_pages, &a);
     const uint32_t m = a.words_per_lane;
     const uint64_t tiles = (a.n_pages + (1ull << a.tile_shift) - 1) >> a.tile_shift;
     const uint64_t waves = (uint64_t)a.blocks * kWavesPerBlock;
-    if (!CC_PAGE_DYN_DIV || m > 32 || (m & (m - 1)) || tiles < waves * 8)
-        return verify ? launch_page_verify(a, s) : launch_page_crc(a, s);
+    auto launch = [&]() {
+        return load_probe ? launch_page_load_probe(a, s) : verify ? launch_page_verify(a, s) : launch_page_crc(a, s);
+    };
+    if (!CC_PAGE_DYN_DIV || m > 32 || (m & (m - 1)) || tiles < waves * 8) return launch();
     a.static_tiles = tiles - tiles / CC_PAGE_DYN_DIV;
     if (zeroed_ctr) {
         a.dyn_ctr = zeroed_ctr;
-        return verify ? launch_page_verify(a, s) : launch_page_crc(a, s);
+        return launch();
     }
     unsigned long long* ctr = nullptr;
     hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(*ctr), s);
     if (e != hipSuccess) return e;
     if ((e = hipMemsetAsync(ctr, 0, sizeof(*ctr), s)) == hipSuccess) {
         a.dyn_ctr = ctr;
-        e = verify ? launch_page_verify(a, s) : launch_page_crc(a, s);
+        e = launch();
     }
     const hipError_t f = hipFreeAsync(ctr, s);
     return e != hipSuccess ? e : f;
@@ -415,6 +417,21 @@ int cc_hbm_read_probe_dev(const void* d_buf, uint64_t bytes, uint32_t* d_sink, v
     int rc = get_ctx(&c);
     if (rc) return rc;
     return map_err(launch_read_probe(d_buf, bytes, d_sink, 2 * c->cus, static_cast<hipStream_t>(stream)));
+}
+
+int cc_page_load_probe_dev(const void* d_pages, uint64_t n_pages, uint32_t* d_out, void* stream) {
+    if (n_pages == 0) return CC_OK;
+    if (!d_pages || !d_out || ((uintptr_t)d_pages & 3u)) return CC_EINVAL;
+    CtxRef c;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    PageLaunch a = {};
+    a.pages = static_cast<const uint32_t*>(d_pages);
+    a.n_pages = n_pages;
+    a.words_per_lane = 4096 / kWaveBytes;
+    a.image = c->image;
+    a.out = d_out;
+    return map_err(launch_page_tail(c.get(), a, false, static_cast<hipStream_t>(stream), nullptr, true));
 }
 
 #if CC_WAVE_TRACE

@@ -60,6 +60,9 @@ int pool_page_launches(const void* d_data, uint64_t n_data_pages, uint32_t page_
                        uint32_t* d_digest, uint64_t digest_words, hipStream_t s, void* ev_begin, void* ev_end);
 hipError_t launch_read_probe(const void* buf, uint64_t bytes, uint32_t* sink, int blocks, hipStream_t s);
 hipError_t launch_page_verify(const PageLaunch& a, hipStream_t s);
+// the page kernel with its CRC arithmetic replaced by a rotate-XOR (4 KiB pages):
+// the same schedule, loads and stores -- the ceiling the real kernel is held to
+hipError_t launch_page_load_probe(const PageLaunch& a, hipStream_t s);
 
 struct FoldLaunch {
     const uint32_t* crcs;

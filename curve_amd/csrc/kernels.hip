@@ -179,7 +179,7 @@ template <int MODE>
 __device__ __forceinline__ void flush_tile(uint32_t acc, uint64_t tile_first, uint32_t cnt, uint32_t lane,
                                            uint32_t* __restrict__ out, const uint32_t* __restrict__ expected,
                                            const VerifySink& vs) {
-    if (MODE == 0) {
+    if (MODE != 1) {  // compute (0) and the load-only probe (2) store the tile
 #if CC_STORE == 1  // diagnostic: no store (wrong output), keeps acc live
         asm volatile("" ::"v"(acc));
 #elif CC_STORE == 2
@@ -246,7 +246,10 @@ __device__ __forceinline__ void load_pages(uint32_t (&w)[P][M], const uint32_t* 
 
 // P independent Horner chains, interleaved step by step so each wave keeps
 // 4*P LDS lookups in flight instead of 4.
-template <int M, int P>
+// LOADS_ONLY: the chain replaced by a rotate-XOR that keeps every loaded word
+// live (the load-only probe, MODE 2: the kernel's own schedule and traffic
+// without the CRC arithmetic)
+template <int M, int P, bool LOADS_ONLY = false>
 __device__ __forceinline__ void chains(const uint32_t* tab, const uint32_t (&w)[P][M], uint32_t c0, uint32_t c1,
                                        uint32_t (&s)[P]) {
 #pragma unroll
@@ -255,11 +258,10 @@ __device__ __forceinline__ void chains(const uint32_t* tab, const uint32_t (&w)[
     for (int j = 1; j < M; j++) {
 #pragma unroll
         for (int q = 0; q < P; q++) {
-#if CC_ABLATE == 1
-            s[q] = ((s[q] << 1) | (s[q] >> 31)) ^ w[q][j];
-#else
-            s[q] = apply_g_xor(tab, s[q], w[q][j], c0, c1);
-#endif
+            if (LOADS_ONLY || CC_ABLATE == 1)
+                s[q] = ((s[q] << 1) | (s[q] >> 31)) ^ w[q][j];
+            else
+                s[q] = apply_g_xor(tab, s[q], w[q][j], c0, c1);
         }
     }
 }
@@ -334,14 +336,14 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
                     const uint64_t kk = k + (uint64_t)st * P;
                     load_pages<M, P>(ring[(st + D) % (D + 1)], base, W, kk + (uint64_t)D * P, last);
                     uint32_t s[P];
-                    chains<M, P>(tab, ring[st], c0, c1, s);
+                    chains<M, P, MODE == 2>(tab, ring[st], c0, c1, s);
 #pragma unroll
                     for (int q = 0; q < P; q++) {
                         const uint64_t kq = kk + q;
                         const uint64_t pc = W.page(kq);
                         if (pc < lim) {
                             const uint64_t pn = W.page(kq + 1);
-                            const uint32_t crc = wave_xor(apply_fin(tab, s[q], cf)) ^ kconst;
+                            const uint32_t crc = MODE == 2 ? wave_xor(s[q]) : wave_xor(apply_fin(tab, s[q], cf)) ^ kconst;
                             const uint32_t slot = (uint32_t)(kq & W.tmask);
                             acc = lane == slot ? crc : acc;
                             if (slot == W.tmask || pn >= lim)
@@ -1804,6 +1806,15 @@ hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_page_crc(const PageLaunch& a, hipStream_t s) { return launch_page<0>(a, s); }
+
+hipError_t launch_page_load_probe(const PageLaunch& a, hipStream_t s) {
+    if (a.words_per_lane != 16) return hipErrorInvalidValue;  // 4 KiB pages only
+    const ZeroRanges zr = {{nullptr, nullptr}, {0, 0}};
+    hipLaunchKernelGGL((page_crc_kernel<16, 2>), dim3(a.blocks), dim3(kBlockThreads), 0, s, a.pages, a.n_pages,
+                       static_cast<const uint4*>(a.image), a.kconst, a.out, a.expected, a.sink, a.tile_shift,
+                       a.dyn_ctr, a.static_tiles, zr);
+    return hipGetLastError();
+}
 
 // Read-only probe (diagnostic): dwordx4 nt loads, 4 in flight per lane, the
 // fastest pure-read shape found by scripts/hbm_probe.hip.  Static strided

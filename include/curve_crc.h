@@ -516,6 +516,13 @@ int cc_lds_image(void* out, size_t bytes);
  * beside the 8 TB/s spec.  Enqueue only. */
 int cc_hbm_read_probe_dev(const void* d_buf, uint64_t bytes, uint32_t* d_sink, void* stream);
 
+/* Diagnostic (no reference counterpart): the page kernel over n_pages 4 KiB
+ * pages with its CRC arithmetic replaced by a rotate-XOR -- the same schedule
+ * (tiles, prefetch ring, dynamic tail), loads and 4-byte-per-page stores into
+ * d_out, so its time is the ceiling cc_page_crc_dev is held to on this device.
+ * d_out receives meaningless words.  Enqueue only. */
+int cc_page_load_probe_dev(const void* d_pages, uint64_t n_pages, uint32_t* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -341,6 +341,27 @@ def test_page_kernel_dynamic_tail(dev, oracle, page_bytes):
     assert not torch.equal(again, pc)
 
 
+def test_page_load_probe_diagnostic(dev):
+    """cc_page_load_probe_dev (the bench's load-only ceiling): runs the page
+    kernel's schedule, static shares and dynamic tail, over 1M + 77 pages and
+    writes one word per page, the same words every run; no CRC arithmetic."""
+    from curve_amd import crc as C
+    n = (1 << 20) + 77
+    d = torch.empty(n * 4096, dtype=torch.uint8, device=dev).random_(0, 256)
+    a = torch.zeros(n, dtype=torch.int32, device=dev)
+    b = torch.ones(n, dtype=torch.int32, device=dev)
+    C.page_load_probe(d, a)
+    C.page_load_probe(d, b)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    # every page was visited: the word of a page changes when the page does
+    d[(n - 1) * 4096] ^= 1
+    d[12345 * 4096 + 7] ^= 1
+    C.page_load_probe(d, b)
+    torch.cuda.synchronize()
+    assert sorted(torch.nonzero(a != b).flatten().tolist()) == [12345, n - 1]
+
+
 def test_write_log_full_size_config3(dev, oracle):
     """BASELINE config 3 at full size: a 16 GiB pool (1024 chunks), 65,536 random
     512 B-4 KiB writes in one log (unaligned, straddling, some overlapping).
