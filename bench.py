@@ -608,6 +608,15 @@ def main():
 
     for _ in range(args.warmup):
         step(None)
+    # The GPU clock ramps over the first ~30-40 ms of work after idle (a kernel
+    # trace shows launches 1..10 at 2.77 -> 2.51 ms).  If the W requested warm-up
+    # steps are shorter than that, run extra UNTIMED steps up to ~40 ms, reported
+    # as "clock_warmup_steps".  The count follows from the per-rank bytes only,
+    # so every rank runs the same number of steps (each step holds a collective).
+    est_ms = n * chunk / 6.5e12 * 1e3  # ~6.5 TB/s
+    clock_warm = max(0, int(np.ceil(40.0 / est_ms)) - args.warmup) if args.warmup > 0 else 0
+    for _ in range(clock_warm):
+        step(None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -688,6 +697,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "clock_warmup_steps": clock_warm,
         "ms_per_step": round(el / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
