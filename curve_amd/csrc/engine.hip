@@ -981,6 +981,7 @@ bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork
 #endif
     uint64_t te = 1024;
     while (te < CC_LOG_TABLE_FACTOR * w->n_pieces) te <<= 1;  // load <= 1 / factor
+    if (te > (1ull << 32)) return false;  // slots and the mask are 32-bit
     w->table_entries = te;
     w->table_off = 256;
     w->next_off = w->table_off + te * 8;

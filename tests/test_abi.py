@@ -69,3 +69,17 @@ def test_argument_checks_need_no_gpu():
     assert L.cc_scan_files(None, 1, 1 << 20, 4096, 4096, 4096, 2, None, res) == _lib.CC_EINVAL
     assert L.cc_scan_files(None, 0, 1 << 20, 4096, 4096, 4096, 2, None, res) == _lib.CC_OK
     assert L.cc_strerror(_lib.CC_ENODEV) == b"no usable HIP device"
+
+
+def test_write_log_work_sizing_limits():
+    """cc_apply_log_work_bytes (host arithmetic only): the hash table holds >= 4
+    entries per piece in a power of two, and a log whose table would need more
+    than 2^32 slots (32-bit slot indices) is refused with 0, not truncated."""
+    from curve_amd import _lib
+    L = _lib.lib()
+    small = L.cc_apply_log_work_bytes(65536, 4096, 4096)  # 2 pieces per write
+    assert small >= 256 + 4 * 131072 * 8 + 2 * 131072 * 4
+    assert L.cc_apply_log_work_bytes(1 << 29, 4096, 4096) > 0          # 2^30 pieces -> 2^32 slots
+    assert L.cc_apply_log_work_bytes((1 << 29) + 1, 4096, 4096) == 0   # would need 2^33 slots
+    assert L.cc_apply_log_work_bytes(0, 4096, 4096) == 0
+    assert L.cc_apply_log_work_bytes(10, 0, 4096) == 0
