@@ -1097,6 +1097,12 @@ int cc_verify_reads_dev(const void* d_pool, uint64_t pool_bytes, uint32_t page_b
     a.kconst = kconst_for(page_bytes);
     a.blocks = c->cus;  // every wave takes an equal share of the (device-computed) page slots
     hipError_t e;
+#ifndef CC_RV_SMALL
+#define CC_RV_SMALL 64  // batches of up to this many reads take the one-launch path
+#endif
+    // (page counts summed in 32 bits there: pools of < 2^26 pages keep 64 reads' sum exact)
+    if (n_reads <= (uint64_t)CC_RV_SMALL && n_reads <= 64 && pool_bytes / page_bytes < (1ull << 26))
+        return map_err(launch_read_verify_small(a, s));
     if ((e = launch_read_counts(a, s)) != hipSuccess) return map_err(e);
     if ((e = exclusive_scan_u64(temp, temp_bytes, a.counts, a.start, n_reads, s)) != hipSuccess)
         return map_err(e);

@@ -171,6 +171,8 @@ size_t scan_temp_bytes(uint64_t n);
 hipError_t exclusive_scan_u64(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
                               hipStream_t s);
 hipError_t launch_read_verify(const ReadVerifyLaunch& a, hipStream_t s);
+// <= 64 reads in one launch (no counts / scan; pages split over waves)
+hipError_t launch_read_verify_small(const ReadVerifyLaunch& a, hipStream_t s);
 // CRC32C (butil Value) of arbitrary byte ranges of one device buffer, on the
 // flat block schedule: range_tiles_kernel writes the 4 KiB-block
 // count of each of kRangeTiles contiguous tiles of the batch (and zeroes

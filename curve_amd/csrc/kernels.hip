@@ -1402,6 +1402,9 @@ __device__ __forceinline__ void load_rows(uint32_t (&w)[M], const unsigned char*
 template <int M, bool Delta>
 __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab) {
     constexpr int WV = log_waves(M, Delta);
+    // a block whose waves own no head (a small log) leaves before filling its
+    // 160 KiB of LDS (uniform per block)
+    if ((uint64_t)blockIdx.x * WV >= *a.head_count) return;
     fill_lds<64 * WV>(tab, static_cast<const uint4*>(a.image));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1643,9 +1646,19 @@ constexpr int kRvWaves = CC_RV_WAVES;
 #ifndef CC_RV_DYN_SLOTS
 #define CC_RV_DYN_SLOTS 32  // slots (pages) per dynamic chunk (64: -1 %, 128: -5 %, 256: -18 % -- too coarse)
 #endif
+#ifndef CC_RV_MIN_SLOTS
+#define CC_RV_MIN_SLOTS 8  // a small batch goes to the fewest waves that give each >= 8 page slots
+#endif
 template <int M>
 __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLaunch a) {
     __shared__ uint32_t tab[kLdsBytes / 4];
+    const uint64_t n = a.n_reads;
+    const uint64_t T = a.start[n - 1] + a.counts[n - 1];
+    // W waves share the slots: all of the grid for a large batch, fewer for a
+    // small one, and the blocks left without a share exit before filling LDS
+    const uint64_t Wg = (uint64_t)gridDim.x * kRvWaves, Wt = (T + CC_RV_MIN_SLOTS - 1) / CC_RV_MIN_SLOTS;
+    const uint64_t W = Wt < Wg ? (Wt ? Wt : 1) : Wg;
+    if ((uint64_t)blockIdx.x * kRvWaves >= W) return;  // uniform per block
     fill_lds<64 * kRvWaves>(tab, static_cast<const uint4*>(a.image));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1653,9 +1666,6 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
     const uint32_t* pages = a.pool + lane;
-    const uint64_t n = a.n_reads;
-    const uint64_t T = a.start[n - 1] + a.counts[n - 1];
-    const uint64_t W = (uint64_t)gridDim.x * kRvWaves;
     const uint64_t w = (uint64_t)blockIdx.x * kRvWaves + wave;
     uint32_t vz = 0;
     asm volatile("" : "+v"(vz));  // opaque zero: keeps uniform-address loads on the vector path
@@ -1683,7 +1693,7 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
     // static shares of the first Ts slots, then dynamic chunks of CC_RV_DYN_SLOTS
     // slots (the page kernel's tail: the XCDs run at different rates)
     const uint64_t Ts = T - T / CC_RV_DYN_DIV;
-    uint64_t lo_slot = Ts * w / W, hi_slot = Ts * (w + 1) / W;
+    uint64_t lo_slot = w < W ? Ts * w / W : Ts, hi_slot = w < W ? Ts * (w + 1) / W : Ts;  // waves past W: tail only
 #pragma unroll 1
     for (;;) {
         const uint64_t rb = lower_bound(lo_slot), re = lower_bound(hi_slot);
@@ -1744,6 +1754,72 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
     }
 }
 
+
+// A small batch (<= 64 reads: one per lane) in ONE launch, for the per-request
+// latency of the read path: no count kernel and no scan.  Every wave loads the
+// batch's descriptors, computes the pages per read (a read past the pool is
+// marked as read_counts_kernel marks it) and their wave prefix sum; the P pages
+// are split evenly over the fewest waves that give each >= CC_RV_MIN_SLOTS, at
+// PAGE granularity (a 32-page read is verified by 4 waves), and the blocks left
+// without pages exit before filling LDS.
+template <int M>
+__global__ __launch_bounds__(64 * kRvWaves) void read_verify_small_kernel(ReadVerifyLaunch a) {
+    __shared__ uint32_t tab[kLdsBytes / 4];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t vz = 0;
+    asm volatile("" : "+v"(vz));
+    const bool valid = lane < a.n_reads;
+    const RangeDesc r = a.reads[(valid ? lane : 0u) + vz];
+    const bool past = r.off >= a.pool_bytes || r.len > a.pool_bytes - r.off;
+    uint32_t cnt = 0;
+    if (valid && !past && r.len) cnt = (uint32_t)((r.off + r.len - 1) / a.page_bytes - r.off / a.page_bytes + 1);
+    if (valid && past && r.len && blockIdx.x == 0 && wave == 0) a.bad_per_read[lane] = 0xFFFFFFFFu;
+    const uint64_t p0 = r.off / a.page_bytes;
+    uint32_t cum = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(cum, d, 64);
+        if (lane >= (uint32_t)d) cum += o;
+    }
+    const uint32_t P = __builtin_amdgcn_readlane(cum, 63);
+    const uint32_t Wg = gridDim.x * kRvWaves, Wt = (P + CC_RV_MIN_SLOTS - 1) / CC_RV_MIN_SLOTS;
+    const uint32_t W = Wt < Wg ? Wt : Wg;
+    if (blockIdx.x * (uint32_t)kRvWaves >= W) return;  // uniform per block (P == 0: every block)
+    fill_lds<64 * kRvWaves>(tab, static_cast<const uint4*>(a.image));
+    const uint32_t w = blockIdx.x * kRvWaves + wave;
+    if (w >= W) return;
+    const uint32_t k0 = (uint32_t)((uint64_t)P * w / W), k1 = (uint32_t)((uint64_t)P * (w + 1) / W);
+    const uint32_t c0 = lane << 2 & 0x7Cu;
+    const uint32_t c1 = c0 | 0x10000u;
+    const uint32_t cf = kFinBase + (lane << 2);
+    const uint32_t* pages = a.pool + lane;
+    auto page_at = [&](uint32_t k, uint32_t& owner) -> uint64_t {
+        owner = (uint32_t)__builtin_ctzll(__ballot(cum > k));
+        const uint32_t before = owner ? (uint32_t)__builtin_amdgcn_readlane(cum, owner - 1) : 0u;
+        return readlane64(p0, owner) + (k - before);
+    };
+    // pages k0 .. k1-1, the next page's loads in flight while one is hashed
+    uint32_t X[M], Y[M];
+    uint32_t ox, oy;
+    uint64_t gx = page_at(k0, ox);
+    uint32_t sx = a.page_crcs[gx + vz];
+    load_page<M>(X, pages + gx * (64u * M));
+    for (uint32_t k = k0; k < k1; k++) {
+        const uint64_t gy = page_at(k + 1 < k1 ? k + 1 : k, oy);  // clamped: same loads every step
+        const uint32_t sy = a.page_crcs[gy + vz];
+        load_page<M>(Y, pages + gy * (64u * M));
+        const uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
+        if (crc != sx && lane == 0) {
+            atomicAdd(a.bad_per_read + ox, 1u);
+            atomicAdd(a.bad_total, 1ull);
+        }
+#pragma unroll
+        for (int j = 0; j < M; j++) X[j] = Y[j];
+        sx = sy;
+        ox = oy;
+    }
+}
 
 __global__ void combine_kernel(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t m,
                                uint64_t n, uint32_t* __restrict__ out) {
@@ -1945,6 +2021,23 @@ hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s) {
 hipError_t launch_read_counts(const ReadVerifyLaunch& a, hipStream_t s) {
     if (a.n_reads == 0) return hipSuccess;
     hipLaunchKernelGGL(read_counts_kernel, dim3((uint32_t)((a.n_reads + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_read_verify_small(const ReadVerifyLaunch& a, hipStream_t s) {
+    if (a.n_reads == 0 || a.n_reads > 64) return hipErrorInvalidValue;
+#define CC_SCASE(MM) \
+    case MM: hipLaunchKernelGGL((read_verify_small_kernel<MM>), dim3(a.blocks), dim3(64 * kRvWaves), 0, s, a); break;
+    switch (a.page_bytes / kWaveBytes) {
+        CC_SCASE(1)
+        CC_SCASE(2)
+        CC_SCASE(4)
+        CC_SCASE(8)
+        CC_SCASE(16)
+        CC_SCASE(32)
+        default: return hipErrorInvalidValue;
+    }
+#undef CC_SCASE
     return hipGetLastError();
 }
 

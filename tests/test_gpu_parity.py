@@ -449,6 +449,45 @@ def test_verify_reads_batch(dev, oracle, page_bytes):
     assert (bad2.cpu().numpy() == got).all() and int(total2.item()) == want_total
 
 
+@pytest.mark.parametrize("page_bytes", [4096, 512])
+@pytest.mark.parametrize("n_reads", [1, 2, 17, 64, 65])
+def test_verify_reads_small_batches(dev, oracle, page_bytes, n_reads):
+    """cc_verify_reads_dev for small batches (<= 64 reads take the one-launch
+    path: counts and a wave prefix sum in registers, pages split over waves;
+    65 takes count + scan + verify): every read shape -- page-aligned, 512 B,
+    unaligned, empty, past the end, the whole pool -- reports exactly the
+    corrupted pages it touches, and the totals agree."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(page_bytes * 1000 + n_reads)
+    n_pages = 3000
+    host = rng.integers(0, 256, n_pages * page_bytes, dtype=np.uint8)
+    stored = to_dev(oracle.page_crcs(host, page_bytes).view(np.int32), dev)
+    pool = to_dev(host, dev)
+    bad_pages = {0, 7, 64, 65, 1999, n_pages - 1}
+    for p in bad_pages:
+        pool[p * page_bytes + int(rng.integers(0, page_bytes))] ^= 0x10
+    total_bytes = n_pages * page_bytes
+    shapes = [(0, total_bytes), (7 * page_bytes, 3 * page_bytes), (total_bytes - 10, 11), (5 * page_bytes, 0),
+              (63 * page_bytes + 17, 2 * page_bytes), (total_bytes - 10, 10), (100, 1), (512, 4096)]
+    reads = shapes[:n_reads]
+    while len(reads) < n_reads:
+        o = int(rng.integers(0, total_bytes - 1))
+        reads.append((o, int(rng.integers(0, min(40 * page_bytes, total_bytes - o) + 1))))
+    off, ln = zip(*reads)
+    bad, total = C.verify_reads(pool, stored, off, ln, page_bytes)
+    got = bad.cpu().numpy()
+    want_total = 0
+    for i, (o, n) in enumerate(reads):
+        if o + n > total_bytes:
+            assert got[i] == -1, i
+            continue
+        touched = set(range(o // page_bytes, (o + n - 1) // page_bytes + 1)) if n else set()
+        want = len(touched & bad_pages)
+        want_total += want
+        assert got[i] == want, (i, o, n)
+    assert int(total.item()) == want_total
+
+
 def test_beyond_4gib_offsets(dev, oracle):
     """Maximum-size addressing: a 4.25 GiB buffer (byte offsets past 2^32):
     every page CRC, verify finding a page past 4 GiB, and ranges at offsets
