@@ -1036,6 +1036,10 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
     const uint64_t blocks = (lw.n_pieces + kLogWaves - 1) / kLogWaves;
     a.blocks = (int)(blocks < (uint64_t)c->cus ? (blocks ? blocks : 1) : (uint64_t)c->cus);
     hipError_t e;
+#ifndef CC_LOG_SMALL
+#define CC_LOG_SMALL 64  // logs of up to this many writes (each within one page's length) take the one-launch path
+#endif
+    if (n_updates <= (uint64_t)CC_LOG_SMALL && n_updates <= 64 && a.slots <= 2) return map_err(launch_log_small(a, s));
     // (memset + insert + pages as ONE cooperative launch with two grid barriers
     // measured 0.221 vs 0.162 ms a batch: not kept)
     if ((e = hipMemsetAsync(w, 0, lw.next_off, s)) != hipSuccess) return map_err(e);  // counter + table

@@ -141,6 +141,8 @@ struct LogLaunch {
 };
 hipError_t launch_log_insert(const LogLaunch& a, hipStream_t s);
 hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s);
+// <= 64 writes of <= 2 pieces each in one launch (no table, no insert)
+hipError_t launch_log_small(const LogLaunch& a, hipStream_t s);
 
 struct RangeDesc {
     uint64_t off, len;

@@ -1605,6 +1605,86 @@ __global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(Log
     log_pages_body<M, Delta>(a, tab);
 }
 
+// A small log (<= 64 writes of <= one page each: at most 2 pieces a write) in
+// ONE launch, for the per-request latency of the write path: no table memset,
+// no insert.  Every wave loads the log into its lanes and finds the distinct
+// touched pages itself (a page belongs to the first write touching it: a
+// 64-step scan over the earlier lanes); page u goes to wave u, which applies
+// every write touching it in log order (a ballot over the lanes, set bits in
+// lane order) through the generic piece merge, stores the changed rows and
+// rehashes the page.  Blocks without a page exit before filling LDS.
+template <int M, bool Delta>
+__global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_small_kernel(LogLaunch a) {
+    constexpr int WV = log_waves(M, Delta);
+    __shared__ uint32_t tab[kLdsBytes / 4];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t pb = a.page_bytes;
+    uint32_t vz = 0;
+    asm volatile("" : "+v"(vz));
+    const bool valid = lane < a.n_updates;
+    const UpdateDesc d = a.upd[(valid ? lane : 0u) + vz];
+    const bool ok = valid && d.len >= 1 && d.len <= a.max_len && d.dst < a.pool_bytes && d.len <= a.pool_bytes - d.dst;
+    const uint64_t q0 = ok ? d.dst / pb : 0, q1 = ok ? (d.dst + d.len - 1) / pb : 0;
+    // write `lane` owns its page q0 (q1) unless an earlier write touches it
+    bool own0 = ok, own1 = ok && q1 != q0;
+    for (uint32_t j = 0; j < 63u && j + 1 < a.n_updates; j++) {
+        const bool okj = __builtin_amdgcn_readlane((uint32_t)ok, j) != 0u;
+        const uint64_t j0 = readlane64(q0, j), j1 = readlane64(q1, j);
+        if (okj && lane > j) {
+            own0 = own0 && !(j0 <= q0 && q0 <= j1);
+            own1 = own1 && !(j0 <= q1 && q1 <= j1);
+        }
+    }
+    const uint64_t m0 = __ballot(own0), m1 = __ballot(own1);
+    const uint32_t D = (uint32_t)__popcll(m0) + (uint32_t)__popcll(m1);  // distinct touched pages
+    const uint32_t Wg = gridDim.x * WV, W = D < Wg ? D : Wg;
+    if (blockIdx.x * (uint32_t)WV >= W) return;  // uniform per block (an empty log: every block)
+    fill_lds<64 * WV>(tab, static_cast<const uint4*>(a.image));
+    const uint32_t c0 = lane << 2 & 0x7Cu;
+    const uint32_t c1 = c0 | 0x10000u;
+    const uint32_t cf = kFinBase + (lane << 2);
+    const uint32_t* pages = reinterpret_cast<const uint32_t*>(a.pool) + lane;
+    const uint32_t n0 = (uint32_t)__popcll(m0);
+    for (uint32_t u = blockIdx.x * WV + wave; u < D; u += W) {
+        // page u: the u-th owned q0 (lane order), then the owned q1s
+        uint64_t mm = u < n0 ? m0 : m1;
+        for (uint32_t r = u < n0 ? u : u - n0; r; r--) mm &= mm - 1;  // drop the lowest r set bits
+        const uint32_t l = (uint32_t)__builtin_ctzll(mm);
+        const uint64_t pg = u < n0 ? readlane64(q0, l) : readlane64(q1, l);
+        const uint64_t pbase = pg * pb;
+        uint32_t X[M], O[Delta ? M : 1];
+        load_page<M>(X, pages + pg * (64u * M));
+        if constexpr (Delta) {
+#pragma unroll
+            for (int j = 0; j < M; j++) O[j] = X[j];
+        }
+        uint32_t dirty = 0;
+        const bool hit = ok && d.dst < pbase + pb && d.dst + d.len > pbase;
+        for (uint64_t m = __ballot(hit); m; m &= m - 1) {  // the writes touching the page, in log order
+            const uint32_t wl = (uint32_t)__builtin_ctzll(m);
+            const Piece pq = piece_in_page(pbase, pb, readlane64(d.dst, wl), readlane64(d.src, wl),
+                                           __builtin_amdgcn_readlane(d.len, wl), a.src);
+            PieceSrc<M> T;
+            fetch_piece<M>(T, pq, lane);
+            merge_piece<M>(X, dirty, T, pq, lane);
+        }
+        const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(a.pool + pbase, 0, 256u * M, kBufFlags);
+#pragma unroll
+        for (int j = 0; j < M; j++)
+            __builtin_amdgcn_raw_buffer_store_b32(X[j], rp, (((dirty >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j, 0, 0);
+        uint32_t crc;
+        if constexpr (Delta) {
+#pragma unroll
+            for (int j = 0; j < M; j++) O[j] ^= X[j];
+            crc = wave_xor(apply_fin(tab, chain<M>(tab, O, c0, c1), cf)) ^ a.page_crcs[pg + vz];
+        } else {
+            crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
+        }
+        if (lane == 0) a.page_crcs[pg] = crc;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Verify-on-read for a batch of datastore reads (cc_verify_reads_dev)
 // ---------------------------------------------------------------------------
@@ -1625,9 +1705,9 @@ __global__ void read_counts_kernel(ReadVerifyLaunch a) {
 
 // Every page a read touches is one slot; read i owns slots start[i] ..
 // start[i] + counts[i] - 1 (start = exclusive scan of counts).  Wave w owns
-// the reads whose first slot lies in [T*w/W, T*(w+1)/W): balanced to within
-// one read whatever the read sizes, found with two 64-ary searches over
-// start[] (lanes probe 64 entries per round trip).  It takes its reads 64 at a
+// the slots [T*w/W, T*(w+1)/W) at page granularity (a read may be split over
+// waves; its mismatches are counted by atomics), found with two 64-ary
+// searches over start[] (lanes probe 64 entries per round trip).  It takes its reads 64 at a
 // time (lane j <- one read: first page, page count) and lays their pages out
 // as one stream with a wave prefix sum: page k of the stream belongs to the
 // first lane whose running count exceeds k (a ballot), so the stream is walked
@@ -1648,6 +1728,9 @@ constexpr int kRvWaves = CC_RV_WAVES;
 #endif
 #ifndef CC_RV_MIN_SLOTS
 #define CC_RV_MIN_SLOTS 8  // a small batch goes to the fewest waves that give each >= 8 page slots
+#endif
+#ifndef CC_RV_SMALL_MIN_SLOTS
+#define CC_RV_SMALL_MIN_SLOTS 2  // the one-launch path (<= 64 reads): >= 2 pages per wave
 #endif
 template <int M>
 __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLaunch a) {
@@ -1696,12 +1779,17 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
     uint64_t lo_slot = w < W ? Ts * w / W : Ts, hi_slot = w < W ? Ts * (w + 1) / W : Ts;  // waves past W: tail only
 #pragma unroll 1
     for (;;) {
-        const uint64_t rb = lower_bound(lo_slot), re = lower_bound(hi_slot);
+        // slots [lo_slot, hi_slot) at PAGE granularity: from the read holding
+        // slot lo_slot (the last read whose first slot is <= it) through the
+        // reads starting before hi_slot, cut at both ends
+        const uint64_t rb = lo_slot < hi_slot ? lower_bound(lo_slot + 1) - 1 : 0;
+        const uint64_t re = lo_slot < hi_slot ? lower_bound(hi_slot) : 0;
         for (uint64_t base = rb; base < re; base += 64) {
             const uint64_t ri = base + lane;
             const bool valid = ri < re;
             const RangeDesc r = a.reads[(valid ? ri : base) + vz];
             const uint32_t cnt = valid ? (uint32_t)a.counts[ri] : 0u;  // 0 also for reads past the pool
+            const uint64_t S = readlane64(a.start[base + vz], 0);      // slot of the group's page 0
             const uint64_t p0 = r.off / a.page_bytes;
             uint32_t cum = cnt;  // inclusive prefix sum over the lanes
 #pragma unroll
@@ -1710,7 +1798,9 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
                 if (lane >= (uint32_t)d) cum += o;
             }
             const uint32_t P = __builtin_amdgcn_readlane(cum, 63);
-            if (P == 0) continue;
+            const uint32_t ks = lo_slot > S ? (uint32_t)(lo_slot - S) : 0u;
+            const uint32_t ke = hi_slot - S < (uint64_t)P ? (uint32_t)(hi_slot - S) : P;
+            if (ks >= ke) continue;
             auto page_at = [&](uint32_t k, uint32_t& owner) -> uint64_t {
                 owner = (uint32_t)__builtin_ctzll(__ballot(cum > k));
                 const uint32_t before = owner ? (uint32_t)__builtin_amdgcn_readlane(cum, owner - 1) : 0u;
@@ -1720,7 +1810,7 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
             };
             uint32_t A[M], B[M], Cq[M];
             uint32_t oA, oB, oC;
-            uint64_t gA = page_at(0, oA), gB = page_at(P > 1 ? 1 : 0, oB), gC = gB;
+            uint64_t gA = page_at(ks, oA), gB = page_at(ks + 1 < ke ? ks + 1 : ks, oB), gC = gB;
             oC = oB;
             uint32_t sA = stored_crc(gA), sB = stored_crc(gB), sC = sB;
             load_page<M>(A, pages + gA * (64u * M));
@@ -1728,8 +1818,8 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
             // hash X (page k: stored CRC sx, owner lane ox); page k+2's loads go into Y
             auto step = [&](uint32_t (&X)[M], uint32_t sx, uint32_t ox, uint32_t k, uint32_t (&Y)[M], uint64_t& gy,
                             uint32_t& sy, uint32_t& oy) {
-                const bool more = k + 1 < P;
-                gy = page_at(k + 2 < P ? k + 2 : P - 1, oy);  // clamped: same loads every step
+                const bool more = k + 1 < ke;
+                gy = page_at(k + 2 < ke ? k + 2 : ke - 1, oy);  // clamped: same loads every step
                 sy = stored_crc(gy);
                 load_page<M>(Y, pages + gy * (64u * M));
                 const uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
@@ -1739,7 +1829,7 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
                 }
                 return more;
             };
-            for (uint32_t k = 0;; k += 3) {
+            for (uint32_t k = ks;; k += 3) {
                 if (!step(A, sA, oA, k, Cq, gC, sC, oC)) break;
                 if (!step(B, sB, oB, k + 1, A, gA, sA, oA)) break;
                 if (!step(Cq, sC, oC, k + 2, B, gB, sB, oB)) break;
@@ -1783,7 +1873,7 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_small_kernel(ReadVe
         if (lane >= (uint32_t)d) cum += o;
     }
     const uint32_t P = __builtin_amdgcn_readlane(cum, 63);
-    const uint32_t Wg = gridDim.x * kRvWaves, Wt = (P + CC_RV_MIN_SLOTS - 1) / CC_RV_MIN_SLOTS;
+    const uint32_t Wg = gridDim.x * kRvWaves, Wt = (P + CC_RV_SMALL_MIN_SLOTS - 1) / CC_RV_SMALL_MIN_SLOTS;
     const uint32_t W = Wt < Wg ? Wt : Wg;
     if (blockIdx.x * (uint32_t)kRvWaves >= W) return;  // uniform per block (P == 0: every block)
     fill_lds<64 * kRvWaves>(tab, static_cast<const uint4*>(a.image));
@@ -2015,6 +2105,30 @@ hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s) {
         default: return hipErrorInvalidValue;
     }
 #undef CC_GCASE
+    return hipGetLastError();
+}
+
+hipError_t launch_log_small(const LogLaunch& a, hipStream_t s) {
+    if (a.n_updates == 0 || a.n_updates > 64 || a.slots > 2) return hipErrorInvalidValue;
+#define CC_SMCASE(MM)                                                                                         \
+    case MM:                                                                                                  \
+        if (a.delta)                                                                                          \
+            hipLaunchKernelGGL((log_small_kernel<MM, true>), dim3(a.blocks), dim3(64 * log_waves(MM, true)), 0, s, \
+                               a);                                                                            \
+        else                                                                                                  \
+            hipLaunchKernelGGL((log_small_kernel<MM, false>), dim3(a.blocks), dim3(64 * log_waves(MM, false)), 0, \
+                               s, a);                                                                         \
+        break;
+    switch (a.page_bytes / kWaveBytes) {
+        CC_SMCASE(1)
+        CC_SMCASE(2)
+        CC_SMCASE(4)
+        CC_SMCASE(8)
+        CC_SMCASE(16)
+        CC_SMCASE(32)
+        default: return hipErrorInvalidValue;
+    }
+#undef CC_SMCASE
     return hipGetLastError();
 }
 

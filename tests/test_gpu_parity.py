@@ -449,6 +449,34 @@ def test_verify_reads_batch(dev, oracle, page_bytes):
     assert (bad2.cpu().numpy() == got).all() and int(total2.item()) == want_total
 
 
+def test_verify_reads_full_batch_with_corruption(dev):
+    """The bench's read-verify shape at full batch size (65,536 reads of 1-32
+    pages over a 2 GiB pool): with 300 corrupted pages every read reports
+    exactly the corrupted pages it touches -- reads split over waves at page
+    granularity and the dynamic tail included -- and the total matches."""
+    from curve_amd import crc as C
+    pb, n = 4096, 65536
+    n_pages = (2 << 30) // pb
+    pool = torch.empty(n_pages * pb, dtype=torch.uint8, device=dev).random_(0, 256)
+    stored = C.page_crc(pool, pb)
+    rng = np.random.default_rng(0xBAD)
+    bad_pages = np.unique(rng.integers(0, n_pages, 300))
+    for p in bad_pages:
+        pool[int(p) * pb + int(rng.integers(0, pb))] ^= 0x01
+    first = rng.integers(0, n_pages - 32, n)
+    npg = rng.integers(1, 33, n)
+    d_reads = torch.from_numpy(np.stack([first * pb, npg * pb], axis=1).reshape(-1).astype(np.int64)).to(dev)
+    bad = torch.zeros(n, dtype=torch.int32, device=dev)
+    total = torch.zeros(1, dtype=torch.int64, device=dev)
+    C.verify_read_records(pool, stored, d_reads, n, bad, total, pb)
+    ind = np.zeros(n_pages + 1, dtype=np.int64)
+    ind[bad_pages + 1] = 1
+    csum = np.cumsum(ind)
+    want = csum[first + npg] - csum[first]
+    assert (bad.cpu().numpy() == want).all()
+    assert int(total.item()) == int(want.sum())
+
+
 @pytest.mark.parametrize("page_bytes", [4096, 512])
 @pytest.mark.parametrize("n_reads", [1, 2, 17, 64, 65])
 def test_verify_reads_small_batches(dev, oracle, page_bytes, n_reads):
@@ -681,6 +709,45 @@ def test_write_log_hot_pages_and_contract(dev, oracle, delta, spread):
     got = d_pool.cpu().numpy()
     assert (got == want).all()
     assert (u32(crcs) == oracle.page_crcs(want, pb)).all()
+
+
+@pytest.mark.parametrize("delta", [False, True])
+@pytest.mark.parametrize("page_bytes", [4096, 512])
+@pytest.mark.parametrize("n", [1, 7, 64, 65])
+def test_write_log_small_logs(dev, oracle, n, page_bytes, delta):
+    """Small logs (<= 64 writes of at most one page's length take the one-launch
+    path: every wave finds the distinct touched pages from the log in its lanes,
+    then replays the writes touching its page in log order): overlapping writes
+    on a few pages, straddling writes, scattered writes and contract breakers
+    (len 0, len > max_len, past the pool) land exactly as in-order application,
+    and every page CRC equals the oracle's (full rehash or delta update)."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(n * 31 + page_bytes + delta)
+    pool_bytes = 4 << 20
+    host = rng.integers(0, 256, pool_bytes, dtype=np.uint8)
+    d_pool = to_dev(host, dev)
+    crcs = C.page_crc(d_pool, page_bytes)
+    max_len = page_bytes
+    lens = rng.integers(1, max_len + 1, n).astype(np.uint32)
+    dst = rng.integers(0, pool_bytes - max_len, n).astype(np.uint64)
+    dst[: n // 2] = rng.integers(3 * page_bytes - 200, 5 * page_bytes, n // 2)  # overlapping, straddling
+    src_off = rng.integers(0, (1 << 16) - max_len, n).astype(np.uint64)
+    src_data = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
+    bad = set()
+    if n >= 7:
+        lens[1] = 0                          # empty
+        lens[3] = max_len + 1                # longer than max_len
+        dst[5], lens[5] = pool_bytes - 3, 7  # runs past the pool
+        bad = {1, 3, 5}
+    rec = C.log_records(dst, src_off, lens)
+    d_log = torch.from_numpy(rec.view(np.uint8)).to(dev)
+    C.apply_log(d_pool, crcs, to_dev(src_data, dev), d_log, n, max_len, page_bytes, delta=delta)
+    want = host.copy()
+    for i in range(n):
+        if i not in bad:
+            want[dst[i]:dst[i] + lens[i]] = src_data[src_off[i]:src_off[i] + lens[i]]
+    assert (d_pool.cpu().numpy() == want).all()
+    assert (u32(crcs) == oracle.page_crcs(want, page_bytes)).all()
 
 
 @pytest.mark.parametrize("page_bytes", [4096, 512])
