@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Interleaved in-process A/B of cc_crc_ranges_dev's two large-batch schedules
-(CC_RANGE_SCHED=flat | sorted) in the bench's WAL-replay shape (65,536 entries,
-data 1-128 KiB, 28-byte header, 4 KiB slots) and at one fixed entry size.
-Both schedules' outputs must agree entry for entry."""
+"""Interleaved in-process A/B of cc_crc_ranges_dev across libcurvecrc builds
+(arguments LIB.so@name) in the bench's WAL-replay shape (65,536 entries, data
+1-128 KiB, 28-byte header, 4 KiB slots) and at one fixed entry size; all
+outputs must agree entry for entry.  (It also drove the round-2 comparison of
+the flat and size-sorted schedules through CC_RANGE_SCHED, since removed with
+the sorted schedule; the variable is now ignored.)"""
 import os
 import sys
 
