@@ -37,6 +37,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=10, help="untimed steps: the first ~7 launches after idle run slow while clocks ramp")
+    p.add_argument("--clock-warm-ms", type=float, default=1000.0,
+                   help="untimed warm-up floor in ms of estimated work (extra steps beyond --warmup; 0 = none)")
     p.add_argument("--chunks", type=int, default=1024, help="chunks per GPU")
     p.add_argument("--page-bytes", type=int, default=4096)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (rank 0, N=1)")
@@ -608,13 +610,17 @@ def main():
 
     for _ in range(args.warmup):
         step(None)
-    # The GPU clock ramps over the first ~30-40 ms of work after idle (a kernel
-    # trace shows launches 1..10 at 2.77 -> 2.51 ms).  If the W requested warm-up
-    # steps are shorter than that, run extra UNTIMED steps up to ~40 ms, reported
-    # as "clock_warmup_steps".  The count follows from the per-rank bytes only,
-    # so every rank runs the same number of steps (each step holds a collective).
+    # The GPU needs sustained load before it runs at its steady rate: launches
+    # ramp 2.77 -> 2.51 ms over the first ~30 ms after idle, and the first
+    # process on a fresh box stays ~4 % slow (2.57 ms a step) through 100 ms of
+    # warm-up but settles at 2.47 ms after ~2.5 s of it.  The metric is the
+    # steady state of a continuous scan, so when the W requested warm-up steps
+    # are shorter than --clock-warm-ms of work, extra UNTIMED steps run up to
+    # that, reported as "clock_warmup_steps".  The count follows from the
+    # per-rank bytes only, so every rank runs the same number of steps (each
+    # step holds a collective).  The timed region is still exactly K steps.
     est_ms = n * chunk / 6.5e12 * 1e3  # ~6.5 TB/s
-    clock_warm = max(0, int(np.ceil(40.0 / est_ms)) - args.warmup) if args.warmup > 0 else 0
+    clock_warm = max(0, int(np.ceil(args.clock_warm_ms / est_ms)) - args.warmup) if args.warmup > 0 else 0
     for _ in range(clock_warm):
         step(None)
     torch.cuda.synchronize()
@@ -712,6 +718,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "page_crc_kernel<16,0>", "kernel_ms_avg": round(kern_ms, 4),
+                     "kernel_ms_each": [round(a.elapsed_time(b), 4) for a, b in ev],
                      "alg_bytes_per_launch": n_pages * ALG_BYTES_PER_PAGE,
                      "traffic_source": traffic_src,
                      "read_probe_GBps": round(probe_gbs, 1),
