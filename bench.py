@@ -19,6 +19,7 @@ import argparse
 import glob
 import json
 import os
+import sys
 import time
 
 import numpy as np
@@ -45,6 +46,7 @@ def parse():
     p.add_argument("--cpu-sample-chunks", type=int, default=256, help="CPU baseline sample: 16 MiB chunks (256 = 4 GiB)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 traffic passes (use profiles/)")
     p.add_argument("--e2e-gib", type=float, default=1.0, help="pinned host buffer for the e2e leg")
     p.add_argument("--updates", type=int, default=65536, help="config-3 updates per batch")
     p.add_argument("--update-batches", type=int, default=10)
@@ -492,6 +494,52 @@ def wal_replay_leg(pool, args):
             "note": "entry records resident in HBM; alg bytes = data bytes read + 4 B CRC written per entry"}
 
 
+def live_traffic(gib):
+    """HBM bytes per page-kernel launch measured in THIS run: two rocprofv3 PMC
+    passes (FETCH_SIZE, then WRITE_SIZE: one counter group each, never combined
+    with tracing), each over scripts/prof_page.py as a child process on the same
+    pool geometry, under a KILL timeout.  gfx950 correction as
+    MI355X_MICROARCH.md prescribes: bytes = FETCH_SIZE x 1024 x 2 + WRITE_SIZE x
+    1024 (calibrated on this access pattern: profiles/probe_r01.jsonl).
+    Returns (bytes or None, note)."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    if any(k.startswith("ROCPROF") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return None, "this run is itself under a profiler (no PMC pass may nest inside a trace)"
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        return None, "rocprofv3 not found"
+    tmp = tempfile.mkdtemp(prefix="cc_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    med = {}
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, ctr)
+            cmd = ["timeout", "-s", "KILL", "120", exe, "--pmc", ctr, "-d", d, "-o", "run", "--output-format", "csv",
+                   "--", sys.executable, os.path.join(ROOT, "scripts", "prof_page.py"), "--n", "2", "--gib", str(gib)]
+            r = subprocess.run(cmd, cwd=tmp, capture_output=True, text=True, timeout=150,
+                               env=dict(os.environ, TMPDIR=tmp))
+            if r.returncode != 0:
+                return None, f"rocprofv3 --pmc {ctr} exited {r.returncode}"
+            vals = []
+            for root, _, files in os.walk(d):
+                for fn in files:
+                    if fn.endswith("counter_collection.csv"):
+                        for row in csv.DictReader(open(os.path.join(root, fn))):
+                            if "page_crc_kernel<16, 0>" in row["Kernel_Name"] and row["Counter_Name"] == ctr:
+                                vals.append(float(row["Counter_Value"]))
+            if not vals:
+                return None, f"no {ctr} samples for the page kernel"
+            med[ctr] = float(np.median(vals))
+    except Exception as e:  # report, never lose the line
+        return None, f"live PMC failed: {e!r}"
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return med["FETCH_SIZE"] * 1024 * 2 + med["WRITE_SIZE"] * 1024, \
+        "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over scripts/prof_page.py in this run"
+
+
 def load_traffic(args):
     path = args.traffic_json
     if path is None:
@@ -692,9 +740,16 @@ def main():
     per_step_bytes = n * chunk * world
     value = per_step_bytes * args.steps / GiB / el
     achieved = n_pages * ALG_BYTES_PER_PAGE / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic(args)
-    if traffic and abs(traffic / (n_pages * ALG_BYTES_PER_PAGE) - 1.0) > 0.05:
-        traffic, traffic_src = None, f"{traffic_src} profiles a different pool size"  # not this workload
+    traffic, traffic_src = None, None
+    if rank == 0 and world == 1 and not args.no_pmc and pb == 4096:
+        traffic, traffic_src = live_traffic(n * chunk / GiB)
+    if traffic is None:  # the committed PMC summary of the same geometry
+        why = traffic_src
+        traffic, traffic_src = load_traffic(args)
+        if traffic and abs(traffic / (n_pages * ALG_BYTES_PER_PAGE) - 1.0) > 0.05:
+            traffic, traffic_src = None, f"{traffic_src} profiles a different pool size"  # not this workload
+        if why:
+            traffic_src = f"{traffic_src} (live measurement unavailable: {why})"
 
     out = {
         "metric": "GiB/s CRC32C over 4KiB pages (device-resident) + % HBM roofline, 1/2/4/8 GPU",
