@@ -361,6 +361,56 @@ void WriteLogBothModes() {  // an ordered write log from plai
     for (void* q : {d_src, d_log, d_work}) EXPECT(hipFree(q) == hipSuccess);
 }
 
+// INTEGRATION.md 6b/6c per request: one client write, then reads verified one at
+// a time, as WriteChunk / ReadChunk would call them (the one-launch paths)
+void PerRequestWriteAndRead() {
+    const uint32_t pb = 4096;
+    const uint64_t pool_bytes = 1 << 20;
+    std::mt19937_64 rng(77);
+    std::string pool(pool_bytes, '\0'), src(8192, '\0');
+    for (auto& c : pool) c = (char)(rng() & 0xFF);
+    for (auto& c : src) c = (char)(rng() & 0xFF);
+    void *d_pool, *d_pc, *d_src, *d_log, *d_work, *d_reads, *d_bad, *d_total;
+    EXPECT(hipMalloc(&d_pool, pool_bytes) == hipSuccess && hipMalloc(&d_pc, pool_bytes / pb * 4) == hipSuccess);
+    EXPECT(hipMalloc(&d_src, src.size()) == hipSuccess && hipMalloc(&d_log, sizeof(cc_update)) == hipSuccess);
+    EXPECT(hipMemcpy(d_pool, pool.data(), pool_bytes, hipMemcpyHostToDevice) == hipSuccess);
+    EXPECT(hipMemcpy(d_src, src.data(), src.size(), hipMemcpyHostToDevice) == hipSuccess);
+    EXPECT(cc_page_crc_dev(d_pool, pool_bytes / pb, pb, (uint32_t*)d_pc, nullptr) == CC_OK);
+    // one write straddling pages 10 and 11
+    const cc_update w = {10 * pb + 3000, 100, 2500, 0};
+    EXPECT(hipMemcpy(d_log, &w, sizeof w, hipMemcpyHostToDevice) == hipSuccess);
+    const uint64_t work = cc_apply_log_work_bytes(1, pb, pb);
+    EXPECT(work > 0 && hipMalloc(&d_work, work) == hipSuccess);
+    EXPECT(cc_apply_log_delta_dev(d_pool, pool_bytes, pb, d_src, (const cc_update*)d_log, 1, pb, (uint32_t*)d_pc,
+                                  d_work, work, nullptr) == CC_OK);
+    pool.replace(w.dst, w.len, src.substr(w.src, w.len));
+    // then bit rot in page 40 (after its CRC was stored)
+    pool[40 * pb + 9] ^= 0x20;
+    EXPECT(hipMemcpy((char*)d_pool + 40 * pb + 9, &pool[40 * pb + 9], 1, hipMemcpyHostToDevice) == hipSuccess);
+    const cc_range reads[3] = {{10 * pb, 2 * pb}, {36 * pb, 8 * pb}, {100 * pb + 512, 4096}};
+    const uint32_t want[3] = {0, 1, 0};
+    const uint64_t rwork = cc_verify_reads_work_bytes(1);
+    EXPECT(rwork > 0 && hipMalloc(&d_reads, sizeof(cc_range)) == hipSuccess && hipMalloc(&d_bad, 4) == hipSuccess &&
+           hipMalloc(&d_total, 8) == hipSuccess);
+    void* d_rwork;
+    EXPECT(hipMalloc(&d_rwork, rwork) == hipSuccess);
+    for (int i = 0; i < 3; i++) {  // ReadChunk: one read per call
+        uint32_t bad = 7;
+        uint64_t total = 7;
+        EXPECT(hipMemset(d_bad, 0, 4) == hipSuccess && hipMemset(d_total, 0, 8) == hipSuccess);
+        EXPECT(hipMemcpy(d_reads, &reads[i], sizeof(cc_range), hipMemcpyHostToDevice) == hipSuccess);
+        EXPECT(cc_verify_reads_dev(d_pool, pool_bytes, pb, (const cc_range*)d_reads, 1, (const uint32_t*)d_pc,
+                                   (uint32_t*)d_bad, (uint64_t*)d_total, d_rwork, rwork, nullptr) == CC_OK);
+        EXPECT(hipMemcpy(&bad, d_bad, 4, hipMemcpyDeviceToHost) == hipSuccess);
+        EXPECT(hipMemcpy(&total, d_total, 8, hipMemcpyDeviceToHost) == hipSuccess);
+        EXPECT(bad == want[i] && total == want[i]);
+    }
+    std::vector<uint32_t> pc(pool_bytes / pb);
+    EXPECT(hipMemcpy(pc.data(), d_pc, pc.size() * 4, hipMemcpyDeviceToHost) == hipSuccess);
+    EXPECT(pc[10] == Oracle(pool.substr(10 * pb, pb)) && pc[11] == Oracle(pool.substr(11 * pb, pb)));
+    for (void* q : {d_pool, d_pc, d_src, d_log, d_work, d_reads, d_bad, d_total, d_rwork}) EXPECT(hipFree(q) == hipSuccess);
+}
+
 // ---- per-page CRC persistence ------------------------------
 void IntegrityTableAndService() {  // CPU: codec, metapage sn, atomic store / load, service state machine
     std::vector<uint32_t> pc(256);
@@ -554,6 +604,7 @@ int main(int argc, char** argv) {
         {"ScanCopysetMaps", true, ScanCopysetMaps},
         {"PoolScanShardRccl", true, PoolScanShardRccl},
         {"WriteLogBothModes", true, WriteLogBothModes},
+        {"PerRequestWriteAndRead", true, PerRequestWriteAndRead},
         {"IntegrityTableAndService", false, IntegrityTableAndService},
         {"IntegrityWritePath", true, IntegrityWritePath},
     };
