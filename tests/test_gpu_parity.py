@@ -750,6 +750,93 @@ def test_write_log_small_logs(dev, oracle, n, page_bytes, delta):
     assert (u32(crcs) == oracle.page_crcs(want, page_bytes)).all()
 
 
+@pytest.mark.parametrize("seed", range(24))
+def test_write_log_random_configs(dev, oracle, seed):
+    """Randomised write logs across the geometry space -- page size 256 B..8 KiB,
+    1..3000 writes (both the one-launch and the hash-table path), max_len up to
+    two pages, overlap density, contract breakers, full or delta CRC mode --
+    against in-order host application and the oracle's page CRCs."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(1000 + seed)
+    pb = int(rng.choice([256, 512, 1024, 4096, 8192]))
+    n = int(rng.choice([1, 2, 5, 33, 64, 65, 300, 3000]))
+    max_len = int(rng.integers(1, 2 * pb + 1))
+    delta = bool(rng.integers(0, 2))
+    pool_bytes = int(rng.choice([1, 2, 4])) << 20
+    host = rng.integers(0, 256, pool_bytes, dtype=np.uint8)
+    d_pool = to_dev(host, dev)
+    crcs = C.page_crc(d_pool, pb)
+    lens = rng.integers(1, max_len + 1, n).astype(np.uint32)
+    span = int(rng.choice([pool_bytes - max_len - 1, 8 * pb]))  # scattered or piled up
+    dst = rng.integers(0, max(1, span), n).astype(np.uint64)
+    src_off = rng.integers(0, (1 << 16) - max_len - 1, n).astype(np.uint64)
+    src_data = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
+    bad = set()
+    for i in rng.choice(n, size=min(n, int(rng.integers(0, 4))), replace=False):
+        kind = int(rng.integers(0, 3))
+        if kind == 0:
+            lens[i] = 0
+        elif kind == 1:
+            lens[i] = max_len + 1
+        else:
+            dst[i], lens[i] = pool_bytes - 1, 2
+        bad.add(int(i))
+    rec = C.log_records(dst, src_off, lens)
+    d_log = torch.from_numpy(rec.view(np.uint8)).to(dev)
+    C.apply_log(d_pool, crcs, to_dev(src_data, dev), d_log, n, max_len, pb, delta=delta)
+    want = host.copy()
+    for i in range(n):
+        if i not in bad:
+            want[dst[i]:dst[i] + lens[i]] = src_data[src_off[i]:src_off[i] + lens[i]]
+    assert (d_pool.cpu().numpy() == want).all(), (pb, n, max_len, delta)
+    assert (u32(crcs) == oracle.page_crcs(want, pb)).all(), (pb, n, max_len, delta)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_verify_reads_random_configs(dev, oracle, seed):
+    """Randomised read batches (1..2000 reads: the one-launch and the count +
+    scan paths; page sizes 256 B..8 KiB; aligned, unaligned, empty, past-the-end
+    and whole-pool reads) over a pool with random corrupted pages: exact
+    per-read bad-page counts."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(2000 + seed)
+    pb = int(rng.choice([256, 512, 1024, 4096, 8192]))
+    n_pages = int(rng.integers(64, 3000))
+    host = rng.integers(0, 256, n_pages * pb, dtype=np.uint8)
+    stored = to_dev(oracle.page_crcs(host, pb).view(np.int32), dev)
+    pool = to_dev(host, dev)
+    bad_pages = set(int(p) for p in rng.choice(n_pages, size=int(rng.integers(0, 12)), replace=False))
+    for p in bad_pages:
+        pool[p * pb + int(rng.integers(0, pb))] ^= 0x04
+    total_bytes = n_pages * pb
+    n = int(rng.choice([1, 3, 64, 65, 500, 2000]))
+    reads = []
+    for _ in range(n):
+        k = int(rng.integers(0, 10))
+        if k == 0:
+            reads.append((int(rng.integers(0, total_bytes)), 0))
+        elif k == 1:
+            o = int(rng.integers(total_bytes - pb, total_bytes))
+            reads.append((o, total_bytes - o + int(rng.integers(1, 100))))  # past the end
+        elif k == 2:
+            reads.append((0, total_bytes))
+        else:
+            o = int(rng.integers(0, total_bytes - 1))
+            reads.append((o, int(rng.integers(1, min(48 * pb, total_bytes - o) + 1))))
+    off, ln = zip(*reads)
+    bad, total = C.verify_reads(pool, stored, off, ln, pb)
+    got = bad.cpu().numpy()
+    want_total = 0
+    for i, (o, m) in enumerate(reads):
+        if o + m > total_bytes:
+            assert got[i] == -1, (i, o, m)
+            continue
+        want = len(set(range(o // pb, (o + m - 1) // pb + 1)) & bad_pages) if m else 0
+        want_total += want
+        assert got[i] == want, (i, o, m, pb, n)
+    assert int(total.item()) == want_total
+
+
 @pytest.mark.parametrize("page_bytes", [4096, 512])
 def test_write_log_delta_keeps_latent_corruption(dev, oracle, page_bytes):
     """cc_apply_log_delta_dev on a pool where some pages were corrupted after
