@@ -11,7 +11,10 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from curve_amd import crc as C  # noqa: E402
+from curve_amd import _lib, crc as C  # noqa: E402
+
+if len(sys.argv) > 1:  # a libcurvecrc variant to load instead of the in-tree one
+    _lib.LIB_PATH = os.path.abspath(sys.argv[1])
 
 dev = torch.device("cuda", 0)
 pb = 4096
@@ -36,7 +39,7 @@ def timed(fn, reps=50):
 
 
 out = {}
-for n in (1, 16, 256):
+for n in (1, 16, 256, 1024, 8192):
     first = rng.integers(0, (16 << 30) // pb - 32, n)
     npg = rng.integers(1, 33, n)
     d_reads = torch.from_numpy(np.stack([first * pb, npg * pb], axis=1).reshape(-1).astype(np.int64)).to(dev)
