@@ -362,6 +362,49 @@ def test_page_load_probe_diagnostic(dev):
     assert sorted(torch.nonzero(a != b).flatten().tolist()) == [12345, n - 1]
 
 
+def test_full_size_config1_scan_step(dev, oracle):
+    """BASELINE config 1 at full size through the bench's own step
+    (cc_pool_scan_dev over 1024 x 16 MiB chunk files, 64 copysets), checked by
+    size-independent properties against the oracle on the host copy: the
+    ordered fold of all 4M page CRCs equals CRC32 of the whole 16 GiB; every
+    copyset digest equals CopysetNode::GetHash's sorted-name chain over its 16
+    files (metapage || data, chained from 0); 32 sampled chunks' four 4 MiB
+    slice CRCs equal the oracle's; 64 sampled pages' CRCs equal the oracle's."""
+    from curve_amd import crc as C
+    from curve_amd.pool import copyset_layout, pool_scan
+    from curve_amd.scan import DevicePool, chunk_file_name
+    n, chunk, meta_sz, G = 1024, C.CHUNK_SIZE, C.META_PAGE_SIZE, 64
+    data = torch.empty((n, chunk), dtype=torch.uint8, device=dev).random_(0, 256)
+    meta = torch.zeros((n, meta_sz), dtype=torch.uint8, device=dev)
+    meta[:, 0] = 2
+    meta[:, 1:9].random_(0, 256)
+    pool = DevicePool(data, meta, list(range(n)), page_bytes=4096)
+    lay = copyset_layout(list(range(n)), [i % G for i in range(n)], [chunk + meta_sz] * n)
+    after_mult = C.xpow8(torch.tensor(lay.after_bytes, dtype=torch.int64, device=dev))
+    group = torch.tensor(lay.group, dtype=torch.int32, device=dev)
+    digest = torch.full((lay.n_groups,), 7, dtype=torch.int32, device=dev)
+    pool_scan(pool, after_mult, group, digest)
+    whole = C.fold(pool.page_crcs, pool.page_crcs.numel(), 4096)
+    torch.cuda.synchronize()
+    hd, hm = data.cpu().numpy(), meta.cpu().numpy()
+    assert int(u32(whole)[0]) == oracle.crc32c(hd.reshape(-1))
+    dig = u32(digest)
+    for g in range(G):
+        mem = sorted((chunk_file_name(i), i) for i in range(n) if i % G == g)
+        crc = 0
+        for _, i in mem:  # CopysetNode::GetHash: whole files in name order, one chained CRC
+            crc = oracle.crc32c(hd[i], oracle.crc32c(hm[i], crc))
+        assert int(dig[lay.group[mem[0][1]]]) == crc, g
+    rng = np.random.default_rng(0xC1)
+    sl = u32(pool.slice_crcs).reshape(n, 4)
+    for i in rng.choice(n, 32, replace=False):
+        ref = oracle.scan_slices(hm[i].tobytes(), hd[i].tobytes(), C.SCAN_SIZE)
+        assert [int(x) for x in sl[i]] == [c for (_, _, c) in ref[1:]]
+    pc = u32(pool.page_crcs)
+    for p in rng.choice(pc.size, 64, replace=False):
+        assert int(pc[p]) == oracle.crc32c(hd.reshape(-1)[p * 4096:(p + 1) * 4096])
+
+
 def test_write_log_full_size_config3(dev, oracle):
     """BASELINE config 3 at full size: a 16 GiB pool (1024 chunks), 65,536 random
     512 B-4 KiB writes in one log (unaligned, straddling, some overlapping).
