@@ -937,6 +937,27 @@ def test_crc_ranges_large_batch(dev, oracle):
     assert bad.size == 0, (bad[:10], offs[bad[:3]], lens[bad[:3]])
 
 
+def test_wal_replay_full_batch(dev, oracle):
+    """The bench's WAL-replay batch at full size: 65,536 entries laid out as
+    CurveSegment::append writes them (28-byte header, 1-128 KiB of data, each
+    entry padded to 4 KiB) over ~4.3 GB, one cc_crc_ranges_dev call -- every
+    entry's data CRC equals the oracle's (static shares, segments cut at share
+    boundaries and the dynamic tail all exercised)."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(0x3A1)
+    n = 65536
+    real = rng.integers(1, (128 << 10) + 1, n).astype(np.uint64)
+    slot = (28 + real + 4095) // 4096 * 4096
+    offs = np.concatenate([[0], np.cumsum(slot)[:-1]]).astype(np.uint64) + 4096 + 28
+    size = int(offs[-1] + real[-1] + 4096)
+    d = torch.empty(size, dtype=torch.uint8, device=dev).random_(0, 256)
+    got = u32(C.crc_ranges(d, offs, real))
+    host = d.cpu().numpy()
+    want = np.array([oracle.crc32c(host[o:o + l]) for o, l in zip(offs.tolist(), real.tolist())], dtype=np.uint32)
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, (bad[:10], offs[bad[:3]], real[bad[:3]])
+
+
 @pytest.mark.parametrize("shape", ["tiny_many", "giants"])
 def test_crc_ranges_flat_schedule(dev, oracle, shape):
     """Large batches through cc_crc_ranges_dev's flat block schedule (every
