@@ -493,13 +493,13 @@ def test_verify_reads_batch(dev, oracle, page_bytes):
 
 
 def test_verify_reads_full_batch_with_corruption(dev):
-    """The bench's read-verify shape at full batch size (65,536 reads of 1-32
-    pages over a 2 GiB pool): with 300 corrupted pages every read reports
-    exactly the corrupted pages it touches -- reads split over waves at page
-    granularity and the dynamic tail included -- and the total matches."""
+    """The bench's read-verify shape at full size (65,536 reads of 1-32 pages
+    over the 16 GiB pool): with 300 corrupted pages every read reports exactly
+    the corrupted pages it touches -- reads split over waves at page granularity
+    and the dynamic tail included -- and the total matches."""
     from curve_amd import crc as C
     pb, n = 4096, 65536
-    n_pages = (2 << 30) // pb
+    n_pages = (16 << 30) // pb
     pool = torch.empty(n_pages * pb, dtype=torch.uint8, device=dev).random_(0, 256)
     stored = C.page_crc(pool, pb)
     rng = np.random.default_rng(0xBAD)
