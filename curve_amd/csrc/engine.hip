@@ -520,7 +520,7 @@ int pool_page_launches(const void* d_data, uint64_t n_data_pages, uint32_t page_
     m.zero[1] = d_digest;
     m.zero_words[1] = d_digest ? digest_words : 0;
     geometry_for(c.get(), n_meta, &m);  // static walk (a tail would need a counter of its own)
-    e = launch_page_crc(m, s);
+    e = launch_page_meta(m, s);
     if (e == hipSuccess && ev_begin) e = hipEventRecord(static_cast<hipEvent_t>(ev_begin), s);
     if (e == hipSuccess) {
         PageLaunch a = {};

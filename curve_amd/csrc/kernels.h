@@ -63,6 +63,8 @@ hipError_t launch_page_verify(const PageLaunch& a, hipStream_t s);
 // the page kernel with its CRC arithmetic replaced by a rotate-XOR (4 KiB pages):
 // the same schedule, loads and stores -- the ceiling the real kernel is held to
 hipError_t launch_page_load_probe(const PageLaunch& a, hipStream_t s);
+// the scan step's metapage pass (a separate instantiation, same code as compute)
+hipError_t launch_page_meta(const PageLaunch& a, hipStream_t s);
 
 struct FoldLaunch {
     const uint32_t* crcs;

@@ -179,7 +179,7 @@ template <int MODE>
 __device__ __forceinline__ void flush_tile(uint32_t acc, uint64_t tile_first, uint32_t cnt, uint32_t lane,
                                            uint32_t* __restrict__ out, const uint32_t* __restrict__ expected,
                                            const VerifySink& vs) {
-    if (MODE != 1) {  // compute (0) and the load-only probe (2) store the tile
+    if (MODE != 1) {  // compute (0; 3 = the metapage pass) and the load-only probe (2) store the tile
 #if CC_STORE == 1  // diagnostic: no store (wrong output), keeps acc live
         asm volatile("" ::"v"(acc));
 #elif CC_STORE == 2
@@ -1972,6 +1972,18 @@ hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_page_crc(const PageLaunch& a, hipStream_t s) { return launch_page<0>(a, s); }
+
+// The scan step's metapage pass: the compute kernel as its own instantiation
+// (MODE 3 = MODE 0), so a kernel trace reports the 1,024-page metapage launches
+// apart from the 16 GiB data launches instead of averaging the two.
+hipError_t launch_page_meta(const PageLaunch& a, hipStream_t s) {
+    if (a.words_per_lane != 16) return launch_page<0>(a, s);
+    const ZeroRanges zr = {{a.zero[0], a.zero[1]}, {a.zero[0] ? a.zero_words[0] : 0, a.zero[1] ? a.zero_words[1] : 0}};
+    hipLaunchKernelGGL((page_crc_kernel<16, 3>), dim3(a.blocks), dim3(kBlockThreads), 0, s, a.pages, a.n_pages,
+                       static_cast<const uint4*>(a.image), a.kconst, a.out, a.expected, a.sink, a.tile_shift,
+                       a.dyn_ctr, a.static_tiles, zr);
+    return hipGetLastError();
+}
 
 hipError_t launch_page_load_probe(const PageLaunch& a, hipStream_t s) {
     if (a.words_per_lane != 16) return hipErrorInvalidValue;  // 4 KiB pages only
