@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--stream-chunks-per-rank", type=int, default=2000, help="N>1: streamed chunks per rank")
     p.add_argument("--file-chunks", type=int, default=128, help="datastore read-path leg (0 = skip)")
     p.add_argument("--wal-entries", type=int, default=65536, help="WAL replay leg: entries per batch (0 = skip)")
+    p.add_argument("--comm-timeout-ms", type=int, default=60000, help="N>1: bound on the native RCCL init")
     p.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/traffic_*.json)")
     return p.parse_args()
 
@@ -602,7 +603,7 @@ def main():
             dist.init_process_group(backend)
 
     from curve_amd import crc as C
-    from curve_amd.pool import comm_from_dist, copyset_layout, pool_scan, reduce_digests, shard_range
+    from curve_amd.pool import agreed_comm, copyset_layout, pool_scan, reduce_digests, shard_range
     from curve_amd.scan import DevicePool
 
     pb = args.page_bytes
@@ -633,14 +634,13 @@ def main():
 
     stream = torch.cuda.current_stream()
     # the digest exchange at N>1: libcurvecrc's own RCCL communicator (what a
-    # C++ chunkserver binds); torch.distributed only carries its 128-byte id
+    # C++ chunkserver binds); torch.distributed only carries its 128-byte id.
+    # Init is bounded (--comm-timeout-ms) and the ranks agree on ONE path: if
+    # any rank's native init failed, every rank uses torch.distributed (a mix
+    # would pair ncclAllGather with all_gather_into_tensor and hang).
     comm, comm_note = None, None
     if world > 1:
-        try:
-            comm = comm_from_dist(dist)
-            comm_note = "native RCCL (cc_comm_init + cc_digest_allreduce_dev)"
-        except Exception as e:  # both paths are RCCL; say which one ran
-            comm_note = f"torch.distributed all_gather (native comm init failed: {e})"
+        comm, comm_note = agreed_comm(dist, device=dev, timeout_ms=args.comm_timeout_ms)
     # per timed step: one event pair around the page kernel, recorded inside the
     # native call on `stream` (created up front: the call re-records them)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -693,7 +693,15 @@ def main():
         local = torch.zeros_like(digest)
         pool_scan(pool, after_mult, group, local, comm=None, stream=stream)
         digest_check = bool(torch.equal(native, reduce_digests(local, dist)))
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_each = [a.elapsed_time(b) for a, b in ev]
+    kern_ms = float(np.mean(kern_each))
+    # every rank's mean page-kernel time: the aggregate roofline is set by the slowest
+    rank_kern = [kern_ms]
+    if world > 1:
+        kt = torch.tensor([kern_ms], dtype=torch.float64, device="cpu" if backend == "gloo" else dev)
+        ga = torch.empty(world, dtype=torch.float64, device=kt.device)
+        dist.all_gather_into_tensor(ga, kt)
+        rank_kern = [float(x) for x in ga.cpu().tolist()]
 
     # verify pass (after the timed region): every page must match
     # (4 back-to-back calls, the first untimed: one call right after a host sync
@@ -767,13 +775,17 @@ def main():
         "data": "synthetic (uniform random bytes generated in HBM)",
         "config": {"workload": f"{n} x 16 MiB chunk files per GPU (+4 KiB metapages), 4 KiB pages: "
                                "page CRC + fused epilogue (4 MiB slice CRCs, file CRC, per-copyset digest)"
-                               + (" + RCCL all_gather of digests" if world > 1 else "") + " (one cc_pool_scan_dev call)",
+                               + (" + digest all_gather inside the one cc_pool_scan_dev call (native RCCL comm)" if comm is not None else
+                                  " (one cc_pool_scan_dev call) + digest all_gather via torch.distributed"
+                                  if world > 1 else " (one cc_pool_scan_dev call)"),
                    "chunks_per_gpu": n, "page_bytes": pb, "copysets": N_COPYSETS,
                    "parallelism": f"chunk-range shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "page_crc_kernel<16,0>", "kernel_ms_avg": round(kern_ms, 4),
-                     "kernel_ms_each": [round(a.elapsed_time(b), 4) for a, b in ev],
+                     "kernel_ms_each": [round(x, 4) for x in kern_each],
+                     "kernel_ms_median": round(float(np.median(kern_each)), 4),
+                     "kernel_spread_pct": round((max(kern_each) - min(kern_each)) / min(kern_each) * 100, 2),
                      "alg_bytes_per_launch": n_pages * ALG_BYTES_PER_PAGE,
                      "traffic_source": traffic_src,
                      "read_probe_GBps": round(probe_gbs, 1),
@@ -784,6 +796,15 @@ def main():
     }
     if world > 1:
         out["digest_exchange"] = {"path": comm_note, "matches_torch_distributed": digest_check}
+        # aggregate roofline over the node: every rank's algorithmic bytes over the
+        # slowest rank's page-kernel time, against N x the per-GPU peak
+        agg = world * n_pages * ALG_BYTES_PER_PAGE / (max(rank_kern) * 1e-3) / 1e9
+        out["roofline"].update({"aggregate_achieved": round(agg, 1), "aggregate_peak": HBM_PEAK_GBS * world,
+                                "aggregate_frac": round(agg / (HBM_PEAK_GBS * world), 4),
+                                "rank_kernel_ms": [round(x, 4) for x in rank_kern],
+                                "rank_kernel_ms_min": round(min(rank_kern), 4),
+                                "rank_kernel_ms_max": round(max(rank_kern), 4),
+                                "note": "frac/achieved/kernel_ms_* are rank 0's; aggregate_* use every rank"})
     if rank == 0 and world == 1 and args.updates:
         out["partial_write"] = partial_write_leg(pool, args)
     if rank == 0 and world == 1 and args.reads:

@@ -23,6 +23,7 @@ CC_ECORRUPT = -74
 CC_ECOMM = -71
 CC_EIO = -5001
 CC_ESTALE = -116
+CC_ETIMEDOUT = -110
 CC_ENOENT = -2
 CC_COMM_ID_BYTES = 128
 
@@ -52,7 +53,7 @@ class IoVec(ctypes.Structure):  # struct iovec
 
 class CcPcrcHeader(ctypes.Structure):  # include/curve_crc.h cc_pcrc_header
     _fields_ = [("page_bytes", _u32), ("n_pages", _u32), ("chunk_sn", _u64), ("data_mtime_ns", ctypes.c_int64),
-                ("data_size", _u64)]
+                ("data_size", _u64), ("stamp_ns", ctypes.c_int64)]
 
 
 class CcIntegrityOpts(ctypes.Structure):
@@ -122,7 +123,9 @@ SIGNATURES = {
     "cc_verify_reads_dev": (_int, [_vp, _u64, _u32, _vp, _u64, _vp, _vp, _vp, _vp, _u64, _vp]),
     "cc_comm_unique_id": (_int, [_vp, _sz]),
     "cc_comm_init": (_int, [ctypes.POINTER(_vp), _int, _int, _vp, _sz]),
+    "cc_comm_init_timeout": (_int, [ctypes.POINTER(_vp), _int, _int, _vp, _sz, _u32]),
     "cc_comm_destroy": (_int, [_vp]),
+    "cc_comm_abort": (_int, [_vp]),
     "cc_comm_size": (_int, [_vp]),
     "cc_comm_rank": (_int, [_vp]),
     "cc_digest_allreduce_dev": (_int, [_vp, _vp, _u64, _vp]),
@@ -133,12 +136,65 @@ SIGNATURES = {
     "cc_chunk_meta_sn": (_int, [_vp, _u32, ctypes.POINTER(_u64)]),
     "cc_pcrc_store": (_int, [ctypes.c_char_p, _u32, ctypes.c_char_p, _vp, _u32, _u32]),
     "cc_pcrc_load": (_int, [ctypes.c_char_p, ctypes.POINTER(CcPcrcHeader), _vp, _u32]),
+    "cc_pcrc_store_expect": (_int, [ctypes.c_char_p, _u32, ctypes.c_char_p, _vp, _u32, _u32,
+                                    ctypes.POINTER(CcPcrcHeader)]),
+    "cc_pcrc_is_racy": (_int, [ctypes.POINTER(CcPcrcHeader)]),
     "cc_integrity_check": (_int, [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p), _u64,
                                   ctypes.POINTER(CcIntegrityOpts), ctypes.POINTER(CcIntegrityResult), _vp, _u64,
                                   ctypes.POINTER(_u64)]),
 }
 
+# ---- the host layer's C ABI (include/curve_integrity.h, curve_amd/host/libcurvehost.so)
+HOST_LIB_PATH = os.path.join(_HERE, "host", "libcurvehost.so")
+
+
+class CcIsvcOpts(ctypes.Structure):
+    _fields_ = [("chunk_bytes", _u32), ("meta_bytes", _u32), ("page_bytes", _u32), ("batch", _u32),
+                ("io_threads", _u32), ("create_missing", _u32), ("refresh_stale", _u32)]
+
+
+class CcIsvcJob(ctypes.Structure):
+    _fields_ = [("id", ctypes.c_int32), ("copyset", ctypes.c_int32), ("state", ctypes.c_int32),
+                ("progress", ctypes.c_int32), ("sched_time", ctypes.c_int32), ("start_time", ctypes.c_int32),
+                ("n_results", _u64), ("error", ctypes.c_char * 256)]
+
+
+class CcIsvcFile(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 256), ("status", ctypes.c_int32), ("table_state", _u32),
+                ("bad_pages", _u32), ("n_bad_listed", _u32), ("first_bad", ctypes.c_int64)]
+
+
+HOST_SIGNATURES = {
+    "cc_isvc_create": (_vp, [ctypes.POINTER(CcIsvcOpts)]),
+    "cc_isvc_destroy": (None, [_vp]),
+    "cc_isvc_schedule": (_int, [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p]),
+    "cc_isvc_cancel": (_int, [_vp, ctypes.c_int32]),
+    "cc_isvc_pause": (_int, [_vp, ctypes.c_int32]),
+    "cc_isvc_resume": (_int, [_vp, ctypes.c_int32]),
+    "cc_isvc_list": (_int, [_vp, _vp, _u64, ctypes.POINTER(_u64)]),
+    "cc_isvc_job_info": (_int, [_vp, ctypes.c_int32, ctypes.POINTER(CcIsvcJob)]),
+    "cc_isvc_file_result": (_int, [_vp, ctypes.c_int32, _u64, ctypes.POINTER(CcIsvcFile), _vp, _u64]),
+    "cc_isvc_wait": (_int, [_vp, ctypes.c_int32, ctypes.c_int32]),
+}
+
 _lib = None
+_host = None
+
+
+def host_lib():
+    """libcurvehost.so (the C++ IntegrityService behind include/curve_integrity.h)."""
+    global _host
+    if _host is None:
+        lib()  # libcurvecrc first (the host library links it)
+        if not os.path.exists(HOST_LIB_PATH):
+            raise OSError(f"{HOST_LIB_PATH} missing: build it with `make -C {os.path.join(_HERE, 'host')}`")
+        H = ctypes.CDLL(HOST_LIB_PATH)
+        for name, (res, args) in HOST_SIGNATURES.items():
+            f = getattr(H, name)
+            f.restype = res
+            f.argtypes = args
+        _host = H
+    return _host
 
 
 class CurveCrcError(RuntimeError):

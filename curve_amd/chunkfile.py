@@ -116,10 +116,12 @@ def read_into(path: str, dst) -> int:
 
 
 def copyset_hash_dir(data_dir: str, chunk_size: int = C.CHUNK_SIZE, meta_size: int = C.META_PAGE_SIZE,
-                     io_threads: int = 8) -> str:
+                     io_threads: int = 8, page_bytes: int = C.PAGE_SIZE) -> str:
     """CopysetNode::GetHash over a real data directory: list, std::sort the
     names, chain CRC32 over whole files.  Chunk files (meta || data of the
-    configured geometry) are read AND hashed by the engine (cc_scan_files:
+    configured geometry: chunkserver.conf's chunk_size / meta_page_size, and
+    block_size as the engine's page -- 4096 or 512, datastore_mock_unittest.cpp:4270-4279)
+    are read AND hashed by the engine (cc_scan_files:
     native pread into pinned staging overlapped with the GPU scan); any other
     file -- or one the engine could not read -- is hashed on the CPU primitive.
     The chain is assembled with crc32c_combine in sorted-name order, identical
@@ -133,7 +135,7 @@ def copyset_hash_dir(data_dir: str, chunk_size: int = C.CHUNK_SIZE, meta_size: i
     chunk_idx = [i for i, s in enumerate(sizes) if s == fsize]
     if chunk_idx:
         st, _, _, fc = C.scan_files([os.path.join(data_dir, names[i]) for i in chunk_idx], chunk_size, meta_size,
-                                    C.PAGE_SIZE, min(C.SCAN_SIZE, chunk_size), io_threads)
+                                    page_bytes, min(C.SCAN_SIZE, chunk_size), io_threads)
         for k, i in enumerate(chunk_idx):
             if st[k] == 0:
                 file_crc[i] = int(fc[k])

@@ -400,6 +400,7 @@ const char* cc_strerror(int code) {
         case CC_ECOMM: return "RCCL communication error";
         case CC_EIO: return "I/O error";
         case CC_ESTALE: return "per-page CRC table is stale";
+        case CC_ETIMEDOUT: return "timed out";
         default: return "unknown error";
     }
 }

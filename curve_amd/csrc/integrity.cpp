@@ -16,20 +16,25 @@
 //   24  chunk_sn u64          metapage sn of the chunk when the table was written
 //   32  data_mtime_ns i64     the chunk FILE's st_mtim then
 //   40  data_size u64         the chunk file's size then
-//   48  reserved u64
+//   48  stamp_ns i64          CLOCK_REALTIME when the CRCs' bytes were known current
+//                             (racy-table rule, include/curve_crc.h cc_pcrc_is_racy)
 //   56  header_crc u32        CRC32C of bytes [0, 56)
 //   60  table_crc u32         CRC32C of the page-CRC array
 //   64  page CRCs, n_pages x u32 (CRC32 of each data page, the file's bytes
 //       [meta_bytes + i * page_bytes, +page_bytes))
 // A table is only ever used to condemn data when it provably describes the
-// chunk's current bytes: both CRCs check, the geometry matches, and the chunk's
-// sn, mtime and size are the ones recorded.  Otherwise it is reported (corrupt
-// / stale) and, by policy, rebuilt -- never turned into bad pages.
+// chunk's current bytes: both CRCs check, the geometry matches, the chunk's
+// sn, mtime and size are the ones recorded, and the table is not racy (its
+// stamp is at least one coarse-clock tick after the recorded mtime, so no
+// write can have kept that mtime after the CRCs were taken).  Otherwise it is
+// reported (corrupt / stale) and, by policy, rebuilt -- never turned into bad
+// pages.
 #include <errno.h>
 #include <fcntl.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <string>
@@ -87,6 +92,24 @@ int write_full(int fd, const void* src, size_t n) {
 
 int64_t mtime_ns(const struct stat& sb) { return (int64_t)sb.st_mtim.tv_sec * 1000000000ll + sb.st_mtim.tv_nsec; }
 
+int64_t now_ns() {
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    return (int64_t)ts.tv_sec * 1000000000ll + ts.tv_nsec;
+}
+
+// One tick of the clock file timestamps come from (the kernel's coarse
+// realtime clock: a jiffy, 1-10 ms); at least 1 ms, at most 1 s.
+int64_t mtime_tick_ns() {
+    static const int64_t tick = [] {
+        struct timespec r;
+        int64_t t = 0;
+        if (clock_getres(CLOCK_REALTIME_COARSE, &r) == 0) t = (int64_t)r.tv_sec * 1000000000ll + r.tv_nsec;
+        return t < 1000000 ? 1000000 : (t > 1000000000 ? 1000000000 : t);
+    }();
+    return tick;
+}
+
 // Chunk file identity for staleness: sn from the metapage, mtime + size from stat.
 struct ChunkId {
     uint64_t sn = 0;
@@ -135,6 +158,7 @@ int cc_pcrc_encode(const cc_pcrc_header* h, const uint32_t* page_crcs, void* out
     put64(p + 24, h->chunk_sn);
     put64(p + 32, (uint64_t)h->data_mtime_ns);
     put64(p + 40, h->data_size);
+    put64(p + 48, (uint64_t)h->stamp_ns);
     memcpy(p + CC_PCRC_HEADER_BYTES, page_crcs, 4ull * h->n_pages);
     put32(p + 56, crc32c_value(p, 56));
     put32(p + 60, crc32c_value(p + CC_PCRC_HEADER_BYTES, 4ull * h->n_pages));
@@ -154,6 +178,7 @@ int cc_pcrc_decode(const void* buf, uint64_t bytes, cc_pcrc_header* h, uint32_t*
     h->chunk_sn = get64(p + 24);
     h->data_mtime_ns = (int64_t)get64(p + 32);
     h->data_size = get64(p + 40);
+    h->stamp_ns = (int64_t)get64(p + 48);
     if (page_crcs) {
         if (n > max_pages) return CC_EINVAL;
         memcpy(page_crcs, p + CC_PCRC_HEADER_BYTES, 4ull * n);
@@ -185,6 +210,11 @@ int cc_chunk_meta_sn(const void* metapage, uint32_t bytes, uint64_t* sn) {
     return CC_OK;
 }
 
+int cc_pcrc_is_racy(const cc_pcrc_header* h) {
+    if (!h) return CC_EINVAL;
+    return h->data_mtime_ns + mtime_tick_ns() > h->stamp_ns ? 1 : 0;
+}
+
 int cc_pcrc_load(const char* table_path, cc_pcrc_header* h, uint32_t* page_crcs, uint32_t max_pages) {
     if (!table_path || !h) return CC_EINVAL;
     const int fd = open(table_path, O_RDONLY | O_CLOEXEC);
@@ -195,15 +225,34 @@ int cc_pcrc_load(const char* table_path, cc_pcrc_header* h, uint32_t* page_crcs,
         close(fd);
         return e;
     }
-    if (sb.st_size > (off_t)cc_pcrc_encoded_bytes(0xFFFFFFFFu)) {
+    // never allocate what a valid table for this caller cannot need: a corrupt
+    // or hostile sidecar must not make a job step read gigabytes
+    const uint64_t cap = page_crcs ? cc_pcrc_encoded_bytes(max_pages) : CC_PCRC_HEADER_BYTES;
+    if (page_crcs && (uint64_t)sb.st_size > cap) {
         close(fd);
         return CC_ECORRUPT;
     }
-    std::vector<unsigned char> buf((size_t)sb.st_size);
-    const int rc = buf.empty() ? 0 : read_full(fd, buf.data(), buf.size(), 0);
+    if ((uint64_t)sb.st_size < CC_PCRC_HEADER_BYTES || sb.st_size > (off_t)cc_pcrc_encoded_bytes(0xFFFFFFFFu)) {
+        close(fd);
+        return CC_ECORRUPT;
+    }
+    std::vector<unsigned char> buf(page_crcs ? (size_t)sb.st_size : (size_t)CC_PCRC_HEADER_BYTES);
+    const int rc = read_full(fd, buf.data(), buf.size(), 0);
     close(fd);
     if (rc) return rc;
-    return cc_pcrc_decode(buf.data(), buf.size(), h, page_crcs, max_pages);
+    if (page_crcs) return cc_pcrc_decode(buf.data(), buf.size(), h, page_crcs, max_pages);
+    // header only: its own CRC, and a length that matches the file
+    unsigned char* p = buf.data();
+    if (memcmp(p, kMagic, 8) != 0 || crc32c_value(p, 56) != get32(p + 56) || get32(p + 8) != kVersion ||
+        (uint64_t)sb.st_size != cc_pcrc_encoded_bytes(get32(p + 16)))
+        return CC_ECORRUPT;
+    h->page_bytes = get32(p + 12);
+    h->n_pages = get32(p + 16);
+    h->chunk_sn = get64(p + 24);
+    h->data_mtime_ns = (int64_t)get64(p + 32);
+    h->data_size = get64(p + 40);
+    h->stamp_ns = (int64_t)get64(p + 48);
+    return CC_OK;
 }
 
 }  // extern "C"
@@ -212,9 +261,10 @@ namespace {
 // The store behind cc_pcrc_store.  With `expect`, the chunk's identity read here
 // must still be the one the CRCs were computed under (else CC_ESTALE, nothing
 // written): a write landing between a job's read and its table refresh must not
-// get a table of the bytes before it.
+// get a table of the bytes before it.  `stamp` is when those bytes were known
+// current (0 = now).
 int store_table(const char* chunk_path, uint32_t meta_bytes, const char* table_path, const uint32_t* page_crcs,
-                uint32_t n_pages, uint32_t page_bytes, const ChunkId* expect) {
+                uint32_t n_pages, uint32_t page_bytes, const ChunkId* expect, int64_t stamp = 0) {
     if (!chunk_path || !table_path || (n_pages && !page_crcs) || page_bytes == 0 || meta_bytes == 0)
         return CC_EINVAL;
     ChunkId id;
@@ -222,7 +272,7 @@ int store_table(const char* chunk_path, uint32_t meta_bytes, const char* table_p
     if (rc) return rc;
     if (id.size != (uint64_t)meta_bytes + (uint64_t)n_pages * page_bytes) return CC_EINVAL;
     if (expect && (id.sn != expect->sn || id.mtime != expect->mtime || id.size != expect->size)) return CC_ESTALE;
-    cc_pcrc_header h = {page_bytes, n_pages, id.sn, id.mtime, id.size};
+    cc_pcrc_header h = {page_bytes, n_pages, id.sn, id.mtime, id.size, stamp ? stamp : now_ns()};
     std::vector<unsigned char> buf(cc_pcrc_encoded_bytes(n_pages));
     if ((rc = cc_pcrc_encode(&h, page_crcs, buf.data(), buf.size()))) return rc;
     // atomic replace: a reader sees the old table or the new one, never a torn one
@@ -246,6 +296,17 @@ int cc_pcrc_store(const char* chunk_path, uint32_t meta_bytes, const char* table
     return store_table(chunk_path, meta_bytes, table_path, page_crcs, n_pages, page_bytes, nullptr);
 }
 
+int cc_pcrc_store_expect(const char* chunk_path, uint32_t meta_bytes, const char* table_path,
+                         const uint32_t* page_crcs, uint32_t n_pages, uint32_t page_bytes,
+                         const cc_pcrc_header* expect) {
+    if (!expect) return CC_EINVAL;
+    ChunkId e;
+    e.sn = expect->chunk_sn;
+    e.mtime = expect->data_mtime_ns;
+    e.size = expect->data_size;
+    return store_table(chunk_path, meta_bytes, table_path, page_crcs, n_pages, page_bytes, &e);
+}
+
 int cc_integrity_check(const char* const* chunk_paths, const char* const* table_paths, uint64_t n,
                        const cc_integrity_opts* o, cc_integrity_result* res, uint64_t* bad_list, uint64_t bad_cap,
                        uint64_t* n_bad) {
@@ -255,7 +316,10 @@ int cc_integrity_check(const char* const* chunk_paths, const char* const* table_
     if (o->page_bytes == 0 || o->chunk_bytes == 0 || o->meta_bytes == 0 || o->chunk_bytes % o->page_bytes)
         return CC_EINVAL;
     const uint32_t n_pages = o->chunk_bytes / o->page_bytes;
-    // 1. identity BEFORE the read: sn from the metapage, mtime + size
+    // 1. identity BEFORE the read: sn from the metapage, mtime + size; and the
+    //    stamp a table rewritten from this read will carry (taken first: every
+    //    byte read below is at least this current)
+    const int64_t stamp = now_ns();
     std::vector<ChunkId> before(n);
     for (uint64_t i = 0; i < n; i++) {
         res[i] = cc_integrity_result{0, CC_TABLE_OK, n_pages, 0, -1};
@@ -294,8 +358,8 @@ int cc_integrity_check(const char* const* chunk_paths, const char* const* table_
                 return;
             }
             // the chunk must still be the one read in step 2 (identity before)
-            const int s =
-                store_table(chunk_paths[i], o->meta_bytes, table_paths[i], got, n_pages, o->page_bytes, &before[i]);
+            const int s = store_table(chunk_paths[i], o->meta_bytes, table_paths[i], got, n_pages, o->page_bytes,
+                                      &before[i], stamp);
             if (s == CC_ESTALE) {
                 r.table_state = CC_TABLE_STALE;
                 return;
@@ -324,6 +388,20 @@ int cc_integrity_check(const char* const* chunk_paths, const char* const* table_
             // not persist its CRCs, or a snapshot): stale, never bad pages
             r.table_state = CC_TABLE_STALE;
             if (o->refresh_stale) rebuild(CC_TABLE_REFRESHED);
+            continue;
+        }
+        if (cc_pcrc_is_racy(&h)) {
+            // the table was written within a clock tick of the chunk's last
+            // write: a later write may have kept the mtime, so a mismatch
+            // proves nothing -- stale; a match re-stamps the table (rewritten
+            // with this check's stamp, one tick or more after the mtime)
+            const bool same = memcmp(got, want.data(), 4ull * n_pages) == 0;
+            if (!same) {
+                r.table_state = CC_TABLE_STALE;
+                if (o->refresh_stale) rebuild(CC_TABLE_REFRESHED);
+            } else {
+                rebuild(CC_TABLE_OK);
+            }
             continue;
         }
         for (uint32_t p = 0; p < n_pages; p++) {

@@ -20,7 +20,11 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <stdlib.h>
+
+#include <chrono>
 #include <mutex>
+#include <thread>
 
 #include "../../include/curve_crc.h"
 #include "kernels.h"
@@ -46,6 +50,39 @@ int map_hip(hipError_t e) {
 
 int map_nccl(ncclResult_t r) { return r == ncclSuccess ? CC_OK : CC_ECOMM; }
 
+constexpr uint32_t kDefaultInitTimeoutMs = 120000;
+
+uint32_t init_timeout_ms(uint32_t asked) {
+    if (asked) return asked;
+    if (const char* e = getenv("CC_COMM_INIT_TIMEOUT_MS")) {
+        const long v = strtol(e, nullptr, 10);
+        if (v > 0) return (uint32_t)v;
+    }
+    return kDefaultInitTimeoutMs;
+}
+
+// The communicator is non-blocking (ncclConfig_t.blocking = 0): every call may
+// return ncclInProgress, and the next call on it may only be issued once
+// ncclCommGetAsyncError reports the state left ncclInProgress.  Polls that
+// state until `deadline`; ncclInProgress past it = CC_ETIMEDOUT (the caller
+// aborts the communicator).  This is what keeps a rank whose peers never join
+// (one rank's init failed before it reached RCCL) from blocking forever inside
+// the bootstrap, as a blocking ncclCommInitRank would.
+int settle(ncclComm_t nc, ncclResult_t r, std::chrono::steady_clock::time_point deadline) {
+    while (r == ncclInProgress) {
+        if (std::chrono::steady_clock::now() > deadline) return CC_ETIMEDOUT;
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (ncclCommGetAsyncError(nc, &r) != ncclSuccess) return CC_ECOMM;
+    }
+    return map_nccl(r);
+}
+
+// enqueue-side wait of an already initialised communicator: bounded as well
+// (a collective's enqueue never waits for peers, so this is microseconds)
+int settle_call(ncclComm_t nc, ncclResult_t r) {
+    return settle(nc, r, std::chrono::steady_clock::now() + std::chrono::seconds(60));
+}
+
 }  // namespace
 
 extern "C" {
@@ -59,37 +96,62 @@ int cc_comm_unique_id(void* id, size_t bytes) {
     return CC_OK;
 }
 
-int cc_comm_init(cc_comm** comm, int nranks, int rank, const void* id, size_t bytes) {
+int cc_comm_init_timeout(cc_comm** comm, int nranks, int rank, const void* id, size_t bytes, uint32_t timeout_ms) {
     if (!comm || !id || bytes < sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks) return CC_EINVAL;
     *comm = nullptr;
     int dev = -1, n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || hipGetDevice(&dev) != hipSuccess) return CC_ENODEV;
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(init_timeout_ms(timeout_ms));
+    ncclComm_t nc = nullptr;
+    const ncclResult_t r = ncclCommInitRankConfig(&nc, nranks, u, rank, &cfg);
+    if (!nc) return CC_ECOMM;  // failed before a communicator existed
+    const int rc = settle(nc, r, deadline);
+    if (rc) {  // failed or timed out: tear down without waiting for the peers
+        (void)ncclCommAbort(nc);
+        return rc;
+    }
     cc_comm* c = new cc_comm();
+    c->nc = nc;
     c->nranks = nranks;
     c->rank = rank;
     c->device = dev;
-    const int rc = map_nccl(ncclCommInitRank(&c->nc, nranks, u, rank));
-    if (rc) {
-        delete c;
-        return rc;
-    }
     *comm = c;
     return CC_OK;
 }
 
-int cc_comm_destroy(cc_comm* comm) {
+int cc_comm_init(cc_comm** comm, int nranks, int rank, const void* id, size_t bytes) {
+    return cc_comm_init_timeout(comm, nranks, rank, id, bytes, 0);
+}
+
+static int comm_release(cc_comm* comm, bool abort) {
     if (!comm) return CC_OK;
     int cur = -1;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(comm->device);
+    int rc = CC_OK;
+    if (comm->nc) {
+        if (abort) {
+            rc = map_nccl(ncclCommAbort(comm->nc));
+        } else {
+            // finalize flushes this rank's outstanding work (non-blocking: settle
+            // it), then destroy frees the resources
+            rc = settle_call(comm->nc, ncclCommFinalize(comm->nc));
+            const int rd = map_nccl(ncclCommDestroy(comm->nc));
+            if (!rc) rc = rd;
+        }
+    }
     if (comm->gather) (void)hipFree(comm->gather);
-    const int rc = comm->nc ? map_nccl(ncclCommDestroy(comm->nc)) : CC_OK;
     if (cur >= 0) (void)hipSetDevice(cur);
     delete comm;
     return rc;
 }
+
+int cc_comm_destroy(cc_comm* comm) { return comm_release(comm, false); }
+int cc_comm_abort(cc_comm* comm) { return comm_release(comm, true); }
 
 int cc_comm_size(const cc_comm* comm) { return comm ? comm->nranks : 0; }
 int cc_comm_rank(const cc_comm* comm) { return comm ? comm->rank : -1; }
@@ -114,7 +176,7 @@ int cc_digest_allreduce_dev(cc_comm* comm, uint32_t* d_digest, uint64_t n, void*
         }
     }
     // ring all-gather of the partials into [rank][n], then out = XOR over ranks
-    int rc = map_nccl(ncclAllGather(d_digest, comm->gather, n, ncclUint32, comm->nc, s));
+    int rc = settle_call(comm->nc, ncclAllGather(d_digest, comm->gather, n, ncclUint32, comm->nc, s));
     if (rc) return rc;
     return cc_digest_fold_dev(comm->gather, (uint32_t)comm->nranks, n, d_digest, stream);
 }

@@ -416,7 +416,7 @@ void IntegrityTableAndService() {  // CPU: codec, metapage sn, atomic store / lo
     std::vector<uint32_t> pc(256);
     std::mt19937_64 rng(5);
     for (auto& c : pc) c = (uint32_t)rng();
-    cc_pcrc_header h = {4096, 256, 9, 123456789, 4096 + (1u << 20)};
+    cc_pcrc_header h = {4096, 256, 9, 123456789, 4096 + (1u << 20), 0};
     std::vector<unsigned char> buf(cc_pcrc_encoded_bytes(256));
     EXPECT(cc_pcrc_encode(&h, pc.data(), buf.data(), buf.size()) == CC_OK);
     cc_pcrc_header g;

@@ -2,6 +2,7 @@
 #include "integrity_service.h"
 
 #include <dirent.h>
+#include <errno.h>
 #include <string.h>
 #include <sys/stat.h>
 #include <time.h>
@@ -12,7 +13,13 @@
 namespace cchost {
 
 namespace {
-std::string ErrText(int rc) { return rc < 0 && rc > -4096 && rc != CC_EINVAL ? strerror(-rc) : cc_strerror(rc); }
+// libcurvecrc's own codes first (CC_ECORRUPT, CC_EHIP, CC_ESTALE ... sit inside
+// the errno range and would read as unrelated errno text), then errno
+std::string ErrText(int rc) {
+    const char* t = cc_strerror(rc);
+    if (strcmp(t, "unknown error") != 0) return t;
+    return rc < 0 && rc > -4096 ? strerror(-rc) : t;
+}
 }  // namespace
 
 std::string TableDirFor(const std::string& dataDir) {
@@ -83,6 +90,32 @@ INTEGRITY_OP_STATUS IntegrityService::ListJobs(std::vector<IntegrityJob>* jobs) 
     jobs->clear();
     for (int32_t id : order_) jobs->push_back(jobs_.at(id));
     return INTEGRITY_OP_STATUS_SUCCESS;
+}
+
+bool IntegrityService::JobInfo(int32_t id, IntegrityJob* out, size_t* nResults) const {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = jobs_.find(id);
+    if (it == jobs_.end()) return false;
+    const IntegrityJob& j = it->second;
+    out->id = j.id;
+    out->copyset = j.copyset;
+    out->state = j.state;
+    out->progress = j.progress;
+    out->sched_time = j.sched_time;
+    out->start_time = j.start_time;
+    out->dataDir = j.dataDir;
+    out->error = j.error;
+    out->results.clear();
+    if (nResults) *nResults = j.results.size();
+    return true;
+}
+
+bool IntegrityService::FileResult(int32_t id, size_t k, IntegrityFileResult* out) const {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = jobs_.find(id);
+    if (it == jobs_.end() || k >= it->second.results.size()) return false;
+    *out = it->second.results[k];
+    return true;
 }
 
 bool IntegrityService::Wait(int32_t id, int timeoutMs, IntegrityJob* out) {
@@ -179,13 +212,16 @@ void IntegrityService::DoJob(IntegrityJob* job) {
         const int rc = cc_integrity_check(cpp.data(), tpp.data(), nb, &o, res.data(), bad.data(), cap, &nbad);
         if (rc) return fail(std::string("cc_integrity_check: ") + ErrText(rc));
         std::vector<IntegrityFileResult> out(nb);
+        // a file's own failure (metapage header CRC -> CC_ECORRUPT, unreadable,
+        // or -ENOENT: deleted between the listing and the check) is that file's
+        // result, never the job's: the rest of the copyset is still checked
         for (size_t k = 0; k < nb; k++) {
             out[k].name = todo[b0 + k];
             out[k].status = res[k].status;
             out[k].tableState = res[k].table_state;
             out[k].badPages = res[k].bad_pages;
             out[k].firstBad = res[k].first_bad;
-            if (res[k].status) return fail("cannot check " + cp[k] + ": " + ErrText(res[k].status));
+            if (res[k].status) out[k].error = res[k].status == -ENOENT ? "vanished" : ErrText(res[k].status);
         }
         for (uint64_t q = 0; q < std::min(nbad, cap); q++) out[bad[q] >> 32].badList.push_back((uint32_t)bad[q]);
         std::lock_guard<std::mutex> lk(mu_);

@@ -42,7 +42,8 @@ enum INTEGRITY_OP_STATUS {  // proto/integrity.proto:45-48
 // Outcome of one chunk file (new; the proto carries only job-level fields).
 struct IntegrityFileResult {
     std::string name;
-    int32_t status = 0;        // 0, -errno, CC_EINVAL, CC_ECORRUPT (metapage)
+    int32_t status = 0;        // 0, -errno (-ENOENT: the chunk vanished mid-job), CC_EINVAL, CC_ECORRUPT (metapage)
+    std::string error;         // text of a non-zero status ("vanished" for -ENOENT)
     uint32_t tableState = 0;   // CC_TABLE_*
     uint32_t badPages = 0;
     int64_t firstBad = -1;
@@ -87,6 +88,10 @@ class IntegrityService {
     INTEGRITY_OP_STATUS ListJobs(std::vector<IntegrityJob>* jobs) const;
     // test / tool helper: block until the job leaves WAITING/RUNNING (or timeout)
     bool Wait(int32_t id, int timeoutMs, IntegrityJob* out);
+    // one job's fields without its per-file results (n = results so far), and
+    // one result: O(1) reads for the C ABI (include/curve_integrity.h)
+    bool JobInfo(int32_t id, IntegrityJob* out, size_t* nResults) const;
+    bool FileResult(int32_t id, size_t k, IntegrityFileResult* out) const;
 
  private:
     void Run();

@@ -20,20 +20,22 @@ its own CRCs is "corrupt".
 Jobs mirror proto/integrity.proto (IntegrityService: ScheduleJob / CancelJob /
 PauseJob / ResumeJob / ListJobs; IntegrityJob{id, copyset, state, progress,
 sched_time, start_time}; INTEGRITY_JOB_STATE) -- declared and compiled in the
-reference (proto/BUILD:78) with no implementation anywhere in src/.  A job walks
-one copyset data directory in batches; each batch is one cc_integrity_check
-call (native pread into pinned staging, every page rehashed on the GPU, compared
-with its table).
+reference (proto/BUILD:78) with no implementation anywhere in src/.  The
+service is the C++ one (curve_amd/host/integrity_service.cpp) behind
+include/curve_integrity.h; `IntegrityService` below is a ctypes facade over it.
+A job walks one copyset data directory in batches; each batch is one
+cc_integrity_check call (native pread into pinned staging, every page rehashed
+on the GPU, compared with its table).  A chunk's own failure (metapage header
+CRC, deleted mid-job) is that file's result; only a failing batch call fails
+the job.
 """
 from __future__ import annotations
 
 import ctypes
 import enum
 import os
-import threading
-import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import List, Optional
 
 import numpy as np
 
@@ -150,7 +152,6 @@ def check_files(paths: List[str], table_paths: List[str], chunk_size: int = C.CH
 class IntegrityJob:  # proto/integrity.proto:32-39
     id: int
     copyset: int
-    data_dir: str
     state: IntegrityJobState = IntegrityJobState.WAITING
     progress: int = 0          # percent of chunk files done
     sched_time: int = 0
@@ -160,122 +161,73 @@ class IntegrityJob:  # proto/integrity.proto:32-39
 
 
 class IntegrityService:
-    """In-process IntegrityService (ScheduleJob/CancelJob/PauseJob/ResumeJob/
-    ListJobs), the Python twin of curve_amd/host/integrity_service.h.  One
-    worker thread runs jobs FIFO; Pause/Cancel take effect at chunk-file batch
-    boundaries.  Work happens on the calling process's current HIP device."""
+    """IntegrityService (ScheduleJob / CancelJob / PauseJob / ResumeJob /
+    ListJobs) -- a ctypes facade over the C++ service of the host layer
+    (curve_amd/host/integrity_service.h through include/curve_integrity.h,
+    libcurvehost.so).  The job state machine, its worker thread and its
+    batches live in C++ only; this class converts arguments and results.
+    Work happens on the process's current HIP device."""
 
     def __init__(self, chunk_size: int = C.CHUNK_SIZE, meta_size: int = C.META_PAGE_SIZE,
                  page_bytes: int = C.PAGE_SIZE, batch: int = 16, create_missing: bool = True,
-                 refresh_stale: bool = True):
-        self.chunk_size, self.meta_size, self.page_bytes = chunk_size, meta_size, page_bytes
-        self.batch, self.create_missing, self.refresh_stale = batch, create_missing, refresh_stale
-        self._jobs: Dict[int, IntegrityJob] = {}
-        self._order: List[int] = []
-        self._cv = threading.Condition()
-        self._stop = False
-        self._worker = threading.Thread(target=self._run, daemon=True)
-        self._worker.start()
+                 refresh_stale: bool = True, io_threads: int = 8):
+        self._H = _lib.host_lib()
+        o = _lib.CcIsvcOpts(chunk_size, meta_size, page_bytes, batch, io_threads, int(create_missing),
+                            int(refresh_stale))
+        self._s = self._H.cc_isvc_create(ctypes.byref(o))
+        if not self._s:
+            raise C.CurveCrcError(_lib.CC_EINVAL, "cc_isvc_create")
+        self.page_bytes, self.pages = page_bytes, chunk_size // page_bytes
 
     # -- RPC surface -----------------------------------------------------
     def ScheduleJob(self, job_id: int, copyset: int, data_dir: str) -> IntegrityOpStatus:
-        with self._cv:
-            if job_id in self._jobs:
-                return IntegrityOpStatus.FAILURE_UNKNOWN
-            self._jobs[job_id] = IntegrityJob(job_id, copyset, data_dir, sched_time=int(time.time()))
-            self._order.append(job_id)
-            self._cv.notify_all()
-        return IntegrityOpStatus.SUCCESS
-
-    def _set(self, job_id: int, frm, to) -> IntegrityOpStatus:
-        with self._cv:
-            j = self._jobs.get(job_id)
-            if j is None or j.state not in frm:
-                return IntegrityOpStatus.FAILURE_UNKNOWN
-            j.state = to
-            self._cv.notify_all()
-        return IntegrityOpStatus.SUCCESS
+        return IntegrityOpStatus(self._H.cc_isvc_schedule(self._s, job_id, copyset, os.fsencode(data_dir)))
 
     def CancelJob(self, job_id: int) -> IntegrityOpStatus:
-        S = IntegrityJobState
-        return self._set(job_id, (S.WAITING, S.RUNNING, S.PAUSED), S.CANCELED)
+        return IntegrityOpStatus(self._H.cc_isvc_cancel(self._s, job_id))
 
     def PauseJob(self, job_id: int) -> IntegrityOpStatus:
-        S = IntegrityJobState
-        return self._set(job_id, (S.WAITING, S.RUNNING), S.PAUSED)
+        return IntegrityOpStatus(self._H.cc_isvc_pause(self._s, job_id))
 
     def ResumeJob(self, job_id: int) -> IntegrityOpStatus:
-        S = IntegrityJobState
-        return self._set(job_id, (S.PAUSED,), S.WAITING)
+        return IntegrityOpStatus(self._H.cc_isvc_resume(self._s, job_id))
 
     def ListJobs(self) -> List[IntegrityJob]:
-        with self._cv:
-            return [self._jobs[i] for i in self._order]
+        n = ctypes.c_uint64(0)
+        check(self._H.cc_isvc_list(self._s, None, 0, ctypes.byref(n)), "cc_isvc_list")
+        ids = (ctypes.c_int32 * max(1, n.value))()
+        check(self._H.cc_isvc_list(self._s, ids, n.value, ctypes.byref(n)), "cc_isvc_list")
+        return [self.job(int(ids[k])) for k in range(min(n.value, len(ids)))]
+
+    def job(self, job_id: int) -> IntegrityJob:
+        info = _lib.CcIsvcJob()
+        check(self._H.cc_isvc_job_info(self._s, job_id, ctypes.byref(info)), "cc_isvc_job_info")
+        j = IntegrityJob(info.id, info.copyset, IntegrityJobState(info.state), info.progress, info.sched_time,
+                         info.start_time, error=info.error.decode(errors="replace"))
+        f = _lib.CcIsvcFile()
+        for k in range(info.n_results):
+            check(self._H.cc_isvc_file_result(self._s, job_id, k, ctypes.byref(f), None, 0), "cc_isvc_file_result")
+            bad = np.zeros(max(1, f.n_bad_listed), dtype=np.uint32)
+            check(self._H.cc_isvc_file_result(self._s, job_id, k, ctypes.byref(f), bad.ctypes.data, bad.size),
+                  "cc_isvc_file_result")
+            j.results.append(FileResult(f.name.decode(errors="replace"), self.pages, int(f.bad_pages), int(f.first_bad),
+                                        _lib.TABLE_STATES.get(int(f.table_state), "?"), int(f.status),
+                                        bad[:f.n_bad_listed].tolist()))
+        return j
 
     def wait(self, job_id: int, timeout: float = 60.0) -> IntegrityJob:
-        end = time.time() + timeout
-        with self._cv:
-            while self._jobs[job_id].state in (IntegrityJobState.WAITING, IntegrityJobState.RUNNING):
-                left = end - time.time()
-                if left <= 0:
-                    break
-                self._cv.wait(left)
-            return self._jobs[job_id]
+        rc = self._H.cc_isvc_wait(self._s, job_id, int(timeout * 1000))
+        if rc < 0:
+            raise C.CurveCrcError(rc, "cc_isvc_wait")
+        return self.job(job_id)
 
     def close(self):
-        with self._cv:
-            self._stop = True
-            self._cv.notify_all()
-        self._worker.join(timeout=10)
+        if self._s:
+            s, self._s = self._s, None
+            self._H.cc_isvc_destroy(s)
 
-    # -- worker ------------------------------------------------------------
-    def _next(self) -> Optional[IntegrityJob]:
-        for i in self._order:
-            if self._jobs[i].state == IntegrityJobState.WAITING:
-                return self._jobs[i]
-        return None
-
-    def _run(self):
-        while True:
-            with self._cv:
-                while not self._stop and self._next() is None:
-                    self._cv.wait()
-                if self._stop:
-                    return
-                job = self._next()
-                job.state = IntegrityJobState.RUNNING
-                if not job.start_time:
-                    job.start_time = int(time.time())
-            try:
-                self._do(job)
-            except Exception as e:  # noqa: BLE001 -- reported through the job state
-                with self._cv:
-                    job.state, job.error = IntegrityJobState.FAILED, repr(e)
-                    self._cv.notify_all()
-
-    def _do(self, job: IntegrityJob):
-        fsize = self.chunk_size + self.meta_size
-        names = sorted(n for n in os.listdir(job.data_dir) if os.path.getsize(os.path.join(job.data_dir, n)) == fsize)
-        tdir = table_dir_for(job.data_dir)
-        os.makedirs(tdir, exist_ok=True)
-        done = {r.name for r in job.results}
-        todo = [n for n in names if n not in done]
-        for b0 in range(0, len(todo), self.batch):
-            with self._cv:
-                if job.state != IntegrityJobState.RUNNING:  # paused or canceled at a batch boundary
-                    self._cv.notify_all()
-                    return
-            part = todo[b0:b0 + self.batch]
-            paths = [os.path.join(job.data_dir, n) for n in part]
-            res = check_files(paths, [sidecar_path(p, tdir) for p in paths], self.chunk_size, self.meta_size,
-                              self.page_bytes, self.create_missing, self.refresh_stale)
-            bad = [r for r in res if r.status]
-            if bad:
-                raise IOError(f"cannot check {bad[0].name}: status {bad[0].status}")
-            job.results.extend(res)
-            with self._cv:
-                job.progress = int(100 * len(job.results) / max(1, len(names)))
-        with self._cv:
-            if job.state == IntegrityJobState.RUNNING:
-                job.state, job.progress = IntegrityJobState.FINISHED, 100
-            self._cv.notify_all()
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass

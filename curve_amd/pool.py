@@ -87,16 +87,18 @@ def digests_as_hash_strings(digests) -> List[str]:
 # torch is only the device-memory / stream / rendezvous plumbing here.
 # ---------------------------------------------------------------------------
 class Comm:
-    """An RCCL communicator created and owned by libcurvecrc (cc_comm_init)."""
+    """An RCCL communicator created and owned by libcurvecrc (cc_comm_init_timeout:
+    non-blocking RCCL init polled against a deadline, aborted when it expires)."""
 
-    def __init__(self, nranks: int, rank: int, uid: bytes):
+    def __init__(self, nranks: int, rank: int, uid: bytes, timeout_ms: int = 0):
         import ctypes
         from . import _lib
         if len(uid) != _lib.CC_COMM_ID_BYTES:
             raise ValueError("unique id must be CC_COMM_ID_BYTES long")
         self._h = ctypes.c_void_p()
         buf = ctypes.create_string_buffer(bytes(uid), len(uid))
-        _lib.check(_lib.lib().cc_comm_init(ctypes.byref(self._h), nranks, rank, buf, len(uid)), "cc_comm_init")
+        _lib.check(_lib.lib().cc_comm_init_timeout(ctypes.byref(self._h), nranks, rank, buf, len(uid),
+                                                   int(timeout_ms)), "cc_comm_init")
         self.nranks, self.rank = nranks, rank
 
     @staticmethod
@@ -122,8 +124,15 @@ class Comm:
     def close(self):
         from . import _lib
         if self._h:
-            _lib.check(_lib.lib().cc_comm_destroy(self._h), "cc_comm_destroy")
-            self._h = None
+            h, self._h = self._h, None
+            _lib.check(_lib.lib().cc_comm_destroy(h), "cc_comm_destroy")
+
+    def abort(self):
+        """Leave without waiting for the peers (cc_comm_abort)."""
+        from . import _lib
+        if self._h:
+            h, self._h = self._h, None
+            _lib.lib().cc_comm_abort(h)
 
     def __del__(self):  # pragma: no cover - best effort
         try:
@@ -132,14 +141,58 @@ class Comm:
             pass
 
 
-def comm_from_dist(dist, group=None) -> Comm:
+# Failure injection for the agreement protocol (the reference's libfiu
+# failpoints play this role, test/failpoint/): when this environment variable
+# holds a rank number, that rank's native init fails before it reaches RCCL,
+# as a rank whose device or RCCL setup broke would.
+FAIL_INIT_RANK_ENV = "CC_INJECT_COMM_INIT_FAIL_RANK"
+
+
+def comm_from_dist(dist, group=None, timeout_ms: int = 0) -> Comm:
     """Rank 0 makes the RCCL unique id, torch.distributed carries its 128 bytes
     to every rank (as the MDS or any out-of-band channel would), then every
     rank joins the native communicator on its current device."""
+    import os
+    from . import _lib
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    obj = [Comm.unique_id() if rank == 0 else None]
+    obj = [None]
+    if rank == 0:  # a failure here is broadcast too: the other ranks must not wait for an id forever
+        try:
+            obj = [Comm.unique_id()]
+        except Exception as e:
+            obj = [f"rank 0 could not create the RCCL id: {e}"]
     dist.broadcast_object_list(obj, src=0, group=group)
-    return Comm(world, rank, obj[0])
+    if not isinstance(obj[0], bytes):
+        raise _lib.CurveCrcError(_lib.CC_ECOMM, f"cc_comm_unique_id ({obj[0]})")
+    if os.environ.get(FAIL_INIT_RANK_ENV, "") == str(rank):
+        raise _lib.CurveCrcError(_lib.CC_ECOMM, f"cc_comm_init (injected failure on rank {rank})")
+    return Comm(world, rank, obj[0], timeout_ms=timeout_ms)
+
+
+def agreed_comm(dist, device=None, group=None, timeout_ms: int = 0):
+    """Every rank takes the SAME digest-exchange path, or a mismatched
+    collective hangs: each rank tries the native communicator (bounded by
+    `timeout_ms`), then the ranks all-reduce(MIN) a success flag.  If any
+    rank failed, the ranks that succeeded abort theirs and every rank returns
+    None (the torch.distributed exchange, reduce_digests).  Returns
+    (comm or None, note saying which path runs and why)."""
+    import torch
+    err = None
+    comm = None
+    try:
+        comm = comm_from_dist(dist, group=group, timeout_ms=timeout_ms)
+    except Exception as e:  # CurveCrcError (ECOMM / ETIMEDOUT / ENODEV) or a rendezvous error
+        err = e
+    on_dev = dist.get_backend(group) != "gloo" and device is not None
+    flag = torch.tensor([0 if err else 1], dtype=torch.int32, device=device if on_dev else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    ok_all = bool(int(flag.item()))
+    if ok_all:
+        return comm, "native RCCL (cc_comm_init_timeout + cc_digest_allreduce_dev)"
+    if comm is not None:
+        comm.abort()
+    why = f"this rank: {err}" if err else "another rank's native init failed"
+    return None, f"torch.distributed all_gather_into_tensor + cc_digest_fold_dev (native comm not agreed: {why})"
 
 
 def pool_scan(pool, after_mult, group, digest, comm: "Comm" = None, stream=None, events=None):

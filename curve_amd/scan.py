@@ -206,7 +206,7 @@ class DevicePool:
 
 def scan_copyset_dir(data_dir: str, logical_pool_id: int, copyset_id: int, first_index: int = 0,
                      chunk_size: int = CHUNK_SIZE, meta_size: int = META_PAGE_SIZE, scan_size: int = SCAN_SIZE,
-                     io_threads: int = 8) -> List[ScanMap]:
+                     io_threads: int = 8, page_bytes: int = PAGE_SIZE) -> List[ScanMap]:
     """ScanManager::ScanJobProcess over a copyset's chunk files on disk
     (scan_manager.cpp:210-296): for every chunk (`chunk_<id>`, the ChunkMap;
     snapshots are not scanned) with a V2 metapage, the metapage op then the
@@ -223,7 +223,7 @@ def scan_copyset_dir(data_dir: str, logical_pool_id: int, copyset_id: int, first
     pat = re.compile(r"^chunk_(\d+)$")
     ids = sorted(int(m.group(1)) for n in os.listdir(data_dir) if (m := pat.match(n)))
     paths = [os.path.join(data_dir, chunk_file_name(i)) for i in ids]
-    st, mc, sc, _ = C.scan_files(paths, chunk_size, meta_size, PAGE_SIZE, scan_size, io_threads)
+    st, mc, sc, _ = C.scan_files(paths, chunk_size, meta_size, page_bytes, scan_size, io_threads)
     out, idx = [], first_index
     for k, cid in enumerate(ids):
         if st[k] != 0:

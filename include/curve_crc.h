@@ -35,6 +35,7 @@ extern "C" {
 #define CC_ECORRUPT (-74) /* verify found mismatching pages (host verify) */
 #define CC_EIO (-5001)    /* reading or writing a file failed (errno is kept where the call says so) */
 #define CC_ESTALE (-116)  /* a per-page CRC table no longer describes its chunk (sn / write generation) */
+#define CC_ETIMEDOUT (-110) /* a bounded wait expired (communicator init whose peers never joined) */
 
 /* ------------------------------------------------------------------------
  * CPU primitive -- drop-in for the inline header src/common/crc32.h
@@ -375,9 +376,22 @@ typedef struct cc_comm cc_comm; /* opaque: an RCCL communicator + gather scratch
  * out of band (the MDS, a TCP store, ...). */
 int cc_comm_unique_id(void* id, size_t bytes);
 /* Collective: every rank calls it with the same id, on the HIP device it owns
- * (the calling thread's current device).  Blocks until all ranks joined. */
-int cc_comm_init(cc_comm** comm, int nranks, int rank, const void* id, size_t bytes);
+ * (the calling thread's current device).  Returns once all ranks joined, or
+ * after `timeout_ms` (0 = $CC_COMM_INIT_TIMEOUT_MS, else 120 s) with
+ * CC_ETIMEDOUT and the half-built communicator aborted: a rank whose peers
+ * never arrive (one failed before reaching RCCL) is never blocked forever.
+ * The communicator is RCCL non-blocking (ncclConfig_t.blocking = 0); every
+ * call below waits for its own enqueue to settle.  The reference's exchange
+ * (FollowScanMap, chunk_closure.cpp:82-104) is likewise bounded (retry x
+ * timeout, scan_manager.cpp:285-289).  Ranks that disagree on whether their
+ * init succeeded must all fall back together (bench.py / pool.agreed_comm
+ * reduce a success flag before the first collective). */
+int cc_comm_init_timeout(cc_comm** comm, int nranks, int rank, const void* id, size_t bytes, uint32_t timeout_ms);
+int cc_comm_init(cc_comm** comm, int nranks, int rank, const void* id, size_t bytes); /* default timeout */
+/* destroy: finalize (flush this rank's work) + free.  abort: free without
+ * waiting for the peers (a rank leaving a communicator its peers gave up on). */
 int cc_comm_destroy(cc_comm* comm);
+int cc_comm_abort(cc_comm* comm);
 int cc_comm_size(const cc_comm* comm);
 int cc_comm_rank(const cc_comm* comm);
 
@@ -443,7 +457,19 @@ typedef struct cc_pcrc_header {
     uint64_t chunk_sn;      /* metapage sn when the table was written */
     int64_t data_mtime_ns;  /* the chunk file's st_mtim then */
     uint64_t data_size;     /* the chunk file's size then */
+    int64_t stamp_ns;       /* CLOCK_REALTIME when the CRCs' bytes were known current: a check's
+                               time just before it read the chunk, a store's call time */
 } cc_pcrc_header;
+
+/* Racy tables (git's "racily clean" index entries).  File mtimes come from a
+ * coarse clock: a write landing in the same clock tick as data_mtime_ns leaves
+ * the identity unchanged.  A table is trusted to condemn data only when that
+ * cannot have happened after its CRCs were taken, i.e. when
+ *     data_mtime_ns + tick <= stamp_ns     (tick = clock_getres(CLOCK_REALTIME_COARSE))
+ * Otherwise it is RACY: its pages are still compared, a match re-stamps it
+ * (the table is rewritten with a later stamp), and a mismatch is reported as
+ * STALE -- refreshed by policy -- never as bad pages. */
+int cc_pcrc_is_racy(const cc_pcrc_header* h);
 
 /* In-memory codec.  decode: CC_ECORRUPT for a bad magic / version / header CRC
  * / table CRC / length; page_crcs may be NULL (header only). */
@@ -459,10 +485,21 @@ int cc_chunk_meta_sn(const void* metapage, uint32_t bytes, uint64_t* sn);
 /* Write the table of chunk file `chunk_path` (metapage of meta_bytes, then
  * n_pages data pages) to `table_path`, atomically (temp file + fsync + rename),
  * recording the chunk's current sn, mtime and size.  Call it after the data
- * write it describes (the write path's CSChunkFile::Write, chunkserver_chunkfile.cpp:287-427). */
+ * write it describes (the write path's CSChunkFile::Write, chunkserver_chunkfile.cpp:287-427),
+ * under the chunk's write lock (CSChunkFile::rwLock_) so no other write lands
+ * between the two. */
 int cc_pcrc_store(const char* chunk_path, uint32_t meta_bytes, const char* table_path, const uint32_t* page_crcs,
                   uint32_t n_pages, uint32_t page_bytes);
-/* Read + decode a table file (-errno if it cannot be read, -ENOENT if absent). */
+/* The same, but only if the chunk's identity is still `expect` (its sn,
+ * data_mtime_ns and data_size; the caller stats the file right after its
+ * pwrite): CC_ESTALE and nothing written otherwise, so a store that runs after
+ * a LATER write cannot pair the newer identity with the older CRCs. */
+int cc_pcrc_store_expect(const char* chunk_path, uint32_t meta_bytes, const char* table_path,
+                         const uint32_t* page_crcs, uint32_t n_pages, uint32_t page_bytes,
+                         const cc_pcrc_header* expect);
+/* Read + decode a table file (-errno if it cannot be read, -ENOENT if absent).
+ * With page_crcs, a file larger than a table of max_pages pages is CC_ECORRUPT
+ * before anything is allocated; without, only the 64-byte header is read. */
 int cc_pcrc_load(const char* table_path, cc_pcrc_header* h, uint32_t* page_crcs, uint32_t max_pages);
 
 /* Table state of one chunk after a check. */

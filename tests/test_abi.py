@@ -9,11 +9,16 @@ import pytest
 from conftest import ROOT
 
 
-def declared_symbols():
+HOST_HEADERS = ("curve_integrity.h",)  # the host layer's C ABI: curve_amd/host/libcurvehost.so
+
+
+def declared_symbols(host=False):
+    """Functions a header declares: libcurvecrc's headers, or (host=True) the
+    host layer's."""
     names = set()
     inc = os.path.join(ROOT, "include")
     for fn in os.listdir(inc):
-        if not fn.endswith(".h"):
+        if not fn.endswith(".h") or (fn in HOST_HEADERS) != host:
             continue
         txt = open(os.path.join(inc, fn)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
@@ -37,6 +42,18 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     # and the python binding describes every one of them
     assert declared_symbols() <= set(_lib.SIGNATURES)
+
+
+def test_host_library_exports_every_declared_symbol():
+    """libcurvehost.so (the C++ IntegrityService's C ABI) loads beside
+    libcurvecrc and exports what include/curve_integrity.h declares."""
+    from curve_amd import _lib
+    H = _lib.host_lib()
+    names = declared_symbols(host=True)
+    assert "cc_isvc_create" in names and "cc_isvc_wait" in names
+    missing = [n for n in sorted(names) if not hasattr(H, n)]
+    assert not missing, missing
+    assert names <= set(_lib.HOST_SIGNATURES)
 
 
 def test_no_gpu_fails_loudly_here():

@@ -85,3 +85,42 @@ def test_lexicographic_order_quirk():
     after = copyset_after_bytes(names, [1, 10, 100])
     # sorted: chunk_1 (100), chunk_10 (10), chunk_2 (1)
     assert after == [0, 1, 11]
+
+
+def _agree_worker(rank, world, port, inject, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if inject is not None:
+        os.environ["CC_INJECT_COMM_INIT_FAIL_RANK"] = str(inject)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from curve_amd.pool import agreed_comm
+        comm, note = agreed_comm(dist, timeout_ms=2000)
+        q.put((rank, comm is None, note))
+    except Exception as e:
+        q.put((rank, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("inject", [None, 0, 1])
+def test_exchange_path_agreement_no_gpu(inject):
+    """The ranks agree on ONE digest-exchange path before any collective
+    (pool.agreed_comm): here no rank has a GPU (rank 0 cannot even make the
+    RCCL id, and says so to the others instead of leaving them in the
+    broadcast), and with a failure injected on one rank, every rank returns the
+    torch.distributed path -- and nobody hangs."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_agree_worker, args=(r, world, port, inject, q)) for r in range(world)]
+    [p.start() for p in ps]
+    try:
+        res = dict((r, (fell_back, note)) for r, fell_back, note in (q.get(timeout=60) for _ in range(world)))
+    finally:
+        [p.join(timeout=30) for p in ps]
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+    assert all(res[r][0] is True for r in range(world)), res
+    assert all("torch.distributed" in res[r][1] for r in range(world)), res

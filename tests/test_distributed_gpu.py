@@ -40,15 +40,19 @@ def _pool_arrays():
     return data, meta, ids, groups
 
 
-def _rank_main(rank, world, port, q):
+def _rank_main(rank, world, port, q, agreed=False, inject=None):
     import sys
+    import time
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if inject is not None:
+        os.environ["CC_INJECT_COMM_INIT_FAIL_RANK"] = str(inject)
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from curve_amd import crc as C
-        from curve_amd.pool import copyset_layout, digests_as_hash_strings, pool_scan, reduce_digests, shard_range
+        from curve_amd.pool import (agreed_comm, copyset_layout, digests_as_hash_strings, pool_scan, reduce_digests,
+                                    shard_range)
         from curve_amd.scan import DevicePool
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
@@ -60,39 +64,49 @@ def _rank_main(rank, world, port, q):
         after = torch.tensor(lay.after_bytes[lo:hi], dtype=torch.int64, device=dev)
         grp = torch.tensor(lay.group[lo:hi], dtype=torch.int32, device=dev)
         digest = torch.full((lay.n_groups,), -1, dtype=torch.int32, device=dev)
-        pool_scan(pool, C.xpow8(after), grp, digest)  # one native call: pages, slices, files, partials
-        full = reduce_digests(digest, dist)            # gloo all-gather + cc_digest_fold_dev
+        comm, note, t_agree = None, "plain", 0.0
+        if agreed:  # the bench's protocol: bounded native init, then ONE path for all ranks
+            t0 = time.perf_counter()
+            comm, note = agreed_comm(dist, device=dev, timeout_ms=4000)
+            t_agree = time.perf_counter() - t0
+        pool_scan(pool, C.xpow8(after), grp, digest, comm=comm)  # one native call: pages, slices, files, partials
+        # without a native comm: gloo all-gather + cc_digest_fold_dev
+        full = digest if comm is not None else reduce_digests(digest, dist)
         torch.cuda.synchronize()
-        q.put((rank, digests_as_hash_strings(full), [int(x) & 0xFFFFFFFF for x in pool.file_crcs.cpu().tolist()]))
+        if comm is not None:
+            comm.close()
+        q.put((rank, digests_as_hash_strings(full), [int(x) & 0xFFFFFFFF for x in pool.file_crcs.cpu().tolist()],
+               note, t_agree))
     except Exception as e:  # report to the parent instead of hanging it
-        q.put((rank, repr(e), None))
+        q.put((rank, repr(e), None, None, None))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_pool_scan_device_fold_matches_whole_pool_chain(oracle, world):
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
+def _run_ranks(world, agreed=False, inject=None):
     import torch.multiprocessing as mp
-    from curve_amd.pool import copyset_layout, shard_range
-    from curve_amd.scan import chunk_file_name
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, q, agreed, inject)) for r in range(world)]
     [p.start() for p in ps]
     try:
         res = {}
         for _ in range(world):
-            r, dig, fcs = q.get(timeout=100)
-            res[r] = (dig, fcs)
+            r, dig, fcs, note, t_agree = q.get(timeout=100)
+            res[r] = (dig, fcs, note, t_agree)
     finally:
         [p.join(timeout=30) for p in ps]
         for p in ps:
             if p.is_alive():
                 p.kill()
     assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    return res
+
+
+def _check_against_oracle(oracle, res, world):
+    from curve_amd.pool import copyset_layout, shard_range
+    from curve_amd.scan import chunk_file_name
     data, meta, ids, groups = _pool_arrays()
     lay = copyset_layout(ids, groups, [CHUNK + 4096] * N_CHUNKS)
     want = []
@@ -104,6 +118,31 @@ def test_sharded_pool_scan_device_fold_matches_whole_pool_chain(oracle, world):
         assert res[r][0] == want, (r, res[r][0])
         lo, hi = shard_range(N_CHUNKS, r, world)
         assert res[r][1] == [oracle.crc32c(meta[i].tobytes() + data[i].tobytes()) for i in range(lo, hi)]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_pool_scan_device_fold_matches_whole_pool_chain(oracle, world):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _check_against_oracle(oracle, _run_ranks(world), world)
+
+
+@pytest.mark.parametrize("inject", [None, 0, 1])
+def test_exchange_agreement_with_one_rank_failing_native_init(oracle, inject):
+    """The N>1 bench's exchange protocol (pool.agreed_comm) on one GPU: a
+    failure injected into ONE rank's native init (rank 0 after it made the
+    RCCL id, or rank 1), or none (RCCL then refuses two ranks on one device
+    by itself).  The other rank's bounded init gives up (4 s here) instead of
+    waiting for its peer forever, the ranks reduce a success flag, all take
+    the torch.distributed exchange, and the digests equal the oracle's
+    whole-pool chain: no mismatched collectives, no hang."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = _run_ranks(2, agreed=True, inject=inject)
+    for r in range(2):
+        assert res[r][2] is not None and "torch.distributed" in res[r][2], res[r]
+        assert res[r][3] < 30.0, res[r][3]  # bounded: the 4 s init timeout + bootstrap
+    _check_against_oracle(oracle, res, 2)
 
 
 @pytest.mark.parametrize("nranks", [1, 2, 3, 8])

@@ -79,3 +79,102 @@ def test_service_state_machine(tmp_path):
         assert svc.ResumeJob(2) == I.IntegrityOpStatus.FAILURE_UNKNOWN  # not paused
     finally:
         svc.close()
+
+
+def _chunk(tmp_path, sn=77, chunk=1 << 16):
+    from curve_amd.chunkfile import ChunkFileMetaPage, write_chunk_file
+    d = tmp_path / "data"
+    d.mkdir(exist_ok=True)
+    path = str(d / f"chunk_{sn}")
+    write_chunk_file(path, ChunkFileMetaPage(sn=sn).encode(), bytes(chunk))
+    return path, np.arange(chunk // 4096, dtype=np.uint32) * 3
+
+
+def test_racy_table_rule(tmp_path):
+    """git's racily-clean rule for tables (cc_pcrc_is_racy): a table stamped
+    within one coarse-clock tick of the chunk's mtime cannot prove a later
+    write did not keep that mtime, so it never condemns data; one stamped a
+    tick or more after it can."""
+    import ctypes
+    import os
+    import time
+    from curve_amd import _lib
+    L = _lib.lib()
+    h = _lib.CcPcrcHeader(4096, 16, 1, 1_000_000_000_000, 4096 * 17, 1_000_000_000_000)
+    assert L.cc_pcrc_is_racy(ctypes.byref(h)) == 1          # same instant
+    h.stamp_ns = h.data_mtime_ns + 2_000_000_000
+    assert L.cc_pcrc_is_racy(ctypes.byref(h)) == 0          # 2 s later
+    h.stamp_ns = 0
+    assert L.cc_pcrc_is_racy(ctypes.byref(h)) == 1          # a table of the old format (no stamp)
+    # a store right after a write whose mtime is "now" is racy; the stamp is the store's clock
+    path, pc = _chunk(tmp_path)
+    os.utime(path, ns=(time.time_ns(), time.time_ns() + 200_000_000))  # the write's mtime is this tick (or later)
+    t0 = time.time_ns()
+    hdr, _ = I.load_table(I.store_table(path, pc, 4096))
+    assert t0 <= hdr.stamp_ns <= time.time_ns()
+    assert L.cc_pcrc_is_racy(ctypes.byref(hdr)) == 1
+    # an old write: not racy
+    os.utime(path, ns=(time.time_ns(), time.time_ns() - 5_000_000_000))
+    hdr, _ = I.load_table(I.store_table(path, pc, 4096))
+    assert L.cc_pcrc_is_racy(ctypes.byref(hdr)) == 0
+
+
+def test_store_expect_refuses_a_later_write(tmp_path):
+    """cc_pcrc_store_expect: the CRCs are stored only under the identity the
+    caller saw right after its own pwrite; a later write (new mtime) in between
+    gets CC_ESTALE and no table."""
+    import ctypes
+    import os
+    from curve_amd import _lib
+    L = _lib.lib()
+    path, pc = _chunk(tmp_path, sn=5)
+    st = os.stat(path)
+    expect = _lib.CcPcrcHeader(4096, pc.size, 5, st.st_mtime_ns, st.st_size, 0)
+    tp = I.sidecar_path(path)
+    os.makedirs(os.path.dirname(tp), exist_ok=True)
+    args = (os.fsencode(path), 4096, os.fsencode(tp), pc.ctypes.data, pc.size, 4096)
+    assert L.cc_pcrc_store_expect(*args, ctypes.byref(expect)) == 0
+    h, got = I.load_table(tp)
+    assert (h.chunk_sn, h.data_mtime_ns) == (5, st.st_mtime_ns) and (got == pc).all()
+    os.unlink(tp)
+    os.utime(path, ns=(st.st_atime_ns, st.st_mtime_ns + 1_000_000))  # a later write landed
+    assert L.cc_pcrc_store_expect(*args, ctypes.byref(expect)) == _lib.CC_ESTALE
+    assert not os.path.exists(tp)
+    expect.chunk_sn = 6  # a snapshot bumped the sn
+    os.utime(path, ns=(st.st_atime_ns, st.st_mtime_ns))
+    assert L.cc_pcrc_store_expect(*args, ctypes.byref(expect)) == _lib.CC_ESTALE
+
+
+def test_load_bounds_a_hostile_sidecar(tmp_path):
+    """cc_pcrc_load never allocates more than a table of max_pages needs: a
+    huge (sparse) sidecar is CC_ECORRUPT at once; header-only loads read 64 B."""
+    import ctypes
+    import os
+    from curve_amd import _lib
+    L = _lib.lib()
+    path, pc = _chunk(tmp_path, sn=9)
+    tp = I.store_table(path, pc, 4096)
+    h = _lib.CcPcrcHeader()
+    out = np.zeros(pc.size, dtype=np.uint32)
+    assert L.cc_pcrc_load(os.fsencode(tp), ctypes.byref(h), None, 0) == 0 and h.n_pages == pc.size
+    assert L.cc_pcrc_load(os.fsencode(tp), ctypes.byref(h), out.ctypes.data, pc.size) == 0 and (out == pc).all()
+    assert L.cc_pcrc_load(os.fsencode(tp), ctypes.byref(h), out.ctypes.data, pc.size - 1) == _lib.CC_ECORRUPT
+    big = str(tmp_path / "hostile.pcrc")
+    with open(big, "wb") as f:
+        f.write(open(tp, "rb").read()[:64])
+        f.truncate(8 << 30)  # 8 GiB, sparse
+    assert L.cc_pcrc_load(os.fsencode(big), ctypes.byref(h), out.ctypes.data, pc.size) == _lib.CC_ECORRUPT
+    assert L.cc_pcrc_load(os.fsencode(big), ctypes.byref(h), None, 0) == _lib.CC_ECORRUPT  # length != header's
+
+
+def test_service_is_the_cpp_one():
+    """The Python IntegrityService is a facade over the C++ service
+    (libcurvehost.so, include/curve_integrity.h): no second state machine."""
+    import inspect
+    src = inspect.getsource(I.IntegrityService)
+    assert "cc_isvc_" in src and "threading" not in src
+    svc = I.IntegrityService()
+    try:
+        assert svc._s
+    finally:
+        svc.close()

@@ -97,3 +97,129 @@ def test_write_path_tables_then_job_then_bit_rot(dev, oracle, tmp_path):
         assert all(x.bad_pages == 0 for k, x in res.items() if k != chunk_file_name(n))
     finally:
         svc.close()
+
+
+def _flip(path, off, restore_mtime=True):
+    st = os.stat(path)
+    with open(path, "r+b") as f:
+        f.seek(off)
+        b = f.read(1)
+        f.seek(off)
+        f.write(bytes([b[0] ^ 0x10]))
+    if restore_mtime:  # bit rot: the bytes change, the file's identity does not
+        os.utime(path, ns=(st.st_atime_ns, st.st_mtime_ns))
+
+
+def test_service_at_product_geometry(dev, oracle, tmp_path):
+    """The C++ IntegrityService (through its C ABI, curve_amd/host/libcurvehost.so)
+    over 12 chunk files of 16 MiB + 4 KiB -- one cc_integrity_check call whose
+    cc_scan_files spans two staging batches (7 files a slot) -- with, in one
+    job: bit rot in the LAST page (4095) of a chunk in the second batch, a
+    stale table (a write that skipped it), a corrupt table, a chunk whose
+    metapage header fails its CRC and an unreadable chunk.  The per-file
+    failures are those files' results; the job still checks every chunk."""
+    import time
+    from curve_amd import _lib
+    from curve_amd import integrity as I
+    from curve_amd.chunkfile import ChunkFileMetaPage, chunk_file_name, write_chunk_file
+    chunk, meta, pb, n = 16 << 20, 4096, 4096, 12
+    d = tmp_path / "data"
+    d.mkdir()
+    rng = np.random.default_rng(12)
+    paths, old = [], time.time_ns() - 30 * 10**9
+    for c in range(n):
+        p = str(d / chunk_file_name(c + 1))
+        write_chunk_file(p, ChunkFileMetaPage(sn=c + 1).encode(), rng.integers(0, 256, chunk, dtype=np.uint8).tobytes())
+        os.utime(p, ns=(old, old))  # written long before the jobs: tables are not racy
+        paths.append(p)
+    names = sorted(chunk_file_name(c + 1) for c in range(n))  # std::sort order: chunk_1, chunk_10, chunk_11, chunk_12, chunk_2 ...
+    svc = I.IntegrityService(chunk_size=chunk, batch=16)
+    try:
+        svc.ScheduleJob(1, 1, str(d))
+        j = svc.wait(1, 180)
+        assert j.state == I.IntegrityJobState.FINISHED, j.error
+        assert [r.name for r in j.results] == names
+        assert all(r.table == "created" and r.status == 0 and r.bad_pages == 0 for r in j.results), j.results
+        for c in (0, n - 1):  # a file of each staging batch: the table is the oracle's CRCs of its data
+            _, tab = I.load_table(I.sidecar_path(paths[c]))
+            with open(paths[c], "rb") as f:
+                assert (tab == oracle.page_crcs(np.frombuffer(f.read()[meta:], dtype=np.uint8), pb)).all()
+        rot = names.index(chunk_file_name(9))      # position 11 of 12: the second staging batch
+        assert rot >= 7
+        _flip(paths[8], meta + 4095 * pb + 77)      # last page of chunk_9
+        with open(paths[1], "r+b") as f:            # chunk_2: a write that skipped its table
+            f.seek(meta + 123_456)
+            f.write(b"unrecorded write")
+        tp = I.sidecar_path(paths[6])               # chunk_7: its table rots
+        with open(tp, "r+b") as f:
+            f.seek(64 + 4 * 1000)
+            f.write(b"\xde\xad\xbe\xef")
+        _flip(paths[4], 3)                          # chunk_5: metapage header (sn) no longer matches its CRC
+        unreadable = os.geteuid() != 0
+        if unreadable:
+            os.chmod(paths[10], 0)                  # chunk_11: cannot be opened
+        svc.ScheduleJob(2, 1, str(d))
+        j = svc.wait(2, 180)
+        assert j.state == I.IntegrityJobState.FINISHED, j.error
+        res = {r.name: r for r in j.results}
+        assert len(res) == n
+        r = res[chunk_file_name(9)]
+        assert (r.table, r.bad_pages, r.first_bad, r.bad_list, r.status) == ("ok", 1, 4095, [4095], 0)
+        assert (res[chunk_file_name(2)].table, res[chunk_file_name(2)].bad_pages) == ("refreshed", 0)
+        assert (res[chunk_file_name(7)].table, res[chunk_file_name(7)].bad_pages) == ("rebuilt", 0)
+        assert res[chunk_file_name(5)].status == _lib.CC_ECORRUPT
+        if unreadable:
+            assert res[chunk_file_name(11)].status == -13  # -EACCES
+        special = {chunk_file_name(c) for c in (9, 2, 7, 5, 11)}
+        assert all(x.status == 0 and x.table == "ok" and x.bad_pages == 0 for k, x in res.items() if k not in special)
+        # the refreshed / rebuilt tables describe the current bytes
+        for c in (1, 6):
+            _, tab = I.load_table(I.sidecar_path(paths[c]))
+            with open(paths[c], "rb") as f:
+                assert (tab == oracle.page_crcs(np.frombuffer(f.read()[meta:], dtype=np.uint8), pb)).all()
+        if unreadable:
+            os.chmod(paths[10], 0o644)
+        # a file that vanishes between a job's listing and its check: that file's -ENOENT
+        got = I.check_files([paths[0], str(d / "chunk_999")],
+                            [I.sidecar_path(paths[0]), I.sidecar_path(str(d / "chunk_999"))], chunk, meta, pb)
+        assert got[0].status == 0 and got[0].bad_pages == 0 and got[1].status == -2
+    finally:
+        svc.close()
+
+
+def test_racy_table_never_condemns_a_same_tick_write(dev, oracle, tmp_path):
+    """mtime comes from a coarse clock, so a second write in the same
+    tick as the one a table was stored after leaves the identity unchanged.
+    Such a table is racy (stamp within a tick of the mtime): a mismatch makes it
+    STALE and refreshed, never bad pages; once re-stamped a tick later, real
+    bit rot with the mtime restored is reported page-exact again."""
+    import time
+    from curve_amd import integrity as I
+    from curve_amd.chunkfile import ChunkFileMetaPage, chunk_file_name, write_chunk_file
+    chunk, pb = 1 << 20, 4096
+    d = tmp_path / "data"
+    d.mkdir()
+    p = str(d / chunk_file_name(1))
+    data = np.random.default_rng(1).integers(0, 256, chunk, dtype=np.uint8)
+    write_chunk_file(p, ChunkFileMetaPage(sn=1).encode(), data.tobytes())
+    # the write path's pwrite and its table in the same tick -- made certain
+    # whatever the kernel's tick by an mtime 200 ms ahead of the clock
+    m = time.time_ns() + 200_000_000
+    os.utime(p, ns=(m, m))
+    I.store_table(p, oracle.page_crcs(data, pb), pb)  # racy: stamped before mtime + one tick
+    _flip(p, 4096 + 10 * pb)                          # a second write in that tick: same mtime
+    svc = I.IntegrityService(chunk_size=chunk)
+    try:
+        svc.ScheduleJob(1, 1, str(d))
+        r = svc.wait(1, 60).results[0]
+        assert (r.table, r.bad_pages) == ("refreshed", 0)
+        time.sleep(0.5)                               # the clock passes mtime + one tick
+        svc.ScheduleJob(2, 1, str(d))                 # racy but matching: re-stamped after the mtime
+        r = svc.wait(2, 60).results[0]
+        assert (r.table, r.bad_pages) == ("ok", 0)
+        _flip(p, 4096 + 200 * pb + 9)                 # bit rot now: reported
+        svc.ScheduleJob(3, 1, str(d))
+        r = svc.wait(3, 60).results[0]
+        assert (r.table, r.bad_pages, r.bad_list) == ("ok", 1, [200])
+    finally:
+        svc.close()
