@@ -303,10 +303,12 @@ def files_leg(args):
         shutil.rmtree(d, ignore_errors=True)
 
 
-def warm_clock(fn, ms=60.0):
+def warm_clock(fn, ms=1000.0):
     """Run `fn` back to back for about `ms` of wall time, untimed: after host-side
     setup the GPU has idled and its clock ramps back over ~10-30 ms of work (a
-    kernel trace shows the first launches of a leg 5-25 % slow)."""
+    kernel trace shows the first launches of a leg 5-25 % slow), and a fresh box
+    needs about a second of sustained load to reach its steady rate -- every
+    leg gets the main leg's floor (--clock-warm-ms)."""
     t0 = time.perf_counter()
     while (time.perf_counter() - t0) * 1e3 < ms:
         for _ in range(4):
@@ -343,7 +345,7 @@ def partial_write_leg(pool, args):
             touched += len(np.unique(np.concatenate([p0, p1])))
             upd_bytes += int(lens.sum())
     # warm: work buffer, and the clock ramp after the host-side setup
-    warm_clock(lambda: C.apply_log(flat, pool.page_crcs, src, logs[0][0], U, 4096, 4096))
+    warm_clock(lambda: C.apply_log(flat, pool.page_crcs, src, logs[0][0], U, 4096, 4096), args.clock_warm_ms)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in logs[1:]]
     for (d_log, _), (e0, e1) in zip(logs[1:], ev):
         e0.record(stream)
@@ -377,6 +379,7 @@ def partial_write_leg(pool, args):
     alg = (2 * upd_bytes + touched * (4096 + 4)) / nb
     return {"updates_per_batch": U, "batches": nb,
             "device_ms_per_batch": round(ms, 4),
+            "ms_median": round(float(np.median(dev_ms)), 4),
             "ms_each": [round(x, 4) for x in dev_ms],
             "updates_per_s": round(U / (ms * 1e-3), 1),
             "touched_pages_per_batch": touched // nb,
@@ -417,7 +420,8 @@ def read_verify_leg(pool, args):
         if it:
             pages += int(npg.sum())
     # untimed: work buffer, and the clock ramp after the host-side setup
-    warm_clock(lambda: C.verify_read_records(flat, pool.page_crcs, batches[0][0], n, bad, total, pb))
+    warm_clock(lambda: C.verify_read_records(flat, pool.page_crcs, batches[0][0], n, bad, total, pb),
+               args.clock_warm_ms)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in batches[1:]]
     for (d_reads, _, _), (e0, e1) in zip(batches[1:], ev):
         e0.record(stream)
@@ -435,6 +439,8 @@ def read_verify_leg(pool, args):
     t = float(np.mean(ms))
     per = pages / len(ms)
     return {"reads_per_batch": n, "pages_per_batch": int(per), "ms_per_batch": round(t, 4),
+            "ms_median": round(float(np.median(ms)), 4),
+            "alg_frac_of_hbm_peak_at_median": round(per * (pb + 4) / (float(np.median(ms)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "ms_each": [round(x, 4) for x in ms],
             "GiBps_verified": round(per * pb / GiB / (t * 1e-3), 1),
             "alg_frac_of_hbm_peak": round(per * (pb + 4) / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -473,7 +479,7 @@ def wal_replay_leg(pool, args):
         C.check(L.cc_crc_ranges_dev(flat.data_ptr(), d_rec.data_ptr(), n, out.data_ptr(),
                                     C._stream_handle(stream)), "cc_crc_ranges_dev")
 
-    warm_clock(call)  # untimed: the clock ramp after the host-side setup (as the main leg's warm-up)
+    warm_clock(call, args.clock_warm_ms)  # untimed: the clock ramp after the host-side setup (the main leg's floor)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
     for e0, e1 in ev:  # back to back, as a replay issues its segments
         e0.record(stream)
@@ -488,6 +494,8 @@ def wal_replay_leg(pool, args):
     t = float(np.mean(ms))
     data = float(real.sum())
     return {"entries_per_batch": n, "data_bytes_per_batch": int(data), "ms_per_batch": round(t, 4),
+            "ms_median": round(float(np.median(ms)), 4),
+            "alg_frac_of_hbm_peak_at_median": round((data + 4 * n) / (float(np.median(ms)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "ms_each": [round(x, 4) for x in ms],
             "entries_per_s": round(n / (t * 1e-3), 1), "GBps": round(data / (t * 1e-3) / 1e9, 1),
             "alg_frac_of_hbm_peak": round((data + 4 * n) / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

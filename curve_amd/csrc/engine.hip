@@ -242,7 +242,7 @@ void geometry_for(const DevCtx* c, uint64_t n_pages, PageLaunch* a) {
 #define CC_PAGE_DYN_DIV 16  // 1/16 of a large launch's tiles form the dynamic tail (0: static only; A/B 2.464 ms vs 2.474-2.478 at 1/8, 2.474 at 1/12, 2.51 at 1/24 and 1/32)
 #endif
 // Page kernel launch with the dynamic tail (kernels.hip, page_crc_kernel) when
-// the batch is large: a stream-ordered, zeroed 8-byte chunk counter per call --
+// the batch is large: stream-ordered, zeroed chunk counters (kDynHeads) per call --
 // `zeroed_ctr` if the caller has one (zeroed on the stream before this launch:
 // cc_pool_scan_dev has the metapage launch clear it), else allocated + memset.
 hipError_t launch_page_tail(const DevCtx* c, PageLaunch& a, bool verify, hipStream_t s,
@@ -261,9 +261,9 @@ hipError_t launch_page_tail(const DevCtx* c, PageLaunch& a, bool verify, hipStre
         return launch();
     }
     unsigned long long* ctr = nullptr;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(*ctr), s);
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ctr), kDynCtrBytes, s);
     if (e != hipSuccess) return e;
-    if ((e = hipMemsetAsync(ctr, 0, sizeof(*ctr), s)) == hipSuccess) {
+    if ((e = hipMemsetAsync(ctr, 0, kDynCtrBytes, s)) == hipSuccess) {
         a.dyn_ctr = ctr;
         e = launch();
     }
@@ -507,7 +507,7 @@ int pool_page_launches(const void* d_data, uint64_t n_data_pages, uint32_t page_
     int rc = get_ctx(&c);
     if (rc) return rc;
     unsigned long long* ctr = nullptr;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(*ctr), s);
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ctr), kDynCtrBytes, s);
     if (e != hipSuccess) return map_err(e);
     PageLaunch m = {};
     m.pages = static_cast<const uint32_t*>(d_meta);
@@ -517,7 +517,7 @@ int pool_page_launches(const void* d_data, uint64_t n_data_pages, uint32_t page_
     m.kconst = kconst_for(meta_bytes);
     m.out = d_meta_crcs;
     m.zero[0] = reinterpret_cast<uint32_t*>(ctr);
-    m.zero_words[0] = sizeof(*ctr) / 4;
+    m.zero_words[0] = kDynCtrBytes / 4;
     m.zero[1] = d_digest;
     m.zero_words[1] = d_digest ? digest_words : 0;
     geometry_for(c.get(), n_meta, &m);  // static walk (a tail would need a counter of its own)

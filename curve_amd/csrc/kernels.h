@@ -18,6 +18,12 @@ constexpr uint32_t kWaveBytes = 256;        // bytes consumed per wave step
 #endif
 constexpr int kWavesPerBlock = CC_WAVES;
 constexpr int kBlockThreads = 64 * kWavesPerBlock;
+#ifndef CC_PAGE_DYN_HEADS
+#define CC_PAGE_DYN_HEADS 8  // dynamic-tail counters of the page kernel: 1, or one per XCD (8)
+#endif
+constexpr uint32_t kDynHeads = CC_PAGE_DYN_HEADS;
+constexpr uint32_t kDynHeadStride = 16;  // 128 bytes between heads: one cache line each
+constexpr uint32_t kDynCtrBytes = kDynHeads * kDynHeadStride * 8;
 
 // Host builder of the 160 KiB LDS image (engine.hip).
 void build_lds_image(uint32_t* image /* kLdsBytes/4 words */);
@@ -44,7 +50,7 @@ struct PageLaunch {
     uint32_t tile_shift;      // 2^tile_shift consecutive pages per wave tile (0..6)
     // dynamic tail: null = every tile in the strided static walk; else tiles
     // [static_tiles, all) are handed out through this zeroed counter
-    unsigned long long* dyn_ctr;
+    unsigned long long* dyn_ctr;  // kDynHeads counters, kDynHeadStride words apart (zeroed before the launch)
     uint64_t static_tiles;
     // block 0 zeroes these word ranges before its walk (stream-ordered for the
     // kernels after it: the next launch's tail counter, a digest to XOR into)

@@ -280,6 +280,13 @@ __device__ __forceinline__ void chains(const uint32_t* tab, const uint32_t (&w)[
 #ifndef CC_PAGE_DYN_PAGES
 #define CC_PAGE_DYN_PAGES 64  // pages per dynamic chunk (A/B: 64 beats 128)
 #endif
+// Dynamic-tail heads (kernels.h kDynHeads): 1 = one counter for the whole grid;
+// 8 = one per XCD (MI355X_MICROARCH.md "dequeue": one word saturates at ~88
+// dequeues/us, shard above 64 pullers).  With 8 heads the tail's chunks are cut
+// into 8 contiguous regions; a wave pulls from its own XCD's region
+// (blockIdx.x % 8: workgroups go round-robin over the XCDs -- placement is
+// speed only, never correctness) and, once that is drained, steals from the
+// next regions in turn.
 struct ZeroRanges {
     uint32_t* p[2];
     uint64_t n[2];
@@ -316,6 +323,7 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
     W.wstride = ((uint64_t)gridDim.x * kWavesPerBlock) << tshift;
     W.wfirst = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) << tshift;
     uint64_t lim = dyn_ctr ? (static_tiles << tshift < n_pages ? static_tiles << tshift : n_pages) : n_pages;
+    uint32_t dyn_head = blockIdx.x % kDynHeads, dyn_tried = 0;  // this XCD's tail region first
 #pragma unroll 1
     for (;;) {
         if (W.wfirst < lim) {
@@ -356,10 +364,27 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
         }
         if (!dyn_ctr) break;
         // next dynamic chunk: CC_PAGE_DYN_PAGES consecutive pages
-        unsigned long long c = 0;
-        if (lane == 0) c = atomicAdd(dyn_ctr, 1ull);
-        c = readlane64(c, 0);
-        const uint64_t p0 = (static_tiles << tshift) + c * CC_PAGE_DYN_PAGES;
+        const uint64_t tail0 = static_tiles << tshift;
+        uint64_t p0 = n_pages;
+        if constexpr (kDynHeads == 1) {
+            unsigned long long c = 0;
+            if (lane == 0) c = atomicAdd(dyn_ctr, 1ull);
+            c = readlane64(c, 0);
+            p0 = tail0 + c * CC_PAGE_DYN_PAGES;
+        } else {
+            const uint64_t chunks = (n_pages - tail0 + CC_PAGE_DYN_PAGES - 1) / CC_PAGE_DYN_PAGES;
+            const uint64_t per = (chunks + kDynHeads - 1) / kDynHeads;
+            for (; dyn_tried < kDynHeads; dyn_tried++, dyn_head = (dyn_head + 1) % kDynHeads) {
+                unsigned long long c = 0;
+                if (lane == 0) c = atomicAdd(dyn_ctr + dyn_head * kDynHeadStride, 1ull);
+                c = readlane64(c, 0);
+                const uint64_t chunk = dyn_head * per + c;
+                if (c < per && chunk < chunks) {
+                    p0 = tail0 + chunk * CC_PAGE_DYN_PAGES;
+                    break;
+                }
+            }
+        }
         if (p0 >= n_pages) break;
         W.wfirst = p0;
         W.wstride = 1ull << tshift;  // consecutive tiles: page(k) = p0 + k

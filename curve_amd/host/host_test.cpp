@@ -527,6 +527,11 @@ void IntegrityWritePath() {
     o.batch = 4;
     IntegrityService svc2(o);
     IntegrityJob j;
+    // the tables were stored within a clock tick of the pwrites: racy
+    // (cc_pcrc_is_racy).  Job 1 re-stamps them once the clock has moved a tick
+    // past the writes, so that bit rot with the mtime restored (job 3) is
+    // provably not a same-tick write.
+    usleep(50000);
     EXPECT(svc2.ScheduleJob(1, 1, dd) == INTEGRITY_OP_STATUS_SUCCESS);
     EXPECT(svc2.Wait(1, 60000, &j) && j.state == INTEGRITY_OP_STATE_FINISHED);
     EXPECT(j.results.size() == n_chunks);
