@@ -1169,9 +1169,12 @@ def test_integrity_job_sidecars(dev, oracle, tmp_path):
     datas = {}
     tmp_path = tmp_path / "data"  # <copyset>/data; sidecars go to <copyset>/pcrc
     tmp_path.mkdir()
+    import time
+    old = time.time_ns() - 30 * 10**9  # written long before the job: its tables are not racy (cc_pcrc_is_racy)
     for cid in range(1, 8):
         data = rng.integers(0, 256, chunk, dtype=np.uint8)
         CF.write_chunk_file(str(tmp_path / CF.chunk_file_name(cid)), CF.ChunkFileMetaPage(sn=cid).encode(), data.tobytes())
+        os.utime(str(tmp_path / CF.chunk_file_name(cid)), ns=(old, old))
         datas[cid] = data
     svc = I.IntegrityService(chunk_size=chunk, batch=3)
     try:
