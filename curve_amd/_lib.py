@@ -110,9 +110,6 @@ SIGNATURES = {
     "cc_digest_dev": (_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
     "cc_page_crc_host": (_int, [_vp, _u64, _u32, _vp]),
     "cc_lds_image": (_int, [_vp, _sz]),
-    "cc_plan_updates": (_int, [_vp, _u64, _vp, _vp, _u32, ctypes.POINTER(_u32)]),
-    "cc_update_work_bytes": (_u64, [_u64, _u64, _u32, _u32]),
-    "cc_apply_updates_dev": (_int, [_vp, _u64, _u32, _vp, _vp, _u64, _vp, _u32, _u32, _vp, _vp, _u64, _vp]),
     "cc_scan_files": (_int, [ctypes.POINTER(ctypes.c_char_p), _u64, _u32, _u32, _u32, _u32, _u32, _vp,
                               ctypes.POINTER(CcFileResult)]),
     "cc_scan_host": (_int, [ctypes.POINTER(CcChunkSrc), _u64, _u32, _u32, _u32, _u32, _vp, _vp, _vp]),

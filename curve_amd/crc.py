@@ -443,93 +443,6 @@ def _update_dtype():
     return UPDATE_DTYPE
 
 
-def split_nonoverlapping(dst, lens):
-    """Split an ORDERED list of byte-range writes into batches whose members do
-    not overlap each other; applying the batches one after another equals
-    applying the writes in order (later writes win, as the raft log orders them,
-    op_request.cpp:429-481).  Level assignment: level(j) = 1 + max level of the
-    earlier writes j overlaps (0 if none); batch b = writes of level b.  The
-    overlap sweep is vectorised (sort by start, running max of ends): random
-    4 KiB writes over 16 GiB overlap in ~0.8 % of cases and need 2-3 batches.
-    Returns a list of index arrays (ascending)."""
-    import numpy as np
-    dst = np.asarray(dst, dtype=np.int64)
-    end = dst + np.asarray(lens, dtype=np.int64)
-    n = dst.size
-    if n == 0:
-        return []
-    order = np.argsort(dst, kind="stable")
-    s_start, s_end = dst[order], end[order]
-    run_max = np.maximum.accumulate(s_end)
-    new_cluster = np.ones(n, dtype=bool)
-    new_cluster[1:] = s_start[1:] >= run_max[:-1]
-    if new_cluster.all():
-        return [np.arange(n)]  # no overlaps at all: one batch
-    level = np.zeros(n, dtype=np.int64)
-    starts = np.flatnonzero(new_cluster)
-    sizes = np.diff(np.append(starts, n))
-    for c in np.flatnonzero(sizes > 1):  # only the (few, small) overlapping clusters
-        mem = np.sort(order[starts[c]:starts[c] + sizes[c]])  # original (write) order
-        _cluster_levels(dst, end, mem, level)
-    return [np.flatnonzero(level == v) for v in range(int(level.max()) + 1)]
-
-
-def _cluster_levels(dst, end, mem, level):
-    """Levels of one cluster of overlapping writes, in write order: a max
-    segment tree over the cluster's distinct endpoints (values = level + 1 of
-    the latest-levelled write covering each elementary segment): O(k log k)."""
-    import numpy as np
-    xs = np.unique(np.concatenate([dst[mem], end[mem]]))
-    size = 1
-    while size < xs.size - 1:
-        size <<= 1
-    mx = [0] * (2 * size)
-    tag = [0] * (2 * size)
-
-    def query(v, vl, vr, l, r):
-        if r <= vl or vr <= l:
-            return 0
-        if l <= vl and vr <= r:
-            return mx[v]
-        mid = (vl + vr) // 2
-        return max(tag[v], query(2 * v, vl, mid, l, r), query(2 * v + 1, mid, vr, l, r))
-
-    def update(v, vl, vr, l, r, val):
-        if r <= vl or vr <= l:
-            return
-        if l <= vl and vr <= r:
-            mx[v] = max(mx[v], val)
-            tag[v] = max(tag[v], val)
-            return
-        mid = (vl + vr) // 2
-        update(2 * v, vl, mid, l, r, val)
-        update(2 * v + 1, mid, vr, l, r, val)
-        mx[v] = max(mx[v], mx[2 * v], mx[2 * v + 1])
-
-    for j in mem:
-        l = int(np.searchsorted(xs, dst[j]))
-        r = int(np.searchsorted(xs, end[j]))
-        lv = query(1, 0, size, l, r)
-        level[j] = lv
-        update(1, 0, size, l, r, lv + 1)
-
-
-def plan_updates(rec_in, max_batches: int = 1 << 16):
-    """cc_plan_updates: write-ordered update records -> (records grouped by
-    overlap level, batch end indices, number of batches)."""
-    import numpy as np
-    n = rec_in.size
-    out = np.empty_like(rec_in)
-    ends = np.zeros(max(1, min(max_batches, n)), dtype=np.uint64)
-    nb = ctypes.c_uint32(0)
-    check(lib().cc_plan_updates(ctypes.c_void_p(rec_in.ctypes.data), n, ctypes.c_void_p(out.ctypes.data),
-                                ctypes.c_void_p(ends.ctypes.data), ends.size, ctypes.byref(nb)), "cc_plan_updates")
-    return out, ends[:nb.value].copy(), nb.value
-
-
-_work_cache = {}
-
-
 def log_records(dst_off, src_off, lens):
     """Write log (in write order) as cc_update records (numpy structured array)."""
     import numpy as np
@@ -596,48 +509,6 @@ def apply_updates(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int 
     if stream is not None:
         d_log.record_stream(stream)
     return n
-
-
-def apply_updates_batched(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int = PAGE_SIZE, stream=None):
-    """Client partial-write path on device (cc_apply_updates_dev): write
-    src[src_off[i]:+lens[i]] to pool[dst_off[i]:+lens[i]] in order, then
-    recompute the CRC of every touched page in `page_crcs` (in place).
-    Returns the number of device calls (batches) used."""
-    import numpy as np
-    torch = _torch()
-    dst_off = np.asarray(dst_off, dtype=np.uint64)
-    src_off = np.asarray(src_off, dtype=np.uint64)
-    lens = np.asarray(lens, dtype=np.uint32)
-    if not (dst_off.size == src_off.size == lens.size):
-        raise CurveCrcError(_lib.CC_EINVAL, "dst/src/len size mismatch")
-    if (lens == 0).any() or (dst_off + lens > _nbytes(pool)).any() or (src_off + lens > _nbytes(src)).any():
-        raise CurveCrcError(_lib.CC_EINVAL, "update out of range or empty")
-    n_pages = _nbytes(pool) // page_bytes
-    max_len = int(lens.max()) if lens.size else 1
-    need = int(lib().cc_update_work_bytes(n_pages, dst_off.size, max_len, page_bytes))
-    # scratch per (device, stream), as apply_log: calls on different streams may overlap
-    key = _stream_key(pool.device, stream)
-    work = _work_cache.get(key)
-    if work is None or work.numel() < need:
-        with _on_stream(stream):
-            work = torch.empty(need, dtype=torch.uint8, device=pool.device)
-        _work_cache[key] = work
-    rec_in = np.zeros(dst_off.size, dtype=_update_dtype())
-    rec_in["dst"], rec_in["src"], rec_in["len"] = dst_off, src_off, lens
-    rec, ends, nb = plan_updates(rec_in)
-    with _on_stream(stream):
-        d_upd = torch.from_numpy(rec.view(np.uint8)).to(pool.device, non_blocking=False)
-    with torch.cuda.device(pool.device):
-        check(lib().cc_apply_updates_dev(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, _dev_ptr(src, "src"),
-                                         _dev_ptr(d_upd, "updates"), rec.size,
-                                         ctypes.c_void_p(ends.ctypes.data), nb, max_len,
-                                         _dev_ptr(page_crcs, "page_crcs"), _dev_ptr(work, "work"), work.numel(),
-                                         _stream_handle(stream)),
-              "cc_apply_updates_dev")
-    if stream is not None:  # buffers must outlive the kernels on `stream`
-        d_upd.record_stream(stream)
-        work.record_stream(stream)
-    return nb
 
 
 _reads_work = {}

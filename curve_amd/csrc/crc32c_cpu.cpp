@@ -164,107 +164,3 @@ int cc_slice_fold(const uint32_t* page_crcs, uint64_t n_pages, uint32_t pages_pe
 
 }  // extern "C"
 
-// ---------------------------------------------------------------------------
-// Partial-write planner (host logic for cc_apply_updates_dev).
-// ---------------------------------------------------------------------------
-extern "C" int cc_plan_updates(const cc_update* in, uint64_t n, cc_update* out, uint64_t* batch_ends,
-                               uint32_t max_batches, uint32_t* n_batches) {
-    if (!n_batches) return CC_EINVAL;
-    *n_batches = 0;
-    if (n == 0) return CC_OK;
-    if (!in || !out || !batch_ends || max_batches == 0 || n > 0xFFFFFFFFull) return CC_EINVAL;
-    // LSD radix sort of (dst, index) pairs, 12-bit digits (count arrays stay
-    // in L1), only as many passes as the largest dst needs
-    uint64_t maxd = 0;
-    std::vector<uint64_t> key(n), ktmp(n);
-    std::vector<uint32_t> idx(n), tmp(n);
-    for (uint64_t i = 0; i < n; i++) {
-        key[i] = in[i].dst;
-        idx[i] = (uint32_t)i;
-        maxd = std::max(maxd, in[i].dst);
-    }
-    for (int shift = 0; shift < 64 && (maxd >> shift); shift += 12) {
-        uint32_t cnt[4097] = {0};
-        for (uint64_t i = 0; i < n; i++) cnt[((key[i] >> shift) & 0xFFF) + 1]++;
-        for (int d = 0; d < 4096; d++) cnt[d + 1] += cnt[d];
-        for (uint64_t i = 0; i < n; i++) {
-            const uint32_t pos = cnt[(key[i] >> shift) & 0xFFF]++;
-            ktmp[pos] = key[i];
-            tmp[pos] = idx[i];
-        }
-        key.swap(ktmp);
-        idx.swap(tmp);
-    }
-    // sweep: clusters of transitively overlapping writes (running max of ends);
-    // inside a cluster, levels in WRITE order through a max segment tree over
-    // the cluster's distinct endpoints: level(j) = max over the elementary
-    // segments j covers of (1 + level of an earlier write covering them), then
-    // j raises its segments to level(j) + 1 -- O(k log k) per cluster of k
-    std::vector<uint32_t> level(n, 0);
-    uint32_t maxlv = 0;
-    uint64_t i = 0;
-    std::vector<uint32_t> mem;
-    std::vector<uint64_t> xs;
-    std::vector<uint32_t> mx, tag;
-    while (i < n) {
-        uint64_t j = i + 1;
-        uint64_t run_end = in[idx[i]].dst + in[idx[i]].len;
-        while (j < n && in[idx[j]].dst < run_end) {
-            run_end = std::max(run_end, in[idx[j]].dst + in[idx[j]].len);
-            j++;
-        }
-        if (j - i > 1) {  // overlapping cluster
-            mem.assign(idx.begin() + i, idx.begin() + j);
-            std::sort(mem.begin(), mem.end());  // write order
-            xs.clear();
-            for (uint32_t m : mem) {
-                xs.push_back(in[m].dst);
-                xs.push_back(in[m].dst + in[m].len);
-            }
-            std::sort(xs.begin(), xs.end());
-            xs.erase(std::unique(xs.begin(), xs.end()), xs.end());
-            const size_t segs = xs.size() - 1;  // elementary segments [xs[k], xs[k+1])
-            size_t size = 1;
-            while (size < segs) size <<= 1;
-            mx.assign(2 * size, 0);
-            tag.assign(2 * size, 0);
-            // mx[v] = max over v's range (tags included); tag[v] = value applied to all of v
-            auto update = [&](auto&& self, size_t v, size_t vl, size_t vr, size_t l, size_t r, uint32_t val) -> void {
-                if (r <= vl || vr <= l) return;
-                if (l <= vl && vr <= r) {
-                    mx[v] = std::max(mx[v], val);
-                    tag[v] = std::max(tag[v], val);
-                    return;
-                }
-                const size_t mid = (vl + vr) / 2;
-                self(self, 2 * v, vl, mid, l, r, val);
-                self(self, 2 * v + 1, mid, vr, l, r, val);
-                mx[v] = std::max(mx[v], std::max(mx[2 * v], mx[2 * v + 1]));
-            };
-            auto query = [&](auto&& self, size_t v, size_t vl, size_t vr, size_t l, size_t r) -> uint32_t {
-                if (r <= vl || vr <= l) return 0;
-                if (l <= vl && vr <= r) return mx[v];
-                const size_t mid = (vl + vr) / 2;
-                return std::max(tag[v], std::max(self(self, 2 * v, vl, mid, l, r), self(self, 2 * v + 1, mid, vr, l, r)));
-            };
-            for (uint32_t m : mem) {
-                const size_t l = std::lower_bound(xs.begin(), xs.end(), in[m].dst) - xs.begin();
-                const size_t r = std::lower_bound(xs.begin(), xs.end(), in[m].dst + in[m].len) - xs.begin();
-                const uint32_t lv = query(query, 1, 0, size, l, r);  // stored values are level + 1
-                level[m] = lv;
-                maxlv = std::max(maxlv, lv);
-                update(update, 1, 0, size, l, r, lv + 1);
-            }
-        }
-        i = j;
-    }
-    if (maxlv + 1 > max_batches) return CC_EINVAL;
-    // stable counting placement by level (write order kept inside a level)
-    std::vector<uint64_t> start(maxlv + 2, 0);
-    for (uint64_t k = 0; k < n; k++) start[level[k] + 1]++;
-    for (uint32_t l = 0; l <= maxlv; l++) start[l + 1] += start[l];
-    for (uint32_t l = 0; l <= maxlv; l++) batch_ends[l] = start[l + 1];
-    for (uint64_t k = 0; k < n; k++) out[start[level[k]]++] = in[k];
-    *n_batches = maxlv + 1;
-    return CC_OK;
-}

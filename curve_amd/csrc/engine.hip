@@ -24,7 +24,6 @@
 #include <memory>
 #include <mutex>
 #include <thread>
-#include <unordered_map>
 #include <vector>
 
 #include "../../include/curve_crc.h"
@@ -101,8 +100,6 @@ struct DevCtx {
     std::mutex tab_mu;  // epilogue-table inserts
     std::atomic<uint64_t> epi_key[kEpiSlots];  // key + 1 (0 = empty); published after epi_ptr
     std::atomic<void*> epi_ptr[kEpiSlots];
-    std::mutex work_mu;  // partial-write generation tags (cc_apply_updates_dev)
-    std::unordered_map<void*, std::pair<uint32_t, uint64_t>> work_gen;  // work buffer -> (gen, n_pages)
     DevCtx() {
         for (int i = 0; i < kEpiSlots; i++) {
             epi_key[i].store(0);
@@ -887,75 +884,6 @@ int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
     }
     if ((rc = ring.drain(slot, take(slot)))) return rc;
     return ring.drain(slot ^ 1, take(slot ^ 1));
-}
-
-uint64_t cc_update_work_bytes(uint64_t n_pages, uint64_t n_updates, uint32_t max_len, uint32_t page_bytes) {
-    (void)n_updates;
-    (void)max_len;
-    if (page_bytes == 0) return 0;
-    return (n_pages * 4 + 255) & ~255ull;  // one generation tag per page
-}
-
-int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
-                         const cc_update* d_updates, uint64_t n_updates, const uint64_t* h_batch_ends,
-                         uint32_t n_batches, uint32_t max_len, uint32_t* d_page_crcs, void* d_work,
-                         uint64_t work_bytes, void* stream) {
-    if (!page_size_ok(page_bytes) || page_bytes / kWaveBytes > 32) return CC_EINVAL;
-    if (n_updates == 0) return CC_OK;
-    if (!d_pool || !d_src || !d_updates || !d_page_crcs || !d_work || max_len == 0) return CC_EINVAL;
-    if (pool_bytes % page_bytes || ((uintptr_t)d_pool & 3u) || ((uintptr_t)d_src & 3u)) return CC_EINVAL;
-    const uint64_t n_pages = pool_bytes / page_bytes;
-    if (work_bytes < cc_update_work_bytes(n_pages, n_updates, max_len, page_bytes)) return CC_EINVAL;
-    CtxRef c;
-    int rc = get_ctx(&c);
-    if (rc) return rc;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    hipError_t e;
-    // generation tags: a work buffer seen for the first time (or after 2^32-1
-    // calls) is zeroed once; afterwards each call just bumps its tag.  The map
-    // is bounded: forgetting a buffer only costs it one more zeroing.
-    uint32_t gen;
-    {
-        constexpr size_t kMaxTracked = 64;
-        std::lock_guard<std::mutex> lk(c->work_mu);
-        auto it = c->work_gen.find(d_work);
-        if (it == c->work_gen.end() && c->work_gen.size() >= kMaxTracked) c->work_gen.clear();
-        auto& g = c->work_gen[d_work];
-        if (g.first == 0 || g.first == 0xFFFFFFFFu || g.second != n_pages) {
-            if ((e = hipMemsetAsync(d_work, 0, n_pages * 4, s)) != hipSuccess) return map_err(e);
-            g = {0u, n_pages};
-        }
-        gen = ++g.first;
-    }
-    UpdateLaunch a = {};
-    a.pool = static_cast<unsigned char*>(d_pool);
-    a.src = static_cast<const unsigned char*>(d_src);
-    a.upd = reinterpret_cast<const UpdateDesc*>(d_updates);
-    a.n_updates = n_updates;
-    a.page_bytes = page_bytes;
-    a.flags = static_cast<uint32_t*>(d_work);
-    a.gen = gen;
-    a.n_pages = n_pages;
-    a.image = c->image;
-    a.kconst = kconst_for(page_bytes);
-    a.page_crcs = d_page_crcs;
-    const uint64_t tiles = (n_pages + 63) / 64;
-    const uint64_t need = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    a.blocks = (int)(need < (uint64_t)c->cus ? (need ? need : 1) : (uint64_t)c->cus);
-    // batches in order (stream-ordered kernels), then ONE recompute pass
-    uint64_t first = 0;
-    const uint32_t nb = h_batch_ends ? n_batches : 1u;
-    for (uint32_t b = 0; b < nb; b++) {
-        const uint64_t last = h_batch_ends ? h_batch_ends[b] : n_updates;
-        if (last < first || last > n_updates) return CC_EINVAL;
-        UpdateLaunch ab = a;
-        ab.upd = a.upd + first;
-        ab.n_updates = last - first;
-        if ((e = launch_apply_updates(ab, s)) != hipSuccess) return map_err(e);
-        first = last;
-    }
-    if (first != n_updates) return CC_EINVAL;
-    return map_err(launch_page_list_crc(a, s));
 }
 
 namespace {

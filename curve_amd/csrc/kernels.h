@@ -92,23 +92,6 @@ struct UpdateDesc {
     uint64_t dst, src;
     uint32_t len, reserved;
 };
-struct UpdateLaunch {
-    unsigned char* pool;
-    const unsigned char* src;
-    const UpdateDesc* upd;
-    uint64_t n_updates;
-    uint32_t page_bytes;
-    uint32_t* flags;            // one word per pool page: == gen <=> touched by this call
-    uint32_t gen;               // generation tag of this call (never 0)
-    uint64_t n_pages;
-    // recompute
-    const void* image;
-    uint32_t kconst;
-    uint32_t* page_crcs;
-    int blocks;
-};
-hipError_t launch_apply_updates(const UpdateLaunch& a, hipStream_t s);
-hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s);
 
 // Write-log path (cc_apply_log_dev): every update of an ORDERED log becomes
 // `slots` pieces, one per page it touches; an open-addressing table keyed by

@@ -993,90 +993,6 @@ __global__ void shift_kernel(const uint32_t* __restrict__ crcs, const uint64_t* 
 }
 
 // ---------------------------------------------------------------------------
-// Partial-write path (BASELINE config 3)
-// ---------------------------------------------------------------------------
-// One wave per update.  Destination-aligned dwords in the middle of the range
-// are assembled from two source dwords with v_alignbyte and stored whole; the
-// (at most 3 + 3) head/tail bytes are stored as bytes, so two non-overlapping
-// updates that share a boundary dword never race.  Lane 0 tags the touched
-// pages with this call's generation (plain stores: every writer writes the
-// same value, no atomics, no clearing between calls).
-__global__ __launch_bounds__(256) void apply_updates_kernel(UpdateLaunch a) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (u >= a.n_updates) return;
-    const UpdateDesc d = a.upd[u];
-    const uint64_t dst = d.dst, src = d.src, len = d.len;
-    if (len == 0) return;
-    const uint64_t end = dst + len;
-    uint64_t w0 = (dst + 3) & ~3ull;  // first full dst dword
-    uint64_t w1 = end & ~3ull;        // end of full dst dwords
-    if (w0 >= w1) w0 = w1 = end;      // no full dword: all bytes are "head"
-    // head bytes [dst, w0) and tail bytes [w1, end): at most 3 + 3 (or len < 8)
-    const uint64_t nhead = w0 - dst, ntail = end - w1;
-    if (lane < nhead) a.pool[dst + lane] = a.src[src + lane];
-    if (lane < ntail) a.pool[w1 + lane] = a.src[src + (w1 - dst) + lane];
-    if (w0 < w1) {
-        const uint64_t delta = src - dst;  // modular: source byte of dst byte p is p + delta
-        for (uint64_t w = w0 + 4ull * lane; w < w1; w += 256) {
-            const uint64_t sb = w + delta;  // source byte address of dst word w
-            const uint64_t sa = sb & ~3ull;
-            const uint32_t sh = (uint32_t)(sb & 3u);
-            const uint32_t lo = *reinterpret_cast<const uint32_t*>(a.src + sa);
-            // the high dword is only needed (and only in range) when misaligned
-            const uint32_t hi = sh ? *reinterpret_cast<const uint32_t*>(a.src + sa + 4) : 0u;
-            *reinterpret_cast<uint32_t*>(a.pool + w) = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
-        }
-    }
-    if (lane == 0) {
-        const uint64_t p0 = dst / a.page_bytes, p1 = (end - 1) / a.page_bytes;
-        for (uint64_t p = p0; p <= p1; p++) a.flags[p] = a.gen;
-    }
-}
-
-// Recompute the CRCs of the pages tagged with this call's generation.  Waves
-// walk 64-page tiles: one coalesced flag load, a ballot, then the flagged pages
-// (next page's loads issued before the current page is hashed); the tile's new
-// CRCs leave as one store masked to the flagged lanes.
-template <int M>
-__global__ __launch_bounds__(kBlockThreads) void page_flagged_kernel(UpdateLaunch a) {
-    __shared__ uint32_t tab[kLdsBytes / 4];
-    fill_lds(tab, static_cast<const uint4*>(a.image));
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t c0 = lane << 2 & 0x7Cu;
-    const uint32_t c1 = c0 | 0x10000u;
-    const uint32_t cf = kFinBase + (lane << 2);
-    const uint32_t* pages = reinterpret_cast<const uint32_t*>(a.pool) + lane;
-    const uint64_t n_tiles = (a.n_pages + 63) >> 6;
-    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + wave; t < n_tiles;
-         t += (uint64_t)gridDim.x * kWavesPerBlock) {
-        const uint64_t p = (t << 6) + lane;
-        const bool mine = p < a.n_pages && a.flags[p] == a.gen;
-        uint64_t bits = __ballot(mine);
-        if (!bits) continue;
-        uint32_t acc = 0;
-        uint32_t A[M], B[M];
-        uint32_t cur = (uint32_t)__builtin_ctzll(bits);
-        bits &= bits - 1;
-        load_page<M>(A, pages + ((t << 6) + cur) * (64u * M));
-        for (;;) {
-            const bool more = bits != 0;
-            const uint32_t nxt = more ? (uint32_t)__builtin_ctzll(bits) : cur;
-            bits &= bits - 1;
-            if (more) load_page<M>(B, pages + ((t << 6) + nxt) * (64u * M));
-            const uint32_t crc = wave_xor(apply_fin(tab, chain<M>(tab, A, c0, c1), cf)) ^ a.kconst;
-            acc = lane == cur ? crc : acc;
-            if (!more) break;
-#pragma unroll
-            for (int j = 0; j < M; j++) A[j] = B[j];
-            cur = nxt;
-        }
-        if (mine) __builtin_nontemporal_store(acc, a.page_crcs + p);
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Write-log path (cc_apply_log_dev): ordering on the device, no host planning.
 // ---------------------------------------------------------------------------
 // Grouping by page without a sort.  Piece t = (update t / slots, its k-th page,
@@ -2088,29 +2004,6 @@ hipError_t launch_shift(const uint32_t* crcs, const uint64_t* shift_bytes, uint6
     if (n == 0) return hipSuccess;
     const uint64_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(shift_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, crcs, shift_bytes, n, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_apply_updates(const UpdateLaunch& a, hipStream_t s) {  // NOLINT
-    if (a.n_updates == 0) return hipSuccess;
-    hipLaunchKernelGGL(apply_updates_kernel, dim3((uint32_t)((a.n_updates + 3) / 4)), dim3(256), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_page_list_crc(const UpdateLaunch& a, hipStream_t s) {
-    const uint32_t m = a.page_bytes / kWaveBytes;
-#define CC_LCASE(MM) \
-    case MM: hipLaunchKernelGGL((page_flagged_kernel<MM>), dim3(a.blocks), dim3(kBlockThreads), 0, s, a); break;
-    switch (m) {
-        CC_LCASE(1)
-        CC_LCASE(2)
-        CC_LCASE(4)
-        CC_LCASE(8)
-        CC_LCASE(16)
-        CC_LCASE(32)
-        default: return hipErrorInvalidValue;
-    }
-#undef CC_LCASE
     return hipGetLastError();
 }
 

@@ -1,4 +1,4 @@
-// curve_amd/csrc/log_sort.hip -- the one library primitive of the batched
+// curve_amd/csrc/read_scan.hip -- the one library primitive of the batched
 // paths, called on rocPRIM directly: the exclusive scan that lays out the page
 // slots of a batch of reads (cc_verify_reads_dev).  Kept in its own
 // translation unit: the template instantiations are heavy and nothing else

@@ -133,11 +133,14 @@ typedef struct cc_range {
 } cc_range;
 
 /* d_out[i] = crc32c_value(d_buf + off_i, len_i) for arbitrary offsets,
- * alignments and lengths (0 allowed).  One wavefront per range: meant for
- * ranges up to ~1 MiB, e.g. raft WAL entries on replay -- the data and header
- * checksums CurveSegment::_load_entry verifies with braft::crc32
- * (= butil::crc32c::Value), src/chunkserver/raftlog/curve_segment.cpp:307-371 --
- * or GetChunkHash's raw-file range (chunkserver_chunkfile.cpp:785-811). */
+ * alignments and lengths (0 allowed), e.g. raft WAL entries on replay -- the
+ * data and header checksums CurveSegment::_load_entry verifies with
+ * braft::crc32 (= butil::crc32c::Value), src/chunkserver/raftlog/curve_segment.cpp:307-371 --
+ * or GetChunkHash's raw-file range (chunkserver_chunkfile.cpp:785-811).  The
+ * batch is one stream of 4 KiB blocks split evenly over the device whatever
+ * the range sizes (a range cut between waves is hashed in segments and
+ * recombined), the last 1/32 handed out dynamically: ranges of any size mix
+ * freely.  Two launches (a tile count, then the blocks). */
 int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, uint32_t* d_out,
                       void* stream);
 
@@ -215,48 +218,18 @@ typedef struct cc_update {
     uint32_t reserved;
 } cc_update;
 
-/* Scratch bytes cc_apply_updates_dev needs for a pool of n_pages pages and up
- * to n_updates updates of at most max_len bytes each. */
-uint64_t cc_update_work_bytes(uint64_t n_pages, uint64_t n_updates, uint32_t max_len, uint32_t page_bytes);
-
-/* Client partial-write path (BASELINE config 3): apply n byte-range updates
- * (any alignment, may straddle pages) to the device pool, then recompute the
- * CRC of every page they touch, in place in d_page_crcs (untouched pages keep
- * their CRC).  Reference write path: WriteChunkRequest::OnApply ->
- * CSChunkFile::Write (op_request.cpp:429-481, chunkserver_chunkfile.cpp:287-427)
- * writes in raft-log order; the per-page CRC table is new.
- * d_updates is grouped into n_batches consecutive batches ending at
- * h_batch_ends[b] (host array; NULL = one batch); updates inside a batch must
- * not overlap, batches are applied in order -- so an ordered write log with
- * overlaps is expressed by splitting it into levels (the Python binding does).
- * One recompute pass covers all batches.  d_work: >= cc_update_work_bytes(...)
- * bytes of device scratch, reused across calls (generation-tagged). */
-int cc_apply_updates_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
-                         const cc_update* d_updates, uint64_t n_updates, const uint64_t* h_batch_ends,
-                         uint32_t n_batches, uint32_t max_len, uint32_t* d_page_crcs, void* d_work,
-                         uint64_t work_bytes, void* stream);
-
-/* Host-side planner for cc_apply_updates_dev: reorders an ORDERED write log
- * (h_in, write order, may overlap) into h_out grouped by level -- level(j) =
- * 1 + max level of the earlier writes j overlaps, 0 if none -- so that no two
- * writes of one level overlap and applying levels in order equals applying the
- * log in order (later writes win, as raft-log order does).  h_batch_ends[b] =
- * end index of level b in h_out; *n_batches = number of levels (<= max_batches,
- * else CC_EINVAL).  Radix sort by offset, a sweep for clusters of overlapping
- * writes, and a max segment tree inside each cluster: O(n log n). */
-int cc_plan_updates(const cc_update* h_in, uint64_t n, cc_update* h_out, uint64_t* h_batch_ends,
-                    uint32_t max_batches, uint32_t* n_batches);
-
-/* Client partial-write path with the ordering done on the device (the
- * drop-in for the write loop of WriteChunkRequest::OnApply -> CSChunkFile::Write,
- * op_request.cpp:429-481, chunkserver_chunkfile.cpp:287-427, which applies
- * writes in raft-log order).  d_log[0..n) is the ORDERED write log: entries may
- * overlap, have any alignment and straddle pages; later entries win.  Every
- * entry becomes one piece per page it touches, a stable device radix sort by
- * page keeps write order inside each page, and one wave per touched page
- * merges that page's pieces in registers, stores the changed dwords and writes
- * the page's new CRC to d_page_crcs (untouched pages keep theirs).  No host
- * planning, one sort + 2 kernels.  Contract per entry: 1 <= len <= max_len and
+/* Client partial-write path (BASELINE config 3), the drop-in for the write
+ * loop of WriteChunkRequest::OnApply -> CSChunkFile::Write (op_request.cpp:429-481,
+ * chunkserver_chunkfile.cpp:287-427, which applies writes in raft-log order);
+ * the per-page CRC table is new.  d_log[0..n) is the ORDERED write
+ * log: entries may overlap, have any alignment and straddle pages; later
+ * entries win.  Every entry becomes one piece per page it touches; the pieces
+ * are grouped by page in a device hash table (one 64-bit CAS per piece: no
+ * sort, no host planning), and one wave per touched page applies that page's
+ * pieces in log order in registers, stores the changed 256-byte rows and
+ * writes the page's new CRC to d_page_crcs (untouched pages keep theirs).
+ * Three launches (table clear, insert, pages); a log of <= 64 entries no longer
+ * than a page takes one.  Contract per entry: 1 <= len <= max_len and
  * dst + len <= pool_bytes -- an entry that breaks it is skipped whole (never
  * half-applied); d_src must not alias d_pool.  page_bytes = 256 * 2^k
  * (k = 0..5).  d_work: >= cc_apply_log_work_bytes(n, max_len, page_bytes) bytes

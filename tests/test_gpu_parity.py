@@ -671,16 +671,15 @@ def test_scan_host_stream(dev, oracle, pinned):
         assert fc[i] == oracle.crc32c(m.tobytes() + d.tobytes())
 
 
-@pytest.mark.parametrize("mode", ["log", "delta", "batched"])
+@pytest.mark.parametrize("mode", ["log", "delta"])
 @pytest.mark.parametrize("page_bytes,n_upd,overlap", [(4096, 3000, False), (4096, 2000, True), (512, 2500, True),
                                                       (256, 1500, True), (8192, 1000, True)])
 def test_partial_writes(dev, oracle, page_bytes, n_upd, overlap, mode):
-    """cc_apply_log_dev / cc_apply_log_delta_dev / cc_apply_updates_dev:
+    """cc_apply_log_dev / cc_apply_log_delta_dev:
     unaligned sub-page writes (1 B .. >1 page, straddling pages, overlapping in
     order) -> pool bytes == in-order host application and every page CRC ==
     oracle on the final bytes (touched pages recomputed or delta-updated,
     untouched ones kept)."""
-    batched = mode == "batched"
     from curve_amd import crc as C
     rng = np.random.default_rng(n_upd + overlap + page_bytes)
     pool_bytes = 8 << 20
@@ -694,13 +693,8 @@ def test_partial_writes(dev, oracle, page_bytes, n_upd, overlap, mode):
     dst = rng.integers(0, span, n_upd)
     src_data = rng.integers(0, 256, int(lens.sum()) + 8, dtype=np.uint8)
     src_off = np.concatenate([[0], np.cumsum(lens)[:-1]]) + rng.integers(0, 4, n_upd) * 0
-    if batched:
-        nb = C.apply_updates_batched(d_pool, crcs, to_dev(src_data, dev), dst, src_off, lens, page_bytes)
-    else:
-        nb = C.apply_updates(d_pool, crcs, to_dev(src_data, dev), dst, src_off, lens, page_bytes,
-                             delta=mode == "delta")
-    assert nb == 1 or batched
-    assert (nb > 1) == overlap or not overlap or not batched
+    nb = C.apply_updates(d_pool, crcs, to_dev(src_data, dev), dst, src_off, lens, page_bytes, delta=mode == "delta")
+    assert nb == 1
     want = host.copy()
     for i in range(n_upd):
         want[dst[i]:dst[i] + lens[i]] = src_data[src_off[i]:src_off[i] + lens[i]]
