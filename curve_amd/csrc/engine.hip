@@ -281,7 +281,8 @@ int staging_init(DevCtx* c) {
         if ((e = hipMalloc(&st.dev[i], per)) != hipSuccess) return map_err(e);
         if ((e = hipMalloc(&st.dcrc[i], per / 256 * 4)) != hipSuccess) return map_err(e);
         if ((e = hipHostMalloc(&st.hcrc[i], per / 256 * 4, hipHostMallocDefault)) != hipSuccess) return map_err(e);
-        if ((e = hipMalloc(&st.tiles[i], (kRangeTiles + 1) * sizeof(uint64_t))) != hipSuccess) return map_err(e);
+        if ((e = hipMalloc(&st.tiles[i], (kRangeTiles + kDynCtrWords64) * sizeof(uint64_t))) != hipSuccess)
+            return map_err(e);
         if ((e = hipStreamCreateWithFlags(&st.stream[i], hipStreamNonBlocking)) != hipSuccess) return map_err(e);
         if ((e = hipEventCreateWithFlags(&st.done[i], hipEventDisableTiming)) != hipSuccess) return map_err(e);
     }
@@ -605,7 +606,7 @@ int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, u
     // every wave an equal share of the batch's 4 KiB blocks; stream-ordered
     // scratch of this call for the tile counts (calls on different streams may overlap)
     uint64_t* tiles = nullptr;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&tiles), (kRangeTiles + 1) * sizeof(uint64_t), s);
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&tiles), (kRangeTiles + kDynCtrWords64) * sizeof(uint64_t), s);
     if (e != hipSuccess) return map_err(e);
     e = launch_range_flat(static_cast<const unsigned char*>(d_buf), rd, n, tiles, c->image, d_out, c->cus, s);
     const hipError_t f = hipFreeAsync(tiles, s);
@@ -995,7 +996,7 @@ uint64_t cc_verify_reads_work_bytes(uint64_t n_reads) {
     if (n_reads == 0 || n_reads >= (1ull << 31)) return 0;
     const size_t temp = scan_temp_bytes(n_reads);
     if (!temp) return 0;
-    return 2 * align256(n_reads * 8) + align256(temp) + 256;  // + the dynamic-tail counter
+    return 2 * align256(n_reads * 8) + align256(temp) + align256(kDynCtrBytes);  // + the dynamic-tail heads
 }
 
 int cc_verify_reads_dev(const void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const cc_range* d_reads,

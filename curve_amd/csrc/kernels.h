@@ -24,6 +24,7 @@ constexpr int kBlockThreads = 64 * kWavesPerBlock;
 constexpr uint32_t kDynHeads = CC_PAGE_DYN_HEADS;
 constexpr uint32_t kDynHeadStride = 16;  // 128 bytes between heads: one cache line each
 constexpr uint32_t kDynCtrBytes = kDynHeads * kDynHeadStride * 8;
+constexpr uint32_t kDynCtrWords64 = kDynHeads * kDynHeadStride;  // the heads as uint64 words
 
 // Host builder of the 160 KiB LDS image (engine.hip).
 void build_lds_image(uint32_t* image /* kLdsBytes/4 words */);
@@ -171,7 +172,7 @@ hipError_t launch_read_verify_small(const ReadVerifyLaunch& a, hipStream_t s);
 // count of each of kRangeTiles contiguous tiles of the batch (and zeroes
 // out[]); range_flat_kernel gives every wave an equal share of the blocks,
 // ranges cut by a share boundary XOR their segments into out[].
-// tile_blocks: kRangeTiles + 1 uint64 of stream-ordered scratch (the last: the
+// tile_blocks: kRangeTiles + kDynCtrWords64 uint64 of stream-ordered scratch (the last: the
 // dynamic-tail chunk counter).
 constexpr uint32_t kRangeTiles = 1024;
 hipError_t wave_trace_read(uint64_t* host);  // CC_WAVE_TRACE builds only: [4][8192]

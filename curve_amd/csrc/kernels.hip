@@ -287,6 +287,41 @@ __device__ __forceinline__ void chains(const uint32_t* tab, const uint32_t (&w)[
 // (blockIdx.x % 8: workgroups go round-robin over the XCDs -- placement is
 // speed only, never correctness) and, once that is drained, steals from the
 // next regions in turn.
+// Next chunk of a dynamic tail of n_chunks chunks, from kDynHeads counters
+// kDynHeadStride words apart (zeroed before the launch).  With one head: a
+// plain dequeue.  With 8: the chunks are cut into 8 contiguous regions, a wave
+// pulls from its own XCD's region first (blockIdx.x % 8 -- workgroups go
+// round-robin over the XCDs; placement is speed only, never correctness) and
+// steals from the next regions once that is drained.  `head` / `tried` are the
+// wave's (uniform) cursor, initialised by tail_cursor().  Returns n_chunks when
+// every region is drained.  Lane 0 does the atomics.
+template <uint32_t H = kDynHeads>
+__device__ __forceinline__ void tail_cursor(uint32_t& head, uint32_t& tried) {
+    head = blockIdx.x % H;
+    tried = 0;
+}
+template <uint32_t H = kDynHeads>
+__device__ __forceinline__ uint64_t tail_pull(unsigned long long* __restrict__ ctr, uint64_t n_chunks, uint32_t& head,
+                                              uint32_t& tried, uint32_t lane) {
+    static_assert(H >= 1 && H <= kDynHeads, "heads beyond the zeroed counters");
+    if constexpr (H == 1) {
+        unsigned long long c = 0;
+        if (lane == 0) c = atomicAdd(ctr, 1ull);
+        c = readlane64(c, 0);
+        return c < n_chunks ? c : n_chunks;
+    } else {
+        const uint64_t per = (n_chunks + H - 1) / H;
+        for (; tried < H; tried++, head = (head + 1) % H) {
+            unsigned long long c = 0;
+            if (lane == 0) c = atomicAdd(ctr + head * kDynHeadStride, 1ull);
+            c = readlane64(c, 0);
+            const uint64_t chunk = head * per + c;
+            if (c < per && chunk < n_chunks) return chunk;
+        }
+        return n_chunks;
+    }
+}
+
 struct ZeroRanges {
     uint32_t* p[2];
     uint64_t n[2];
@@ -323,7 +358,8 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
     W.wstride = ((uint64_t)gridDim.x * kWavesPerBlock) << tshift;
     W.wfirst = ((uint64_t)blockIdx.x * kWavesPerBlock + wave) << tshift;
     uint64_t lim = dyn_ctr ? (static_tiles << tshift < n_pages ? static_tiles << tshift : n_pages) : n_pages;
-    uint32_t dyn_head = blockIdx.x % kDynHeads, dyn_tried = 0;  // this XCD's tail region first
+    uint32_t dyn_head, dyn_tried;  // this XCD's tail region first
+    tail_cursor(dyn_head, dyn_tried);
 #pragma unroll 1
     for (;;) {
         if (W.wfirst < lim) {
@@ -365,27 +401,10 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
         if (!dyn_ctr) break;
         // next dynamic chunk: CC_PAGE_DYN_PAGES consecutive pages
         const uint64_t tail0 = static_tiles << tshift;
-        uint64_t p0 = n_pages;
-        if constexpr (kDynHeads == 1) {
-            unsigned long long c = 0;
-            if (lane == 0) c = atomicAdd(dyn_ctr, 1ull);
-            c = readlane64(c, 0);
-            p0 = tail0 + c * CC_PAGE_DYN_PAGES;
-        } else {
-            const uint64_t chunks = (n_pages - tail0 + CC_PAGE_DYN_PAGES - 1) / CC_PAGE_DYN_PAGES;
-            const uint64_t per = (chunks + kDynHeads - 1) / kDynHeads;
-            for (; dyn_tried < kDynHeads; dyn_tried++, dyn_head = (dyn_head + 1) % kDynHeads) {
-                unsigned long long c = 0;
-                if (lane == 0) c = atomicAdd(dyn_ctr + dyn_head * kDynHeadStride, 1ull);
-                c = readlane64(c, 0);
-                const uint64_t chunk = dyn_head * per + c;
-                if (c < per && chunk < chunks) {
-                    p0 = tail0 + chunk * CC_PAGE_DYN_PAGES;
-                    break;
-                }
-            }
-        }
-        if (p0 >= n_pages) break;
+        const uint64_t chunks = (n_pages - tail0 + CC_PAGE_DYN_PAGES - 1) / CC_PAGE_DYN_PAGES;
+        const uint64_t chunk = tail_pull(dyn_ctr, chunks, dyn_head, dyn_tried, lane);
+        if (chunk >= chunks) break;
+        const uint64_t p0 = tail0 + chunk * CC_PAGE_DYN_PAGES;
         W.wfirst = p0;
         W.wstride = 1ull << tshift;  // consecutive tiles: page(k) = p0 + k
         lim = p0 + CC_PAGE_DYN_PAGES < n_pages ? p0 + CC_PAGE_DYN_PAGES : n_pages;
@@ -614,8 +633,8 @@ __global__ __launch_bounds__(256) void range_tiles_kernel(const RangeDesc* __res
     __syncthreads();
     if (threadIdx.x == 0) {
         tile_blocks[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
-        if (blockIdx.x == 0) tile_blocks[kRangeTiles] = 0;  // the dynamic chunk counter
     }
+    if (blockIdx.x == 0 && threadIdx.x < kDynCtrWords64) tile_blocks[kRangeTiles + threadIdx.x] = 0;  // tail heads
 }
 
 __device__ __forceinline__ uint64_t wave_scan_incl(uint64_t v, uint32_t lane) {
@@ -640,6 +659,9 @@ constexpr int kFlatWaves = CC_FLAT_WAVES;
 #ifndef CC_RANGE_DYN_DIV
 #define CC_RANGE_DYN_DIV 32  // 1/32 of the blocks go to the dynamic tail (0: none; A/B: 1/8 and 1/16 lose to
                              // the one counter's atomics, 1/64 leaves tail)
+#endif
+#ifndef CC_RANGE_HEADS
+#define CC_RANGE_HEADS 1  // tail heads (A/B round 3: 8 per-XCD heads = one counter at 1/32)
 #endif
 #ifndef CC_RANGE_DYN_BLOCKS
 #define CC_RANGE_DYN_BLOCKS 16  // blocks per dynamic chunk (A/B: 8 slower, 16 = 32)
@@ -675,6 +697,8 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsig
     const uint64_t Bs = CC_RANGE_DYN_DIV ? B - B / CC_RANGE_DYN_DIV : B;  // statically dealt blocks
     const uint64_t n_dyn = (B - Bs + CC_RANGE_DYN_BLOCKS - 1) / CC_RANGE_DYN_BLOCKS;
     unsigned long long* dyn_ctr = reinterpret_cast<unsigned long long*>(tile_blocks + kRangeTiles);
+    uint32_t dyn_head, dyn_tried;
+    tail_cursor<CC_RANGE_HEADS>(dyn_head, dyn_tried);
 
     // work items: static pieces item < rounds, then dynamic chunks until the counter runs out
 #pragma unroll 1
@@ -686,9 +710,7 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsig
             b1 = Bs * (c + 1) / RW;
             if (b0 >= b1) continue;
         } else {
-            uint64_t c = 0;
-            if (lane == 0) c = atomicAdd(dyn_ctr, 1ull);
-            c = readlane64(c, 0);
+            const uint64_t c = tail_pull<CC_RANGE_HEADS>(dyn_ctr, n_dyn, dyn_head, dyn_tried, lane);
             if (c >= n_dyn) break;
             b0 = Bs + c * CC_RANGE_DYN_BLOCKS;
             b1 = b0 + CC_RANGE_DYN_BLOCKS < B ? b0 + CC_RANGE_DYN_BLOCKS : B;
@@ -1632,7 +1654,7 @@ __global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_small_kernel(Log
 // Pages each read touches (a read past the pool touches none and is marked).
 __global__ void read_counts_kernel(ReadVerifyLaunch a) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) *a.dyn_ctr = 0;  // read_verify_kernel's dynamic-tail counter
+    if (i < kDynCtrWords64) a.dyn_ctr[i] = 0;  // read_verify_kernel's dynamic-tail heads
     if (i >= a.n_reads) return;
     const RangeDesc r = a.reads[i];
     uint64_t c = 0;
@@ -1663,6 +1685,9 @@ __global__ void read_counts_kernel(ReadVerifyLaunch a) {
 constexpr int kRvWaves = CC_RV_WAVES;
 #ifndef CC_RV_DYN_DIV
 #define CC_RV_DYN_DIV 16  // 1/16 of the slots form the dynamic tail (A/B: 2-3 % over none; 1/8, 1/32 less)
+#endif
+#ifndef CC_RV_HEADS
+#define CC_RV_HEADS 1  // tail heads (A/B round 3: 8 per-XCD heads = one counter at 1/16)
 #endif
 #ifndef CC_RV_DYN_SLOTS
 #define CC_RV_DYN_SLOTS 32  // slots (pages) per dynamic chunk (64: -1 %, 128: -5 %, 256: -18 % -- too coarse)
@@ -1717,6 +1742,8 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
     // static shares of the first Ts slots, then dynamic chunks of CC_RV_DYN_SLOTS
     // slots (the page kernel's tail: the XCDs run at different rates)
     const uint64_t Ts = T - T / CC_RV_DYN_DIV;
+    uint32_t dyn_head, dyn_tried;
+    tail_cursor<CC_RV_HEADS>(dyn_head, dyn_tried);
     uint64_t lo_slot = w < W ? Ts * w / W : Ts, hi_slot = w < W ? Ts * (w + 1) / W : Ts;  // waves past W: tail only
 #pragma unroll 1
     for (;;) {
@@ -1776,11 +1803,10 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
                 if (!step(Cq, sC, oC, k + 2, B, gB, sB, oB)) break;
             }
         }
-        unsigned long long c = 0;
-        if (lane == 0) c = atomicAdd(a.dyn_ctr, 1ull);
-        c = readlane64(c, 0);
+        const uint64_t n_dyn = (T - Ts + CC_RV_DYN_SLOTS - 1) / CC_RV_DYN_SLOTS;
+        const uint64_t c = tail_pull<CC_RV_HEADS>(a.dyn_ctr, n_dyn, dyn_head, dyn_tried, lane);
+        if (c >= n_dyn) break;
         lo_slot = Ts + c * CC_RV_DYN_SLOTS;
-        if (lo_slot >= T) break;
         hi_slot = lo_slot + CC_RV_DYN_SLOTS < T ? lo_slot + CC_RV_DYN_SLOTS : T;
     }
 }
