@@ -138,9 +138,10 @@ static int comm_release(cc_comm* comm, bool abort) {
             rc = map_nccl(ncclCommAbort(comm->nc));
         } else {
             // finalize flushes this rank's outstanding work (non-blocking: settle
-            // it), then destroy frees the resources
+            // it), then destroy frees the resources; a finalize that fails or
+            // does not settle (a peer gone) is aborted instead of destroyed
             rc = settle_call(comm->nc, ncclCommFinalize(comm->nc));
-            const int rd = map_nccl(ncclCommDestroy(comm->nc));
+            const int rd = rc ? map_nccl(ncclCommAbort(comm->nc)) : map_nccl(ncclCommDestroy(comm->nc));
             if (!rc) rc = rd;
         }
     }
