@@ -753,16 +753,23 @@ def main():
     load_only_gbs = pool.data.numel() // 4096 * ALG_BYTES_PER_PAGE / (float(np.mean(lo_ms)) * 1e-3) / 1e9
 
     n_pages = n * chunk // pb
+    # the timed launch: with a metapage the size of a page and a batch big enough
+    # for the page kernel's dynamic tail, cc_pool_scan_dev hashes the n metapages
+    # inside the data launch (engine.hip pool_page_launches / plan_tail: >= 8
+    # 64-page tiles per wave of a one-workgroup-per-CU grid), so they are its bytes too
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    fused_meta = meta_sz == pb and pb == 4096 and n_pages // 64 >= cus * 8 * 8
+    launch_pages = n_pages + (n if fused_meta else 0)
     per_step_bytes = n * chunk * world
     value = per_step_bytes * args.steps / GiB / el
-    achieved = n_pages * ALG_BYTES_PER_PAGE / (kern_ms * 1e-3) / 1e9
+    achieved = launch_pages * ALG_BYTES_PER_PAGE / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src = None, None
     if rank == 0 and world == 1 and not args.no_pmc and pb == 4096:
         traffic, traffic_src = live_traffic(n * chunk / GiB)
     if traffic is None:  # the committed PMC summary of the same geometry
         why = traffic_src
         traffic, traffic_src = load_traffic(args)
-        if traffic and abs(traffic / (n_pages * ALG_BYTES_PER_PAGE) - 1.0) > 0.05:
+        if traffic and abs(traffic / (launch_pages * ALG_BYTES_PER_PAGE) - 1.0) > 0.05:
             traffic, traffic_src = None, f"{traffic_src} profiles a different pool size"  # not this workload
         if why:
             traffic_src = f"{traffic_src} (live measurement unavailable: {why})"
@@ -794,7 +801,9 @@ def main():
                      "kernel_ms_each": [round(x, 4) for x in kern_each],
                      "kernel_ms_median": round(float(np.median(kern_each)), 4),
                      "kernel_spread_pct": round((max(kern_each) - min(kern_each)) / min(kern_each) * 100, 2),
-                     "alg_bytes_per_launch": n_pages * ALG_BYTES_PER_PAGE,
+                     "alg_bytes_per_launch": launch_pages * ALG_BYTES_PER_PAGE,
+                     "pages_per_launch": launch_pages,
+                     "metapages_in_launch": n if fused_meta else 0,
                      "traffic_source": traffic_src,
                      "read_probe_GBps": round(probe_gbs, 1),
                      "frac_of_read_probe": round(achieved / probe_gbs, 4),
@@ -806,7 +815,7 @@ def main():
         out["digest_exchange"] = {"path": comm_note, "matches_torch_distributed": digest_check}
         # aggregate roofline over the node: every rank's algorithmic bytes over the
         # slowest rank's page-kernel time, against N x the per-GPU peak
-        agg = world * n_pages * ALG_BYTES_PER_PAGE / (max(rank_kern) * 1e-3) / 1e9
+        agg = world * launch_pages * ALG_BYTES_PER_PAGE / (max(rank_kern) * 1e-3) / 1e9
         out["roofline"].update({"aggregate_achieved": round(agg, 1), "aggregate_peak": HBM_PEAK_GBS * world,
                                 "aggregate_frac": round(agg / (HBM_PEAK_GBS * world), 4),
                                 "rank_kernel_ms": [round(x, 4) for x in rank_kern],

@@ -100,6 +100,22 @@ struct DevCtx {
     std::mutex tab_mu;  // epilogue-table inserts
     std::atomic<uint64_t> epi_key[kEpiSlots];  // key + 1 (0 = empty); published after epi_ptr
     std::atomic<void*> epi_ptr[kEpiSlots];
+    // the page kernel's self-resetting tail counters, one block per stream
+    // (kernels.hip tail_reset): zeroed on the stream when created, left zero by
+    // every launch that uses it, so a call needs no allocation or memset
+    std::mutex tail_mu;
+    std::vector<std::pair<hipStream_t, unsigned long long*>> tails;
+    // the write log's page tables, one per stream (apply_log); log_mu is held
+    // over a call's whole enqueue (insert + pages) so calls sharing a stream
+    // cannot interleave on its table
+    struct LogTable {
+        hipStream_t s;
+        unsigned char* p;
+        uint64_t entries;
+        bool dirty;
+    };
+    std::mutex log_mu;
+    std::vector<LogTable> log_tabs;
     DevCtx() {
         for (int i = 0; i < kEpiSlots; i++) {
             epi_key[i].store(0);
@@ -163,6 +179,9 @@ DevCtx::~DevCtx() {
         if (image) hipFree(image);
         for (int i = 0; i < kEpiSlots; i++)
             if (void* p = epi_ptr[i].load()) hipFree(p);
+        for (auto& t : tails) hipFree(t.second);
+        for (auto& t : log_tabs) (void)hipFreeAsync(t.p, nullptr);
+        (void)hipDeviceSynchronize();
     }
     if (cur >= 0) (void)hipSetDevice(cur);
 }
@@ -238,23 +257,52 @@ void geometry_for(const DevCtx* c, uint64_t n_pages, PageLaunch* a) {
 #ifndef CC_PAGE_DYN_DIV
 #define CC_PAGE_DYN_DIV 16  // 1/16 of a large launch's tiles form the dynamic tail (0: static only; A/B 2.464 ms vs 2.474-2.478 at 1/8, 2.474 at 1/12, 2.51 at 1/24 and 1/32)
 #endif
-// Page kernel launch with the dynamic tail (kernels.hip, page_crc_kernel) when
-// the batch is large: stream-ordered, zeroed chunk counters (kDynHeads) per call --
-// `zeroed_ctr` if the caller has one (zeroed on the stream before this launch:
-// cc_pool_scan_dev has the metapage launch clear it), else allocated + memset.
-hipError_t launch_page_tail(const DevCtx* c, PageLaunch& a, bool verify, hipStream_t s,
-                            unsigned long long* zeroed_ctr = nullptr, bool load_probe = false) {
+// Tile schedule of a page launch: geometry, and (true) a dynamic tail of the
+// last 1/CC_PAGE_DYN_DIV of the tiles when the batch is large and the page size
+// has a fixed-M instantiation.
+bool plan_tail(const DevCtx* c, PageLaunch& a) {
     geometry_for(c, a.n_pages, &a);
     const uint32_t m = a.words_per_lane;
     const uint64_t tiles = (a.n_pages + (1ull << a.tile_shift) - 1) >> a.tile_shift;
     const uint64_t waves = (uint64_t)a.blocks * kWavesPerBlock;
+    if (!CC_PAGE_DYN_DIV || m > 32 || (m & (m - 1)) || tiles < waves * 8) return false;
+    a.static_tiles = tiles - tiles / CC_PAGE_DYN_DIV;
+    return true;
+}
+
+constexpr size_t kMaxTailBlocks = 256;  // streams with a block of their own
+
+// The stream's self-resetting tail-counter block, created (and zeroed on the
+// stream) on first use; null when kMaxTailBlocks streams already hold one.
+// Keyed by the stream handle: a destroyed stream's handle is only reused for a
+// new stream after hipStreamDestroy, which the caller orders after that
+// stream's work as for any of its buffers.
+unsigned long long* tail_block(DevCtx* c, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(c->tail_mu);
+    for (auto& t : c->tails)
+        if (t.first == s) return t.second;
+    if (c->tails.size() >= kMaxTailBlocks) return nullptr;
+    void* p = nullptr;
+    if (hipMalloc(&p, kTailBlockBytes) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(p, 0, kTailBlockBytes, s) != hipSuccess) {
+        (void)hipFree(p);
+        return nullptr;
+    }
+    c->tails.push_back({s, static_cast<unsigned long long*>(p)});
+    return static_cast<unsigned long long*>(p);
+}
+
+// Page kernel launch (kernels.hip, page_crc_kernel) with its dynamic tail when
+// plan_tail() gives one: the tail's counters are the stream's self-resetting
+// block, or (no block free) a counter allocated + zeroed for this launch.
+hipError_t launch_page_tail(DevCtx* c, PageLaunch& a, bool verify, hipStream_t s, bool load_probe = false) {
     auto launch = [&]() {
         return load_probe ? launch_page_load_probe(a, s) : verify ? launch_page_verify(a, s) : launch_page_crc(a, s);
     };
-    if (!CC_PAGE_DYN_DIV || m > 32 || (m & (m - 1)) || tiles < waves * 8) return launch();
-    a.static_tiles = tiles - tiles / CC_PAGE_DYN_DIV;
-    if (zeroed_ctr) {
-        a.dyn_ctr = zeroed_ctr;
+    if (!plan_tail(c, a)) return launch();
+    if (unsigned long long* blk = tail_block(c, s)) {
+        a.dyn_ctr = blk;
+        a.done_ctr = blk + kDynCtrWords64;
         return launch();
     }
     unsigned long long* ctr = nullptr;
@@ -430,7 +478,7 @@ int cc_page_load_probe_dev(const void* d_pages, uint64_t n_pages, uint32_t* d_ou
     a.words_per_lane = 4096 / kWaveBytes;
     a.image = c->image;
     a.out = d_out;
-    return map_err(launch_page_tail(c.get(), a, false, static_cast<hipStream_t>(stream), nullptr, true));
+    return map_err(launch_page_tail(c.get(), a, false, static_cast<hipStream_t>(stream), true));
 }
 
 #if CC_WAVE_TRACE
@@ -504,36 +552,42 @@ int pool_page_launches(const void* d_data, uint64_t n_data_pages, uint32_t page_
     CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
-    unsigned long long* ctr = nullptr;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ctr), kDynCtrBytes, s);
-    if (e != hipSuccess) return map_err(e);
-    PageLaunch m = {};
-    m.pages = static_cast<const uint32_t*>(d_meta);
-    m.n_pages = n_meta;
-    m.words_per_lane = meta_bytes / kWaveBytes;
-    m.image = c->image;
-    m.kconst = kconst_for(meta_bytes);
-    m.out = d_meta_crcs;
-    m.zero[0] = reinterpret_cast<uint32_t*>(ctr);
-    m.zero_words[0] = kDynCtrBytes / 4;
-    m.zero[1] = d_digest;
-    m.zero_words[1] = d_digest ? digest_words : 0;
-    geometry_for(c.get(), n_meta, &m);  // static walk (a tail would need a counter of its own)
-    e = launch_page_meta(m, s);
-    if (e == hipSuccess && ev_begin) e = hipEventRecord(static_cast<hipEvent_t>(ev_begin), s);
-    if (e == hipSuccess) {
-        PageLaunch a = {};
-        a.pages = static_cast<const uint32_t*>(d_data);
-        a.n_pages = n_data_pages;
-        a.words_per_lane = page_bytes / kWaveBytes;
-        a.image = c->image;
-        a.kconst = kconst_for(page_bytes);
-        a.out = d_page_crcs;
-        e = launch_page_tail(c.get(), a, false, s, ctr);
+    PageLaunch a = {};
+    a.pages = static_cast<const uint32_t*>(d_data);
+    a.n_pages = n_data_pages;
+    a.words_per_lane = page_bytes / kWaveBytes;
+    a.image = c->image;
+    a.kconst = kconst_for(page_bytes);
+    a.out = d_page_crcs;
+    hipError_t e = hipSuccess;
+    if (meta_bytes == page_bytes && n_meta && plan_tail(c.get(), a)) {
+        // ONE launch: the metapages are chunks of the data launch's dynamic tail
+        // (same page size, same kconst); block 0 clears the digest
+        a.meta_pages = static_cast<const uint32_t*>(d_meta);
+        a.n_meta = n_meta;
+        a.meta_out = d_meta_crcs;
+        a.zero[0] = d_digest;
+        a.zero_words[0] = d_digest ? digest_words : 0;
+        if (ev_begin) e = hipEventRecord(static_cast<hipEvent_t>(ev_begin), s);
+        if (e == hipSuccess) e = launch_page_tail(c.get(), a, false, s);
+    } else {
+        // a metapage launch of its own (static walk; clears the digest), then the data
+        PageLaunch m = {};
+        m.pages = static_cast<const uint32_t*>(d_meta);
+        m.n_pages = n_meta;
+        m.words_per_lane = meta_bytes / kWaveBytes;
+        m.image = c->image;
+        m.kconst = kconst_for(meta_bytes);
+        m.out = d_meta_crcs;
+        m.zero[0] = d_digest;
+        m.zero_words[0] = d_digest ? digest_words : 0;
+        geometry_for(c.get(), n_meta, &m);
+        e = launch_page_meta(m, s);
+        if (e == hipSuccess && ev_begin) e = hipEventRecord(static_cast<hipEvent_t>(ev_begin), s);
+        if (e == hipSuccess) e = launch_page_tail(c.get(), a, false, s);
     }
     if (e == hipSuccess && ev_end) e = hipEventRecord(static_cast<hipEvent_t>(ev_end), s);
-    const hipError_t f = hipFreeAsync(ctr, s);
-    return map_err(e != hipSuccess ? e : f);
+    return map_err(e);
 }
 }  // namespace cc
 }  // extern "C++"
@@ -896,12 +950,14 @@ inline uint32_t log_slots(uint32_t max_len, uint32_t page_bytes) { return (max_l
 }  // namespace
 
 namespace {
-// Work layout of the write log: counter (head_count) | page table | next links |
-// head slots.  Only the counter and the table are
-// cleared per call (one memset).
+// The caller's work buffer of the write log: next links | head slots (neither
+// needs clearing).  The page table lives in the engine (LogTable): header of
+// 256 bytes (head count at 0, the page kernel's block-arrival count at 64), then
+// the open-addressing table.
 struct LogWork {
-    uint64_t n_pieces, table_entries, table_off, next_off, heads_off, bytes;
+    uint64_t n_pieces, table_entries, next_off, heads_off, bytes;
 };
+constexpr uint64_t kLogTableHeader = 256;
 bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork* w) {
     if (!log_page_ok(page_bytes) || max_len == 0 || n_updates == 0) return false;
     w->n_pieces = n_updates * log_slots(max_len, page_bytes);
@@ -913,11 +969,43 @@ bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork
     while (te < CC_LOG_TABLE_FACTOR * w->n_pieces) te <<= 1;  // load <= 1 / factor
     if (te > (1ull << 32)) return false;  // slots and the mask are 32-bit
     w->table_entries = te;
-    w->table_off = 256;
-    w->next_off = w->table_off + te * 8;
-    w->heads_off = w->next_off + align256(w->n_pieces * 4);
+    w->next_off = 0;
+    w->heads_off = align256(w->n_pieces * 4);
     w->bytes = w->heads_off + align256(w->n_pieces * 4);
     return true;
+}
+
+// The stream's write-log table with >= `entries` slots, zero when the call's
+// launches run (caller holds c->log_mu).  Created or grown (stream-ordered
+// free of the old one) with a clear on the stream; a table a failed call left
+// dirty is cleared.  nullptr when kMaxTailBlocks streams already hold one.
+DevCtx::LogTable* log_table(DevCtx* c, hipStream_t s, uint64_t entries, hipError_t* err) {
+    *err = hipSuccess;
+    DevCtx::LogTable* t = nullptr;
+    for (auto& x : c->log_tabs)
+        if (x.s == s) t = &x;
+    if (t && t->entries < entries) {
+        if ((*err = hipFreeAsync(t->p, s)) != hipSuccess) return nullptr;
+        t->p = nullptr;
+        t->entries = 0;
+    }
+    if (!t) {
+        if (c->log_tabs.size() >= kMaxTailBlocks) return nullptr;
+        c->log_tabs.push_back({s, nullptr, 0, false});
+        t = &c->log_tabs.back();
+    }
+    if (!t->p) {
+        void* p = nullptr;
+        if ((*err = hipMallocAsync(&p, kLogTableHeader + entries * 8, s)) != hipSuccess) return nullptr;
+        t->p = static_cast<unsigned char*>(p);
+        t->entries = entries;
+        t->dirty = true;
+    }
+    if (t->dirty) {
+        if ((*err = hipMemsetAsync(t->p, 0, kLogTableHeader + t->entries * 8, s)) != hipSuccess) return nullptr;
+        t->dirty = false;
+    }
+    return t;
 }
 }  // namespace
 
@@ -953,9 +1041,6 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
     a.max_len = max_len;
     a.slots = log_slots(max_len, page_bytes);
     a.n_pieces = lw.n_pieces;
-    a.head_count = reinterpret_cast<uint32_t*>(w);
-    a.table = reinterpret_cast<uint64_t*>(w + lw.table_off);
-    a.table_mask = (uint32_t)(lw.table_entries - 1);
     a.next = reinterpret_cast<uint32_t*>(w + lw.next_off);
     a.heads = reinterpret_cast<uint32_t*>(w + lw.heads_off);
     a.image = c->image;
@@ -972,9 +1057,34 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
     if (n_updates <= (uint64_t)CC_LOG_SMALL && n_updates <= 64 && a.slots <= 2) return map_err(launch_log_small(a, s));
     // (memset + insert + pages as ONE cooperative launch with two grid barriers
     // measured 0.221 vs 0.162 ms a batch: not kept)
-    if ((e = hipMemsetAsync(w, 0, lw.next_off, s)) != hipSuccess) return map_err(e);  // counter + table
-    if ((e = launch_log_insert(a, s)) != hipSuccess) return map_err(e);
-    return map_err(launch_log_pages(a, s));
+    std::lock_guard<std::mutex> lk(c->log_mu);
+    DevCtx::LogTable* t = log_table(c.get(), s, lw.table_entries, &e);
+    if (e != hipSuccess) return map_err(e);
+    unsigned char* tmp = nullptr;  // no table free for this stream: a cleared one for this call
+    if (t) {
+        a.head_count = reinterpret_cast<uint32_t*>(t->p);
+        a.done = reinterpret_cast<uint32_t*>(t->p + 64);
+        a.table = reinterpret_cast<uint64_t*>(t->p + kLogTableHeader);
+        a.table_mask = (uint32_t)(t->entries - 1);
+    } else {
+        const uint64_t bytes = kLogTableHeader + lw.table_entries * 8;
+        if ((e = hipMallocAsync(reinterpret_cast<void**>(&tmp), bytes, s)) != hipSuccess) return map_err(e);
+        if ((e = hipMemsetAsync(tmp, 0, bytes, s)) != hipSuccess) {
+            (void)hipFreeAsync(tmp, s);
+            return map_err(e);
+        }
+        a.head_count = reinterpret_cast<uint32_t*>(tmp);
+        a.table = reinterpret_cast<uint64_t*>(tmp + kLogTableHeader);
+        a.table_mask = (uint32_t)(lw.table_entries - 1);
+    }
+    e = launch_log_insert(a, s);
+    if (e == hipSuccess) e = launch_log_pages(a, s);
+    if (t && e != hipSuccess) t->dirty = true;  // the insert may have run: clear before the next use
+    if (tmp) {
+        const hipError_t f = hipFreeAsync(tmp, s);
+        if (e == hipSuccess) e = f;
+    }
+    return map_err(e);
 }
 }  // namespace
 

@@ -25,6 +25,10 @@ constexpr uint32_t kDynHeads = CC_PAGE_DYN_HEADS;
 constexpr uint32_t kDynHeadStride = 16;  // 128 bytes between heads: one cache line each
 constexpr uint32_t kDynCtrBytes = kDynHeads * kDynHeadStride * 8;
 constexpr uint32_t kDynCtrWords64 = kDynHeads * kDynHeadStride;  // the heads as uint64 words
+// A self-resetting counter block (page kernel): the heads, then the launch's
+// wave-arrival counter on a line of its own.
+constexpr uint32_t kTailBlockWords64 = kDynCtrWords64 + kDynHeadStride;
+constexpr uint32_t kTailBlockBytes = kTailBlockWords64 * 8;
 
 // Host builder of the 160 KiB LDS image (engine.hip).
 void build_lds_image(uint32_t* image /* kLdsBytes/4 words */);
@@ -53,6 +57,15 @@ struct PageLaunch {
     // [static_tiles, all) are handed out through this zeroed counter
     unsigned long long* dyn_ctr;  // kDynHeads counters, kDynHeadStride words apart (zeroed before the launch)
     uint64_t static_tiles;
+    // self-reset (non-null = dyn_ctr is a kTailBlockWords64 block, this is its
+    // arrival word): the last wave out of the launch zeroes the heads and this
+    // word, so the block is zero again for the stream's next launch
+    unsigned long long* done_ctr;
+    // fused metapages (cc_pool_scan_dev when metapage size == page size): n_meta
+    // more pages of the same size, appended to the dynamic tail as chunks of their own
+    const uint32_t* meta_pages;
+    uint64_t n_meta;
+    uint32_t* meta_out;
     // block 0 zeroes these word ranges before its walk (stream-ordered for the
     // kernels after it: the next launch's tail counter, a digest to XOR into)
     uint32_t* zero[2];
@@ -125,6 +138,10 @@ struct LogLaunch {
     uint32_t* next;             // [n_pieces] next piece of the same page (kNoPiece = end)
     uint32_t* heads;            // [n_pieces] table slots of the touched pages (unordered)
     uint32_t* head_count;       // number of them
+    // non-null: the table and head_count are the engine's per-stream table, to be
+    // left zero -- the page kernel clears each slot it consumes, and the last
+    // block out (counted here) zeroes head_count and this word
+    uint32_t* done;
     const void* image;
     uint32_t kconst;
     uint32_t* page_crcs;        // out; in delta mode also in (the CRCs before the batch)

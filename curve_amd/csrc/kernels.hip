@@ -331,11 +331,34 @@ struct ZeroRanges {
             for (uint64_t i = threadIdx.x; i < n[k]; i += blockDim.x) p[k][i] = 0u;
     }
 };
+// The dynamic tail's extras (PageLaunch::meta_pages / done_ctr): a second page
+// array appended to the tail as chunks of its own, and the arrival word of a
+// self-resetting counter block.
+struct TailExtra {
+    const uint32_t* pages;
+    uint64_t n;
+    uint32_t* out;
+    unsigned long long* done;
+};
+// Self-reset: every wave arrives once, after its last pull; the last to arrive
+// zeroes the heads and the arrival word (device-scope atomics, like the pulls),
+// so the block is zero for the next launch on the stream.  A wave's pulls have
+// returned before it arrives (its exit depends on their values), so no pull can
+// follow the reset -- and no fence is needed: a device-scope fence here would
+// write back the XCD's L2 once per wave (A/B: +1.7 % on the page kernel).
+__device__ __forceinline__ void tail_reset(unsigned long long* ctr, unsigned long long* done, uint32_t lane) {
+    if (lane != 0) return;
+    const unsigned long long waves = (unsigned long long)gridDim.x * kWavesPerBlock;
+    if (atomicAdd(done, 1ull) != waves - 1) return;
+    for (uint32_t h = 0; h < kDynHeads; h++) atomicExch(ctr + h * kDynHeadStride, 0ull);
+    atomicExch(done, 0ull);
+}
+
 template <int M, int MODE>
 __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
     const uint32_t* __restrict__ pages, uint64_t n_pages, const uint4* __restrict__ image,
     uint32_t kconst, uint32_t* __restrict__ out, const uint32_t* __restrict__ expected, VerifySink vs,
-    uint32_t tshift, unsigned long long* __restrict__ dyn_ctr, uint64_t static_tiles, ZeroRanges zr) {
+    uint32_t tshift, unsigned long long* __restrict__ dyn_ctr, uint64_t static_tiles, ZeroRanges zr, TailExtra ex) {
     __shared__ uint32_t tab[kLdsBytes / 4];
     if (blockIdx.x == 0) zr.clear();
     fill_lds(tab, image);
@@ -349,6 +372,7 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
     const uint32_t* base = pages + lane;
+    uint32_t* dst = out;
     constexpr int D = CC_PREFETCH;
     constexpr int P = (M <= 16) ? CC_PAIR : 1;  // register budget: P*(D+1)*M data VGPRs
     // item 0: the strided static walk over tiles [0, static_tiles); then dynamic chunks
@@ -391,7 +415,7 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
                             const uint32_t slot = (uint32_t)(kq & W.tmask);
                             acc = lane == slot ? crc : acc;
                             if (slot == W.tmask || pn >= lim)
-                                flush_tile<MODE>(acc, pc - slot, slot + 1u, lane, out, expected, vs);
+                                flush_tile<MODE>(acc, pc - slot, slot + 1u, lane, dst, expected, vs);
                         }
                     }
                 }
@@ -399,16 +423,31 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
             }
         }
         if (!dyn_ctr) break;
-        // next dynamic chunk: CC_PAGE_DYN_PAGES consecutive pages
+        // next dynamic chunk: CC_PAGE_DYN_PAGES consecutive pages of the fused
+        // metapages (the first chunk indices: pulled early, so the tail's last
+        // chunks stay data chunks that even out as before), then of the data
         const uint64_t tail0 = static_tiles << tshift;
-        const uint64_t chunks = (n_pages - tail0 + CC_PAGE_DYN_PAGES - 1) / CC_PAGE_DYN_PAGES;
+        const uint64_t mchunks = (ex.n + CC_PAGE_DYN_PAGES - 1) / CC_PAGE_DYN_PAGES;
+        const uint64_t chunks = mchunks + (n_pages - tail0 + CC_PAGE_DYN_PAGES - 1) / CC_PAGE_DYN_PAGES;
         const uint64_t chunk = tail_pull(dyn_ctr, chunks, dyn_head, dyn_tried, lane);
         if (chunk >= chunks) break;
-        const uint64_t p0 = tail0 + chunk * CC_PAGE_DYN_PAGES;
+        uint64_t p0, end;
+        if (chunk >= mchunks) {
+            base = pages + lane;
+            dst = out;
+            p0 = tail0 + (chunk - mchunks) * CC_PAGE_DYN_PAGES;
+            end = n_pages;
+        } else {
+            base = ex.pages + lane;
+            dst = ex.out;
+            p0 = chunk * CC_PAGE_DYN_PAGES;
+            end = ex.n;
+        }
         W.wfirst = p0;
         W.wstride = 1ull << tshift;  // consecutive tiles: page(k) = p0 + k
-        lim = p0 + CC_PAGE_DYN_PAGES < n_pages ? p0 + CC_PAGE_DYN_PAGES : n_pages;
+        lim = p0 + CC_PAGE_DYN_PAGES < end ? p0 + CC_PAGE_DYN_PAGES : end;
     }
+    if (dyn_ctr && ex.done) tail_reset(dyn_ctr, ex.done, lane);
 #if CC_WAVE_TRACE
     wave_trace((uint64_t)blockIdx.x * kWavesPerBlock + wave, t_start);
 #endif
@@ -1387,6 +1426,7 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         const bool hv = ih < H;
         const uint32_t hslot = a.heads[hv ? ih : base];
         const unsigned long long ent = reinterpret_cast<const unsigned long long*>(a.table)[hslot];
+        if (a.done && hv) a.table[hslot] = 0ull;  // the slot is this lane's alone (one head per page)
         const uint32_t key = (uint32_t)(ent >> 32) - 1u;  // the page
         const uint32_t pfirst = (uint32_t)ent - 1u;       // one of its pieces (the list head)
         const uint32_t nxt = a.next[pfirst];
@@ -1566,6 +1606,15 @@ template <int M, bool Delta>
 __global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(LogLaunch a) {
     __shared__ uint32_t tab[kLdsBytes / 4];
     log_pages_body<M, Delta>(a, tab);
+    if (a.done) {
+        // every thread of the block has read head_count (the early exit is per
+        // block); the last block out leaves the counters zero for the next call
+        __syncthreads();
+        if (threadIdx.x == 0 && atomicAdd(a.done, 1u) == gridDim.x - 1) {
+            atomicExch(a.head_count, 0u);
+            atomicExch(a.done, 0u);
+        }
+    }
 }
 
 // A small log (<= 64 writes of <= one page each: at most 2 pieces a write) in
@@ -1911,15 +1960,23 @@ __global__ void xor_fold_kernel(const uint32_t* __restrict__ gathered, uint32_t 
     out[i] = v;
 }
 
+// Fused metapages only ride a dynamic tail (the static walk knows one array).
+TailExtra tail_extra(const PageLaunch& a) {
+    const bool meta = a.dyn_ctr && a.meta_pages && a.n_meta;
+    return {meta ? a.meta_pages : nullptr, meta ? a.n_meta : 0, meta ? a.meta_out : nullptr,
+            a.dyn_ctr ? a.done_ctr : nullptr};
+}
+
 template <int MODE>
 hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
     const dim3 grid(a.blocks), block(kBlockThreads);
     const uint4* img = static_cast<const uint4*>(a.image);
     const ZeroRanges zr = {{a.zero[0], a.zero[1]}, {a.zero[0] ? a.zero_words[0] : 0, a.zero[1] ? a.zero_words[1] : 0}};
+    const TailExtra ex = tail_extra(a);
 #define CC_CASE(MM)                                                                                     \
     case MM:                                                                                            \
         hipLaunchKernelGGL((page_crc_kernel<MM, MODE>), grid, block, 0, s, a.pages, a.n_pages, img,    \
-                           a.kconst, a.out, a.expected, a.sink, a.tile_shift, a.dyn_ctr, a.static_tiles, zr); \
+                           a.kconst, a.out, a.expected, a.sink, a.tile_shift, a.dyn_ctr, a.static_tiles, zr, ex); \
         break;
     switch (a.words_per_lane) {
         CC_CASE(1)
@@ -1948,7 +2005,7 @@ hipError_t launch_page_meta(const PageLaunch& a, hipStream_t s) {
     const ZeroRanges zr = {{a.zero[0], a.zero[1]}, {a.zero[0] ? a.zero_words[0] : 0, a.zero[1] ? a.zero_words[1] : 0}};
     hipLaunchKernelGGL((page_crc_kernel<16, 3>), dim3(a.blocks), dim3(kBlockThreads), 0, s, a.pages, a.n_pages,
                        static_cast<const uint4*>(a.image), a.kconst, a.out, a.expected, a.sink, a.tile_shift,
-                       a.dyn_ctr, a.static_tiles, zr);
+                       a.dyn_ctr, a.static_tiles, zr, tail_extra(a));
     return hipGetLastError();
 }
 
@@ -1957,7 +2014,7 @@ hipError_t launch_page_load_probe(const PageLaunch& a, hipStream_t s) {
     const ZeroRanges zr = {{nullptr, nullptr}, {0, 0}};
     hipLaunchKernelGGL((page_crc_kernel<16, 2>), dim3(a.blocks), dim3(kBlockThreads), 0, s, a.pages, a.n_pages,
                        static_cast<const uint4*>(a.image), a.kconst, a.out, a.expected, a.sink, a.tile_shift,
-                       a.dyn_ctr, a.static_tiles, zr);
+                       a.dyn_ctr, a.static_tiles, zr, tail_extra(a));
     return hipGetLastError();
 }
 

@@ -228,12 +228,16 @@ typedef struct cc_update {
  * sort, no host planning), and one wave per touched page applies that page's
  * pieces in log order in registers, stores the changed 256-byte rows and
  * writes the page's new CRC to d_page_crcs (untouched pages keep theirs).
- * Three launches (table clear, insert, pages); a log of <= 64 entries no longer
- * than a page takes one.  Contract per entry: 1 <= len <= max_len and
+ * Two launches (insert, pages); a log of <= 64 entries no longer than a page
+ * takes one.  The hash table is the engine's, one per stream, created (and
+ * grown) on the stream on first use and left clear by every call, so no call
+ * clears it; calls sharing a stream are serialised by the engine while they
+ * enqueue.  Contract per entry: 1 <= len <= max_len and
  * dst + len <= pool_bytes -- an entry that breaks it is skipped whole (never
  * half-applied); d_src must not alias d_pool.  page_bytes = 256 * 2^k
  * (k = 0..5).  d_work: >= cc_apply_log_work_bytes(n, max_len, page_bytes) bytes
- * (0 = unsupported sizes). */
+ * (the pieces' list links and the touched-page list; no clearing needed;
+ * 0 = unsupported sizes: a table of more than 2^32 slots). */
 uint64_t cc_apply_log_work_bytes(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes);
 int cc_apply_log_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void* d_src,
                      const cc_update* d_log, uint64_t n_updates, uint32_t max_len, uint32_t* d_page_crcs,

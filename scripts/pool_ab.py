@@ -62,12 +62,13 @@ for p in libs:
     call(p)
     torch.cuda.synchronize()
     results[p] = (pool.slice_crcs.clone(), pool.file_crcs.clone(), digests[p].clone())
-for _ in range(20):
+# ~3 s of sustained load first: the clock settles only after ~2.5 s of it (bench.py warm_clock)
+for _ in range(1200):
     call(sys.argv[1])
 torch.cuda.synchronize()
 step, kern = {p: [] for p in libs}, {p: [] for p in libs}
 order = list(libs)
-for r in range(16):
+for r in range(32):
     for p in (order if r % 2 == 0 else order[::-1]):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)

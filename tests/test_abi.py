@@ -89,13 +89,15 @@ def test_argument_checks_need_no_gpu():
 
 
 def test_write_log_work_sizing_limits():
-    """cc_apply_log_work_bytes (host arithmetic only): the hash table holds >= 4
-    entries per piece in a power of two, and a log whose table would need more
-    than 2^32 slots (32-bit slot indices) is refused with 0, not truncated."""
+    """cc_apply_log_work_bytes (host arithmetic only): the caller's buffer holds
+    a list link and a touched-page slot per piece (the hash table is the
+    engine's, >= 4 entries per piece in a power of two), and a log whose table
+    would need more than 2^32 slots (32-bit slot indices) is refused with 0, not
+    truncated."""
     from curve_amd import _lib
     L = _lib.lib()
     small = L.cc_apply_log_work_bytes(65536, 4096, 4096)  # 2 pieces per write
-    assert small >= 256 + 4 * 131072 * 8 + 2 * 131072 * 4
+    assert small >= 2 * 131072 * 4
     assert L.cc_apply_log_work_bytes(1 << 29, 4096, 4096) > 0          # 2^30 pieces -> 2^32 slots
     assert L.cc_apply_log_work_bytes((1 << 29) + 1, 4096, 4096) == 0   # would need 2^33 slots
     assert L.cc_apply_log_work_bytes(0, 4096, 4096) == 0

@@ -405,6 +405,59 @@ def test_full_size_config1_scan_step(dev, oracle):
         assert int(pc[p]) == oracle.crc32c(hd.reshape(-1)[p * 4096:(p + 1) * 4096])
 
 
+@pytest.mark.parametrize("meta_sz", [4096, 8192])
+def test_pool_scan_fused_metapages_and_tail_reuse(dev, oracle, meta_sz):
+    """cc_pool_scan_dev large enough for the page kernel's dynamic tail (300
+    chunks = 1,228,800 pages).  A 4 KiB metapage (the page size) rides the data
+    launch's tail as chunks of its own -- 300 metapages = 4 full 64-page chunks
+    and a partial one; an 8 KiB metapage gets a launch of its own.  Every page,
+    metapage and slice CRC and every digest equals the oracle's, and stays so
+    over back-to-back scans on one stream and on two streams in turn: the
+    stream's tail counters reset themselves at the end of each launch
+    (kernels.hip tail_reset), so no call zeroes them."""
+    from curve_amd import crc as C
+    from curve_amd.pool import copyset_layout, pool_scan
+    from curve_amd.scan import DevicePool, chunk_file_name
+    n, chunk, G = 300, C.CHUNK_SIZE, 7
+    data = torch.empty((n, chunk), dtype=torch.uint8, device=dev).random_(0, 256)
+    meta = torch.empty((n, meta_sz), dtype=torch.uint8, device=dev).random_(0, 256)
+    meta[:, 0] = 2
+    pool = DevicePool(data, meta, list(range(n)), page_bytes=4096)
+    lay = copyset_layout(list(range(n)), [i % G for i in range(n)], [chunk + meta_sz] * n)
+    after_mult = C.xpow8(torch.tensor(lay.after_bytes, dtype=torch.int64, device=dev))
+    group = torch.tensor(lay.group, dtype=torch.int32, device=dev)
+    hd, hm = data.cpu().numpy(), meta.cpu().numpy()
+    want_pc = oracle.page_crcs(hd.reshape(-1), 4096, threads=16)
+    want_mc = [oracle.crc32c(hm[i].tobytes()) for i in range(n)]
+    want_dig = {}
+    for g in range(G):
+        mem = sorted((chunk_file_name(i), i) for i in range(n) if i % G == g)
+        crc = 0
+        for _, i in mem:
+            crc = oracle.crc32c(hd[i], oracle.crc32c(hm[i], crc))
+        want_dig[lay.group[mem[0][1]]] = crc
+    rng = np.random.default_rng(0xF5)
+    sample = rng.choice(n, 8, replace=False)
+    want_sl = {int(i): [c for (_, _, c) in oracle.scan_slices(hm[i].tobytes(), hd[i].tobytes(), C.SCAN_SIZE)[1:]]
+               for i in sample}
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    for rep, st in enumerate([0, 0, 1, 0, 1, 1]):
+        s = streams[st]
+        s.wait_stream(torch.cuda.current_stream())
+        pool.page_crcs.fill_(0)
+        pool.meta_crcs.fill_(0)
+        digest = torch.full((lay.n_groups,), rep, dtype=torch.int32, device=dev)
+        with torch.cuda.stream(s):
+            pool_scan(pool, after_mult, group, digest, stream=s)
+        s.synchronize()
+        assert (u32(pool.page_crcs) == want_pc).all(), rep
+        assert u32(pool.meta_crcs[:n]).tolist() == want_mc, rep
+        dig = u32(digest)
+        assert all(int(dig[k]) == v for k, v in want_dig.items()), rep
+        sl = u32(pool.slice_crcs).reshape(n, 4)
+        assert all([int(x) for x in sl[i]] == want_sl[i] for i in want_sl), rep
+
+
 def test_write_log_full_size_config3(dev, oracle):
     """BASELINE config 3 at full size: a 16 GiB pool (1024 chunks), 65,536 random
     512 B-4 KiB writes in one log (unaligned, straddling, some overlapping).
@@ -627,6 +680,34 @@ def test_streams_and_multithread_callers(dev, oracle):
     [t.join() for t in ts]
     for i in range(4):
         assert (results[i] == oracle.page_crcs(bufs[i], 4096)).all()
+
+
+def test_dynamic_tail_concurrent_streams(dev, oracle):
+    """Four Python threads, each on a stream of its own, run tail-sized page
+    launches (1M + 77 pages of 256 B) back to back at the same time: each stream
+    has its own self-resetting tail counters, so every run of every thread
+    equals the oracle."""
+    import threading
+    from curve_amd import crc as C
+    n_pages, pb = (1 << 20) + 77, 256
+    bufs = [torch.empty(n_pages * pb, dtype=torch.uint8, device=dev).random_(0, 256) for _ in range(4)]
+    torch.cuda.synchronize()
+    want = [oracle.page_crcs(b.cpu().numpy(), pb, threads=16) for b in bufs]
+    bad = []
+
+    def work(i):
+        s = torch.cuda.Stream(device=dev)
+        with torch.cuda.stream(s):
+            outs = [C.page_crc(bufs[i], pb, stream=s) for _ in range(4)]
+            s.synchronize()
+        for k, o in enumerate(outs):
+            if not (u32(o) == want[i]).all():
+                bad.append((i, k))
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert bad == []
 
 
 @pytest.mark.parametrize("n_pages", [8192 + 5, 20000, 65536 + 3, 262144 + 77])
