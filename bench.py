@@ -319,7 +319,8 @@ def warm_clock(fn, ms=1000.0):
 def partial_write_leg(pool, args):
     """BASELINE config 3: client partial writes into the resident 1024-chunk pool.
     Per batch a write LOG of U random updates (size uniform in [512, 4096] B,
-    offset uniform and unaligned; ~12 % straddle two pages; overlapping entries
+    offset uniform and unaligned; ~54 % straddle two pages -- ~101,000 touched
+    pages a batch, ~1 % of them with more than one piece; overlapping entries
     apply in log order) and its data, both resident in HBM as the pool is: one
     cc_apply_log_dev call groups the pieces by page on the device (a hash
     table, no sort), applies them and rehashes every touched page in place.  Timed with HIP events on the

@@ -115,14 +115,21 @@ struct UpdateDesc {
 // A page with more than 64 pieces is finished by its wave replaying the log.
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
 #ifndef CC_LOG_WAVES
-#define CC_LOG_WAVES 12  // waves per CU of the write-log page kernel (A/B: 12 beats 8 by ~6 %; 16 forces <= 128 VGPRs and spills in delta mode)
+#define CC_LOG_WAVES 12  // waves per CU of the write-log page kernel at 8 KiB pages (A/B at 4 KiB, round 1: 12 beats 8 by ~6 %)
 #endif
 constexpr int kLogWaves = CC_LOG_WAVES;
 #ifndef CC_LOG_WAVES_FULL
-#define CC_LOG_WAVES_FULL 16  // full mode, pages <= 4 KiB: 127 VGPRs since the row-select merge, so 16 fit (A/B ~1.5 %)
+#define CC_LOG_WAVES_FULL 16  // full mode, pages <= 4 KiB: 103 VGPRs since the row offsets went into the offset field
+#endif
+#ifndef CC_LOG_WAVES_DELTA
+#define CC_LOG_WAVES_DELTA 16  // delta mode, pages <= 4 KiB: 120 VGPRs at 16 waves (was 12 waves: 129 would spill)
 #endif
 // waves per workgroup of log_pages_kernel<M, Delta>
-constexpr int log_waves(int m, bool delta) { return (!delta && m <= 16) ? CC_LOG_WAVES_FULL : CC_LOG_WAVES; }
+constexpr int log_waves(int m, bool delta) {
+    return m > 16 ? CC_LOG_WAVES : (delta ? CC_LOG_WAVES_DELTA : CC_LOG_WAVES_FULL);
+}
+// waves per workgroup of log_small_kernel<M, Delta>
+constexpr int log_small_waves(int m, bool delta) { return (!delta && m <= 16) ? CC_LOG_WAVES_FULL : CC_LOG_WAVES; }
 struct LogLaunch {
     unsigned char* pool;
     uint64_t pool_bytes;

@@ -495,11 +495,28 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
 #ifndef CC_LOG_ROWSEL
 #define CC_LOG_ROWSEL 1  // full mode: one-piece pages through the per-row source/page select (merge_edges)
 #endif
+#ifndef CC_LOG_MULTI_FAST
+#define CC_LOG_MULTI_FAST 1  // pages with several pieces: first two links + descriptors in one round trip
+#endif
 #ifndef CC_LOG_STORE_AUX
 #define CC_LOG_STORE_AUX 2  // cache policy bits of the write-log row stores (2 = nontemporal: -20 us a batch)
 #endif
 constexpr uint32_t kBufOOB = 0x80000000u;   // offset past num_records: load 0 / store dropped
 constexpr uint32_t kBufFlags = 0x00020000u;  // buffer resource dword 3 for gfx9-family (CDNA)
+// A per-row buffer offset is `sel + 256 j` with sel = (lane's dword wanted ?
+// its offset : kBufOOB).  Left alone, the compiler folds the add into both arms
+// of the select and keeps 2 x M loop-invariant row constants in VGPRs (32 at
+// 4 KiB pages); with sel opaque the 256 j goes into the instruction's 12-bit
+// offset field (kBufOOB + 256 j is still past num_records).
+#ifndef CC_ROW_OPAQUE
+#define CC_ROW_OPAQUE 1
+#endif
+__device__ __forceinline__ uint32_t row_sel(uint32_t v) {
+#if CC_ROW_OPAQUE
+    asm("" : "+v"(v));
+#endif
+    return v;
+}
 
 
 // ---------------------------------------------------------------------------
@@ -1225,7 +1242,7 @@ __device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint
     for (int j = 0; j < M; j++) {
         const bool full = pl.o + 256u * j < pl.l3;
         r.S[j] = __builtin_amdgcn_raw_buffer_load_b32(
-            rw, (full && CC_LOG_ABLATE != 2 && CC_LOG_ABLATE != 5 ? l4 : kBufOOB) + 256u * j, 0, CC_LOG_SRC_AUX);
+            rw, row_sel(full && CC_LOG_ABLATE != 2 && CC_LOG_ABLATE != 5 ? l4 : kBufOOB) + 256u * j, 0, CC_LOG_SRC_AUX);
     }
     uint32_t e[2];
     piece_edges(p, e);
@@ -1310,7 +1327,7 @@ __device__ __forceinline__ void load_rows_sel(uint32_t (&w)[M], const unsigned c
                                                                          kBufFlags);
 #pragma unroll
     for (int j = 0; j < M; j++)
-        w[j] = __builtin_amdgcn_raw_buffer_load_b32(((cov >> j) & 1u) ? rs : rp, 4u * lane + 256u * j, 0, 2);
+        w[j] = __builtin_amdgcn_raw_buffer_load_b32(((cov >> j) & 1u) ? rs : rp, row_sel(4u * lane) + 256u * j, 0, 2);
 }
 
 template <int M>
@@ -1398,7 +1415,7 @@ __device__ __forceinline__ void load_rows(uint32_t (&w)[M], const unsigned char*
                                                                          kBufFlags);
 #pragma unroll
     for (int j = 0; j < M; j++)
-        w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, (((rows >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j, 0, 2);
+        w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, row_sel(((rows >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j, 0, 2);
 }
 
 template <int M, bool Delta>
@@ -1431,8 +1448,16 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         const uint32_t pfirst = (uint32_t)ent - 1u;       // one of its pieces (the list head)
         const uint32_t nxt = a.next[pfirst];
         const UpdateDesc d = a.upd[pfirst / a.slots];
+#if CC_LOG_MULTI_FAST
+        // the head piece's geometry in its page, packed: rlo | rhi << 16 and the
+        // source pointer (3 VGPRs instead of the 5 of its descriptor)
+        const Piece hp0 = piece_in_page((uint64_t)key * pb, pb, d.dst, d.src, d.len, a.src);
+        const uint32_t hrr = hp0.rlo | hp0.rhi << 16;
+        const uint64_t hsp = (uint64_t)(uintptr_t)hp0.sp;
+#else
         const uint64_t ddst = d.dst, dsrc = d.src;
         const uint32_t dlen = d.len;
+#endif
         const bool single = nxt == kNoPiece;  // the page's only piece
         const uint64_t singles = __ballot(single);
         const uint32_t cnt = (uint32_t)__popcll(__ballot(hv));  // valid lanes are 0 .. cnt-1
@@ -1452,8 +1477,13 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
             }
         };
         auto head_piece = [&](uint32_t k, uint32_t pg) {
+#if CC_LOG_MULTI_FAST
+            const uint32_t rr = __builtin_amdgcn_readlane(hrr, k);
+            return Piece{rr & 0xFFFFu, rr >> 16, reinterpret_cast<const unsigned char*>(readlane64(hsp, k))};
+#else
             return piece_in_page((uint64_t)pg * pb, pb, readlane64(ddst, k), readlane64(dsrc, k),
                                  __builtin_amdgcn_readlane(dlen, k), a.src);
+#endif
         };
         // one page step: merge + store + rehash page `pg` from (X, SX, px) while
         // the loads of the next page go into (Y, SY); false after the last page
@@ -1511,12 +1541,29 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
                     merge_piece<M>(X, dirty, SX, px, lane);
                 }
             } else {  // several pieces: collect the list, apply in log (update index) order
+#if CC_LOG_MULTI_FAST
+                // the list's first two pieces came with the metadata; their
+                // descriptors (lanes 0, 1) and the third link load together, so a
+                // two-piece page (nearly every page with several) pays one round
+                // trip for its list instead of four
+                const uint32_t p0 = __builtin_amdgcn_readlane(pfirst, hh), p1 = __builtin_amdgcn_readlane(nxt, hh);
+                uint32_t cnt = 2, mine = lane == 0 ? p0 : (lane == 1 ? p1 : kNoPiece);
+                UpdateDesc dl = a.upd[(lane < 2 ? mine : p0) / a.slots];
+                uint32_t q = a.next[p1];
+                while (q != kNoPiece && cnt < 64u) {
+                    mine = lane == cnt ? q : mine;
+                    cnt++;
+                    q = a.next[q];
+                }
+                if (cnt > 2 && q == kNoPiece) dl = a.upd[(lane < cnt ? mine : p0) / a.slots];  // rare
+#else
                 uint32_t q = __builtin_amdgcn_readlane(pfirst, hh), cnt = 0, mine = kNoPiece;
                 while (q != kNoPiece && cnt < 64u) {
                     mine = lane == cnt ? q : mine;
                     cnt++;
                     q = a.next[q];
                 }
+#endif
                 if (q != kNoPiece) {  // > 64 pieces (a log hammering this page: rare)
                     // its own wave replays the whole log for this page, 64 records per round
                     // (a ballot of the records touching it), in log order
@@ -1539,10 +1586,29 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
                     const uint32_t idx = lane < cnt ? mine / a.slots : 0xFFFFFFFFu;
                     uint32_t rank = lane < cnt ? 0u : 0xFFFFu;
                     for (uint32_t j = 0; j < cnt; j++) rank += (uint32_t)__builtin_amdgcn_readlane(idx, j) < idx;
+#if CC_LOG_MULTI_FAST
+                    if (kRowSel && cnt == 2) {  // both pieces' source bytes in flight together
+                        const uint32_t l0 = (uint32_t)__builtin_ctzll(__ballot(rank == 0)), l1 = l0 ^ 1u;
+                        const Piece q0 = piece_in_page(pbase, pb, readlane64(dl.dst, l0), readlane64(dl.src, l0),
+                                                       __builtin_amdgcn_readlane(dl.len, l0), a.src);
+                        const Piece q1 = piece_in_page(pbase, pb, readlane64(dl.dst, l1), readlane64(dl.src, l1),
+                                                       __builtin_amdgcn_readlane(dl.len, l1), a.src);
+                        PieceSrc<M> T0, T1;
+                        fetch_piece<M>(T0, q0, lane);
+                        fetch_piece<M>(T1, q1, lane);
+                        merge_piece<M>(X, dirty, T0, q0, lane);
+                        merge_piece<M>(X, dirty, T1, q1, lane);
+                    } else
+#endif
                     for (uint32_t r = 0; r < cnt; r++) {
                         const uint32_t l = (uint32_t)__builtin_ctzll(__ballot(rank == r));
+#if CC_LOG_MULTI_FAST
+                        const Piece pq = piece_in_page(pbase, pb, readlane64(dl.dst, l), readlane64(dl.src, l),
+                                                       __builtin_amdgcn_readlane(dl.len, l), a.src);
+#else
                         const UpdateDesc dq = a.upd[__builtin_amdgcn_readlane(idx, l)];
                         const Piece pq = piece_in_page(pbase, pb, dq.dst, dq.src, dq.len, a.src);
+#endif
                         if constexpr (kRowSel) {
                             PieceSrc<M> T;
                             fetch_piece<M>(T, pq, lane);
@@ -1559,12 +1625,11 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
                     __builtin_amdgcn_make_buffer_rsrc(a.pool + pbase, 0, 256u * M, kBufFlags);
 #pragma unroll
                 for (int j = 0; j < M; j++)
-                    __builtin_amdgcn_raw_buffer_store_b32(X[j], rp,
-                                                          (((dirty >> j) & 1u) && CC_LOG_ABLATE != 1 && CC_LOG_ABLATE != 5
-                                                               ? 4u * lane
-                                                               : kBufOOB) +
-                                                              256u * j,
-                                                          0, CC_LOG_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b32(
+                        X[j], rp,
+                        row_sel(((dirty >> j) & 1u) && CC_LOG_ABLATE != 1 && CC_LOG_ABLATE != 5 ? 4u * lane : kBufOOB) +
+                            256u * j,
+                        0, CC_LOG_STORE_AUX);
             }
             uint32_t crc;
             if constexpr (Delta) {
@@ -1626,8 +1691,8 @@ __global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(Log
 // lane order) through the generic piece merge, stores the changed rows and
 // rehashes the page.  Blocks without a page exit before filling LDS.
 template <int M, bool Delta>
-__global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_small_kernel(LogLaunch a) {
-    constexpr int WV = log_waves(M, Delta);
+__global__ __launch_bounds__(64 * log_small_waves(M, Delta)) void log_small_kernel(LogLaunch a) {
+    constexpr int WV = log_small_waves(M, Delta);
     __shared__ uint32_t tab[kLdsBytes / 4];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1684,7 +1749,7 @@ __global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_small_kernel(Log
         const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(a.pool + pbase, 0, 256u * M, kBufFlags);
 #pragma unroll
         for (int j = 0; j < M; j++)
-            __builtin_amdgcn_raw_buffer_store_b32(X[j], rp, (((dirty >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(X[j], rp, row_sel(((dirty >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j, 0, 0);
         uint32_t crc;
         if constexpr (Delta) {
 #pragma unroll
@@ -2126,10 +2191,10 @@ hipError_t launch_log_small(const LogLaunch& a, hipStream_t s) {
 #define CC_SMCASE(MM)                                                                                         \
     case MM:                                                                                                  \
         if (a.delta)                                                                                          \
-            hipLaunchKernelGGL((log_small_kernel<MM, true>), dim3(a.blocks), dim3(64 * log_waves(MM, true)), 0, s, \
+            hipLaunchKernelGGL((log_small_kernel<MM, true>), dim3(a.blocks), dim3(64 * log_small_waves(MM, true)), 0, s, \
                                a);                                                                            \
         else                                                                                                  \
-            hipLaunchKernelGGL((log_small_kernel<MM, false>), dim3(a.blocks), dim3(64 * log_waves(MM, false)), 0, \
+            hipLaunchKernelGGL((log_small_kernel<MM, false>), dim3(a.blocks), dim3(64 * log_small_waves(MM, false)), 0, \
                                s, a);                                                                         \
         break;
     switch (a.page_bytes / kWaveBytes) {
