@@ -495,9 +495,6 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
 #ifndef CC_LOG_ROWSEL
 #define CC_LOG_ROWSEL 1  // full mode: one-piece pages through the per-row source/page select (merge_edges)
 #endif
-#ifndef CC_LOG_MULTI_FAST
-#define CC_LOG_MULTI_FAST 1  // pages with several pieces: first two links + descriptors in one round trip
-#endif
 #ifndef CC_LOG_STORE_AUX
 #define CC_LOG_STORE_AUX 2  // cache policy bits of the write-log row stores (2 = nontemporal: -20 us a batch)
 #endif
@@ -1447,18 +1444,15 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         const uint32_t key = (uint32_t)(ent >> 32) - 1u;  // the page
         const uint32_t pfirst = (uint32_t)ent - 1u;       // one of its pieces (the list head)
         const uint32_t nxt = a.next[pfirst];
-        const UpdateDesc d = a.upd[pfirst / a.slots];
-#if CC_LOG_MULTI_FAST
+        const uint32_t u0 = pfirst / a.slots;  // the head piece's update
+        const UpdateDesc d = a.upd[u0];
         // the head piece's geometry in its page, packed: rlo | rhi << 16 and the
         // source pointer (3 VGPRs instead of the 5 of its descriptor)
         const Piece hp0 = piece_in_page((uint64_t)key * pb, pb, d.dst, d.src, d.len, a.src);
         const uint32_t hrr = hp0.rlo | hp0.rhi << 16;
         const uint64_t hsp = (uint64_t)(uintptr_t)hp0.sp;
-#else
-        const uint64_t ddst = d.dst, dsrc = d.src;
-        const uint32_t dlen = d.len;
-#endif
         const bool single = nxt == kNoPiece;  // the page's only piece
+        const uint32_t u1 = single ? 0u : nxt / a.slots;  // several pieces: the second one's update
         const uint64_t singles = __ballot(single);
         const uint32_t cnt = (uint32_t)__popcll(__ballot(hv));  // valid lanes are 0 .. cnt-1
         // two pages in flight: k (being merged + hashed) and k+1.  (A third
@@ -1476,14 +1470,9 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
                 fetch_piece<M>(r, p, lane);
             }
         };
-        auto head_piece = [&](uint32_t k, uint32_t pg) {
-#if CC_LOG_MULTI_FAST
+        auto head_piece = [&](uint32_t k) {
             const uint32_t rr = __builtin_amdgcn_readlane(hrr, k);
             return Piece{rr & 0xFFFFu, rr >> 16, reinterpret_cast<const unsigned char*>(readlane64(hsp, k))};
-#else
-            return piece_in_page((uint64_t)pg * pb, pb, readlane64(ddst, k), readlane64(dsrc, k),
-                                 __builtin_amdgcn_readlane(dlen, k), a.src);
-#endif
         };
         // one page step: merge + store + rehash page `pg` from (X, SX, px) while
         // the loads of the next page go into (Y, SY); false after the last page
@@ -1524,7 +1513,7 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
             // and the vmcnt waits stay exact)
             const uint32_t h1 = more ? hh + 1 : hh;
             pgy = __builtin_amdgcn_readlane(key, h1);
-            py = head_piece(h1, pgy);
+            py = head_piece(h1);
             load_next(Y, py, pgy, h1, ocy);
             fetch(SY, py);
             const uint64_t pbase = (uint64_t)pg * pb;
@@ -1541,29 +1530,26 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
                     merge_piece<M>(X, dirty, SX, px, lane);
                 }
             } else {  // several pieces: collect the list, apply in log (update index) order
-#if CC_LOG_MULTI_FAST
                 // the list's first two pieces came with the metadata; their
-                // descriptors (lanes 0, 1) and the third link load together, so a
-                // two-piece page (nearly every page with several) pays one round
-                // trip for its list instead of four
-                const uint32_t p0 = __builtin_amdgcn_readlane(pfirst, hh), p1 = __builtin_amdgcn_readlane(nxt, hh);
-                uint32_t cnt = 2, mine = lane == 0 ? p0 : (lane == 1 ? p1 : kNoPiece);
-                UpdateDesc dl = a.upd[(lane < 2 ? mine : p0) / a.slots];
-                uint32_t q = a.next[p1];
+                // descriptors (lanes 0, 1) and the link after the second load
+                // together, so a two-piece page (nearly every page with several)
+                // pays one round trip for its list instead of four.  (Loading these
+                // with the previous step's edge loads instead measured equal.)
+                const uint32_t u0h = __builtin_amdgcn_readlane(u0, hh), u1h = __builtin_amdgcn_readlane(u1, hh);
+                uint32_t cnt = 2, mu = lane == 0 ? u0h : (lane == 1 ? u1h : 0xFFFFFFFFu);  // update of lane's piece
+                const UpdateDesc dq = a.upd[lane < 2 ? mu : u0h];
+                uint32_t q = a.next[__builtin_amdgcn_readlane(nxt, hh)];
+                uint64_t dd = dq.dst, ds = dq.src;
+                uint32_t dn = dq.len;
                 while (q != kNoPiece && cnt < 64u) {
-                    mine = lane == cnt ? q : mine;
+                    mu = lane == cnt ? q / a.slots : mu;
                     cnt++;
                     q = a.next[q];
                 }
-                if (cnt > 2 && q == kNoPiece) dl = a.upd[(lane < cnt ? mine : p0) / a.slots];  // rare
-#else
-                uint32_t q = __builtin_amdgcn_readlane(pfirst, hh), cnt = 0, mine = kNoPiece;
-                while (q != kNoPiece && cnt < 64u) {
-                    mine = lane == cnt ? q : mine;
-                    cnt++;
-                    q = a.next[q];
+                if (cnt > 2 && q == kNoPiece) {  // rare: the other descriptors
+                    const UpdateDesc dq = a.upd[lane < cnt ? mu : u0h];
+                    dd = dq.dst, ds = dq.src, dn = dq.len;
                 }
-#endif
                 if (q != kNoPiece) {  // > 64 pieces (a log hammering this page: rare)
                     // its own wave replays the whole log for this page, 64 records per round
                     // (a ballot of the records touching it), in log order
@@ -1583,32 +1569,23 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
                         }
                     }
                 } else {
-                    const uint32_t idx = lane < cnt ? mine / a.slots : 0xFFFFFFFFu;
-                    uint32_t rank = lane < cnt ? 0u : 0xFFFFu;
-                    for (uint32_t j = 0; j < cnt; j++) rank += (uint32_t)__builtin_amdgcn_readlane(idx, j) < idx;
-#if CC_LOG_MULTI_FAST
+                    uint32_t rank = lane < cnt ? 0u : 0xFFFFu;  // lanes < cnt: distinct updates
+                    for (uint32_t j = 0; j < cnt; j++) rank += (uint32_t)__builtin_amdgcn_readlane(mu, j) < mu;
+                    auto lane_piece = [&](uint32_t l) {
+                        return piece_in_page(pbase, pb, readlane64(dd, l), readlane64(ds, l),
+                                             __builtin_amdgcn_readlane(dn, l), a.src);
+                    };
                     if (kRowSel && cnt == 2) {  // both pieces' source bytes in flight together
                         const uint32_t l0 = (uint32_t)__builtin_ctzll(__ballot(rank == 0)), l1 = l0 ^ 1u;
-                        const Piece q0 = piece_in_page(pbase, pb, readlane64(dl.dst, l0), readlane64(dl.src, l0),
-                                                       __builtin_amdgcn_readlane(dl.len, l0), a.src);
-                        const Piece q1 = piece_in_page(pbase, pb, readlane64(dl.dst, l1), readlane64(dl.src, l1),
-                                                       __builtin_amdgcn_readlane(dl.len, l1), a.src);
+                        const Piece q0 = lane_piece(l0), q1 = lane_piece(l1);
                         PieceSrc<M> T0, T1;
                         fetch_piece<M>(T0, q0, lane);
                         fetch_piece<M>(T1, q1, lane);
                         merge_piece<M>(X, dirty, T0, q0, lane);
                         merge_piece<M>(X, dirty, T1, q1, lane);
                     } else
-#endif
                     for (uint32_t r = 0; r < cnt; r++) {
-                        const uint32_t l = (uint32_t)__builtin_ctzll(__ballot(rank == r));
-#if CC_LOG_MULTI_FAST
-                        const Piece pq = piece_in_page(pbase, pb, readlane64(dl.dst, l), readlane64(dl.src, l),
-                                                       __builtin_amdgcn_readlane(dl.len, l), a.src);
-#else
-                        const UpdateDesc dq = a.upd[__builtin_amdgcn_readlane(idx, l)];
-                        const Piece pq = piece_in_page(pbase, pb, dq.dst, dq.src, dq.len, a.src);
-#endif
+                        const Piece pq = lane_piece((uint32_t)__builtin_ctzll(__ballot(rank == r)));
                         if constexpr (kRowSel) {
                             PieceSrc<M> T;
                             fetch_piece<M>(T, pq, lane);
@@ -1657,7 +1634,7 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         // k+1's loads land in the other
         uint32_t pgA = __builtin_amdgcn_readlane(key, 0), pgB = pgA;
         uint32_t ocA = 0, ocB = 0;
-        Piece pA = head_piece(0, pgA), pB = pA;
+        Piece pA = head_piece(0), pB = pA;
         load_next(A, pA, pgA, 0, ocA);
         fetch(S0, pA);
         for (uint32_t h = 0;; h += 2) {
