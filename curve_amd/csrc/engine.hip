@@ -484,6 +484,9 @@ int cc_page_load_probe_dev(const void* d_pages, uint64_t n_pages, uint32_t* d_ou
 #if CC_WAVE_TRACE
 int cc_debug_wave_trace(uint64_t* host) { return map_err(wave_trace_read(host)); }
 #endif
+#if CC_LOG_TRACE
+int cc_debug_log_trace(uint64_t* host) { return map_err(log_trace_read(host)); }
+#endif
 
 int cc_device_count(void) {
     int n = 0;

@@ -200,6 +200,7 @@ hipError_t launch_read_verify_small(const ReadVerifyLaunch& a, hipStream_t s);
 // dynamic-tail chunk counter).
 constexpr uint32_t kRangeTiles = 1024;
 hipError_t wave_trace_read(uint64_t* host);  // CC_WAVE_TRACE builds only: [4][8192]
+hipError_t log_trace_read(uint64_t* host);   // CC_LOG_TRACE builds only: [6][4096]
 hipError_t launch_range_flat(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, uint64_t* tile_blocks,
                              const void* image, uint32_t* out, int blocks, hipStream_t s);
 // x^(-8t) mod P for t = 0..kXinvEntries-1 (undoing the zero pad after a range in its last 4 KiB block)

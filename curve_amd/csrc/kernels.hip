@@ -49,6 +49,14 @@ constexpr uint32_t kPolyDev = 0x82F63B78u;
 #ifndef CC_WAVE_TRACE
 #define CC_WAVE_TRACE 0  // diagnostic builds: per-wave start/end wall clock of the page and range kernels
 #endif
+#ifndef CC_LOG_TRACE
+#define CC_LOG_TRACE 0  // diagnostic builds: per-wave phase clocks of the write-log page kernel
+#endif
+#if CC_LOG_TRACE
+// wave w: start, LDS filled, first metadata batch in registers, end,
+// pages | several-piece pages << 16 | hw id << 32, clock after its 12th page
+__device__ uint64_t g_ltrace[6][4096];
+#endif
 #if CC_WAVE_TRACE
 __device__ uint64_t g_rtrace[4][8192];  // start, end, block, cu
 __device__ __forceinline__ void wave_trace(uint64_t w, uint64_t t_start) {
@@ -494,6 +502,21 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
 #endif
 #ifndef CC_LOG_ROWSEL
 #define CC_LOG_ROWSEL 1  // full mode: one-piece pages through the per-row source/page select (merge_edges)
+#endif
+#ifndef CC_LOG_SKEW
+#define CC_LOG_SKEW 1  // write-log page kernel: heads cut among a workgroup's waves by SIMD age (weights below)
+#endif
+#ifndef CC_LOG_SKEW_W0
+#define CC_LOG_SKEW_W0 33  // A/B (profiles/write_log_skew_ab_r03.txt): 33/27/22/18 = 32/28/22/18 =
+#endif                     // 34/26/22/18 < 30/26/23/21 < 28/26/24/22 < 36/28/21/15 < equal
+#ifndef CC_LOG_SKEW_W1
+#define CC_LOG_SKEW_W1 27
+#endif
+#ifndef CC_LOG_SKEW_W2
+#define CC_LOG_SKEW_W2 22
+#endif
+#ifndef CC_LOG_SKEW_W3
+#define CC_LOG_SKEW_W3 18
 #endif
 #ifndef CC_LOG_STORE_AUX
 #define CC_LOG_STORE_AUX 2  // cache policy bits of the write-log row stores (2 = nontemporal: -20 us a batch)
@@ -1418,23 +1441,60 @@ __device__ __forceinline__ void load_rows(uint32_t (&w)[M], const unsigned char*
 template <int M, bool Delta>
 __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab) {
     constexpr int WV = log_waves(M, Delta);
+#if CC_LOG_SKEW
+    // an equal share of the heads per workgroup: [hb0, hb1); a workgroup without
+    // one (a small log) leaves before filling its 160 KiB of LDS
+    const uint32_t Hall = *a.head_count;
+    const uint32_t hb0 = (uint32_t)((uint64_t)Hall * blockIdx.x / gridDim.x);
+    const uint32_t hb1 = (uint32_t)((uint64_t)Hall * (blockIdx.x + 1) / gridDim.x);
+    if (hb0 >= hb1) return;
+#else
     // a block whose waves own no head (a small log) leaves before filling its
     // 160 KiB of LDS (uniform per block)
     if ((uint64_t)blockIdx.x * WV >= *a.head_count) return;
+#endif
+#if CC_LOG_TRACE
+    const uint64_t tt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     fill_lds<64 * WV>(tab, static_cast<const uint4*>(a.image));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if CC_LOG_TRACE
+    const uint64_t tt1 = __builtin_amdgcn_s_memrealtime();
+    uint64_t tt2 = 0, tpages = 0, tmid = 0;
+#endif
     const uint32_t c0 = lane << 2 & 0x7Cu;
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
     const uint32_t* pages = reinterpret_cast<const uint32_t*>(a.pool) + lane;
     const uint32_t pb = a.page_bytes;
+#if CC_LOG_SKEW
+    // The workgroup's heads are cut among its waves by age.  Its waves sit 4 to a
+    // SIMD (wave t on SIMD t % 4, the (t / 4)-th oldest there) and the SIMD
+    // issues oldest-first: with equal shares the four age groups ended at 80, 92,
+    // 103 and 113 us (per-wave clocks, scripts/trace_log.py) and the workgroup
+    // ran its last ~30 us with fewer waves than pages in flight.  Shares
+    // weighted by age group (kSkew[t / 4]) end them within ~10 us of each other:
+    // -3 % a batch (a priority that rotates every step instead: -1.5 %).
+    constexpr uint32_t kSkew[4] = {CC_LOG_SKEW_W0, CC_LOG_SKEW_W1, CC_LOG_SKEW_W2, CC_LOG_SKEW_W3};
+    auto wprefix = [&](uint32_t t) {  // sum of the weights of waves 0 .. t-1
+        uint32_t p = 0;
+        for (uint32_t u = 0; u < t; u++) p += kSkew[(u / 4) & 3];
+        return p;
+    };
+    const uint32_t Hb = hb1 - hb0, wsum = wprefix(WV);
+    const uint32_t H = hb0 + (uint32_t)((uint64_t)Hb * wprefix(wave + 1) / wsum);  // this wave: [first, H)
+    const uint32_t first = hb0 + (uint32_t)((uint64_t)Hb * wprefix(wave) / wsum);
+    constexpr uint32_t W = 1;  // lane k <- head base + k
+#else
     const uint32_t H = *a.head_count;
     const uint32_t W = gridDim.x * WV;
+    const uint32_t first = blockIdx.x * WV + wave;
+#endif
     // static shares only: a dynamic tail (the last 1/8 or 1/16 of the heads in
     // chunks of 4-16 through one atomic counter, as the page kernel does) measured
     // 7-19 % slower here (0.177-0.197 vs 0.165 ms a batch)
-    for (uint32_t base = blockIdx.x * WV + wave; base < H; base += 64u * W) {
+    for (uint32_t base = first; base < H; base += 64u * W) {
         // lane k <- head base + k*W (clamped loads: no branches around them)
         const uint64_t ih = (uint64_t)base + (uint64_t)lane * W;
         const bool hv = ih < H;
@@ -1455,6 +1515,11 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         const uint32_t u1 = single ? 0u : nxt / a.slots;  // several pieces: the second one's update
         const uint64_t singles = __ballot(single);
         const uint32_t cnt = (uint32_t)__popcll(__ballot(hv));  // valid lanes are 0 .. cnt-1
+#if CC_LOG_TRACE
+        asm volatile("" ::"v"(u1), "v"(hsp));  // the metadata has arrived
+        if (!tt2) tt2 = __builtin_amdgcn_s_memrealtime();
+        tpages += cnt | (uint64_t)__popcll(~singles & __ballot(hv)) << 16;
+#endif
         // two pages in flight: k (being merged + hashed) and k+1.  (A third
         // buys nothing: a page iteration issues ~53 VMEM instructions -- 16 page
         // loads, 20 source loads, 17 stores -- and gfx950's 6-bit vmcnt cannot
@@ -1508,6 +1573,9 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         auto step = [&](uint32_t (&X)[M], Src& SX, const Piece& px, uint32_t pg, uint32_t hh, uint32_t ocx,
                         uint32_t (&Y)[M], Src& SY, Piece& py, uint32_t& pgy, uint32_t& ocy) {
             const bool more = hh + 1 < cnt;
+#if CC_LOG_TRACE
+            if (hh == 12) tmid = __builtin_amdgcn_s_memrealtime();
+#endif
             // next page + its first piece's source bytes in flight (clamped to the
             // last page: a harmless re-read, so every step issues the same loads
             // and the vmcnt waits stay exact)
@@ -1642,6 +1710,17 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
             if (!step(B, S1, pB, pgB, h + 1, ocB, A, S0, pA, pgA, ocA)) break;
         }
     }
+#if CC_LOG_TRACE
+    const uint32_t wv = blockIdx.x * WV + wave;
+    if (lane == 0 && wv < 4096) {
+        g_ltrace[0][wv] = tt0;
+        g_ltrace[1][wv] = tt1;
+        g_ltrace[2][wv] = tt2;
+        g_ltrace[3][wv] = __builtin_amdgcn_s_memrealtime();
+        g_ltrace[4][wv] = tpages | (uint64_t)__smid() << 32;
+        g_ltrace[5][wv] = tmid;
+    }
+#endif
 }
 
 template <int M, bool Delta>
@@ -2107,6 +2186,9 @@ hipError_t launch_fold(const FoldLaunch& a, hipStream_t s) {
 }
 
 
+#if CC_LOG_TRACE
+hipError_t log_trace_read(uint64_t* host) { return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ltrace), sizeof(g_ltrace)); }
+#endif
 #if CC_WAVE_TRACE
 hipError_t wave_trace_read(uint64_t* host) { return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rtrace), sizeof(g_rtrace)); }
 #endif
