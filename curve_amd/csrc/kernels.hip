@@ -1521,9 +1521,10 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         tpages += cnt | (uint64_t)__popcll(~singles & __ballot(hv)) << 16;
 #endif
         // two pages in flight: k (being merged + hashed) and k+1.  (A third
-        // buys nothing: a page iteration issues ~53 VMEM instructions -- 16 page
-        // loads, 20 source loads, 17 stores -- and gfx950's 6-bit vmcnt cannot
-        // count two iterations' worth, so the waits stop being exact.)
+        // bought nothing, round 3: 0.1488 vs 0.1454 ms in a timing ablation.  A
+        // page iteration issues ~39 VMEM instructions in full mode -- 16 row
+        // loads, 6 edge loads, 16 row stores, the CRC -- and ~53 on the generic
+        // path; gfx950's 6-bit vmcnt counts at most 63 outstanding.)
         uint32_t A[M], B[M];
         constexpr bool kRowSel = CC_LOG_ROWSEL && !Delta && CC_LOG_ABLATE == 0;
         using Src = typename std::conditional<kRowSel, PieceEdges, PieceSrc<M>>::type;
