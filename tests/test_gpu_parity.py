@@ -868,19 +868,21 @@ def test_write_log_small_logs(dev, oracle, n, page_bytes, delta):
     assert (u32(crcs) == oracle.page_crcs(want, page_bytes)).all()
 
 
-@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("seed", range(40))
 def test_write_log_random_configs(dev, oracle, seed):
     """Randomised write logs across the geometry space -- page size 256 B..8 KiB,
-    1..3000 writes (both the one-launch and the hash-table path), max_len up to
-    two pages, overlap density, contract breakers, full or delta CRC mode --
-    against in-order host application and the oracle's page CRCs."""
+    1..20000 writes (the one-launch path, the hash-table path, and logs with more
+    touched pages than the grid has waves x 64, where every workgroup's share is
+    cut among its waves by SIMD age), max_len up to two pages, overlap density,
+    contract breakers, full or delta CRC mode -- against in-order host
+    application and the oracle's page CRCs."""
     from curve_amd import crc as C
     rng = np.random.default_rng(1000 + seed)
     pb = int(rng.choice([256, 512, 1024, 4096, 8192]))
-    n = int(rng.choice([1, 2, 5, 33, 64, 65, 300, 3000]))
+    n = int(rng.choice([1, 2, 5, 33, 64, 65, 300, 3000, 20000]))
     max_len = int(rng.integers(1, 2 * pb + 1))
     delta = bool(rng.integers(0, 2))
-    pool_bytes = int(rng.choice([1, 2, 4])) << 20
+    pool_bytes = (int(rng.choice([1, 2, 4])) << 20) if n < 20000 else (64 << 20)
     host = rng.integers(0, 256, pool_bytes, dtype=np.uint8)
     d_pool = to_dev(host, dev)
     crcs = C.page_crc(d_pool, pb)
