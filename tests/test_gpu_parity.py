@@ -871,9 +871,9 @@ def test_write_log_small_logs(dev, oracle, n, page_bytes, delta):
 @pytest.mark.parametrize("seed", range(40))
 def test_write_log_random_configs(dev, oracle, seed):
     """Randomised write logs across the geometry space -- page size 256 B..8 KiB,
-    1..20000 writes (the one-launch path, the hash-table path, and logs with more
-    touched pages than the grid has waves x 64, where every workgroup's share is
-    cut among its waves by SIMD age), max_len up to two pages, overlap density,
+    1..20000 writes (the one-launch path, and the hash-table path from a handful of
+    touched pages to thousands in every workgroup, each workgroup's share cut
+    among its waves by SIMD age), max_len up to two pages, overlap density,
     contract breakers, full or delta CRC mode -- against in-order host
     application and the oracle's page CRCs."""
     from curve_amd import crc as C
