@@ -82,5 +82,6 @@ ref = results[order[0]]
 for p in libs:
     same = all(torch.equal(a, b) for a, b in zip(results[p], ref))
     st, kt = sorted(step[p]), sorted(kern[p])
-    print(f"{os.path.basename(p)}: step median {st[len(st) // 2]:.4f} ms, page kernel median {kt[len(kt) // 2]:.4f} ms, "
-          f"same_results {same}", flush=True)
+    med = kt[len(kt) // 2]
+    print(f"{os.path.basename(p)}: step median {st[len(st) // 2]:.4f} ms, page kernel median {med:.4f} ms "
+          f"(spread {(kt[-1] - kt[0]) / med * 100:.2f} %, mean {sum(kt) / len(kt):.4f}), same_results {same}", flush=True)
