@@ -966,7 +966,7 @@ bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork
     w->n_pieces = n_updates * log_slots(max_len, page_bytes);
     if (w->n_pieces >= (1ull << 31)) return false;
 #ifndef CC_LOG_TABLE_FACTOR
-#define CC_LOG_TABLE_FACTOR 4  // table entries >= 4 x pieces: insert 15.8 -> 11.2 us (fewer probe round trips; 8: 10.3 us but a 5 us memset)
+#define CC_LOG_TABLE_FACTOR 8  // table entries >= 8 x pieces (2 x -> 4 x: insert 15.8 -> 11.2 us; 8 x cost a 5 us memset until the engine-owned table needed none: round 3, 8 x -1.1 % a batch)
 #endif
     uint64_t te = 1024;
     while (te < CC_LOG_TABLE_FACTOR * w->n_pieces) te <<= 1;  // load <= 1 / factor
