@@ -1095,7 +1095,7 @@ __global__ void shift_kernel(const uint32_t* __restrict__ crcs, const uint64_t* 
 // ---------------------------------------------------------------------------
 // Grouping by page without a sort.  Piece t = (update t / slots, its k-th page,
 // k = t % slots).  Every piece inserts its page into an open-addressing table
-// (linear probing, <= 50 % load) whose 64-bit entry holds {page + 1, piece + 1}
+// (linear probing, <= 12.5 % load: >= 8 x pieces, engine.hip) whose 64-bit entry holds {page + 1, piece + 1}
 // of the page's most recently inserted piece: one CAS both claims the page and
 // pushes the piece onto the page's list (next[piece] = the previous head).
 // The piece that claims an empty entry appends the entry's slot to the head
