@@ -518,6 +518,9 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
 #ifndef CC_LOG_SKEW_W3
 #define CC_LOG_SKEW_W3 18
 #endif
+#ifndef CC_LOG_ROW_AUX
+#define CC_LOG_ROW_AUX 2  // cache policy bits of the write-log row loads (full mode; 2 = nontemporal)
+#endif
 #ifndef CC_LOG_STORE_AUX
 #define CC_LOG_STORE_AUX 2  // cache policy bits of the write-log row stores (2 = nontemporal: -20 us a batch)
 #endif
@@ -1347,7 +1350,8 @@ __device__ __forceinline__ void load_rows_sel(uint32_t (&w)[M], const unsigned c
                                                                          kBufFlags);
 #pragma unroll
     for (int j = 0; j < M; j++)
-        w[j] = __builtin_amdgcn_raw_buffer_load_b32(((cov >> j) & 1u) ? rs : rp, row_sel(4u * lane) + 256u * j, 0, 2);
+        w[j] = __builtin_amdgcn_raw_buffer_load_b32(((cov >> j) & 1u) ? rs : rp, row_sel(4u * lane) + 256u * j, 0,
+                                                    CC_LOG_ROW_AUX);
 }
 
 template <int M>
