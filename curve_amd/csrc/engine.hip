@@ -968,9 +968,10 @@ bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork
 #ifndef CC_LOG_TABLE_FACTOR
 #define CC_LOG_TABLE_FACTOR 8  // table entries >= 8 x pieces (2 x -> 4 x: insert 15.8 -> 11.2 us; 8 x cost a 5 us memset until the engine-owned table needed none: round 3, 8 x -1.1 % a batch)
 #endif
+    // load <= 1 / factor, up to the 2^32 slots 32-bit slot indices reach; never above 1/4
     uint64_t te = 1024;
-    while (te < CC_LOG_TABLE_FACTOR * w->n_pieces) te <<= 1;  // load <= 1 / factor
-    if (te > (1ull << 32)) return false;  // slots and the mask are 32-bit
+    while (te < CC_LOG_TABLE_FACTOR * w->n_pieces && te < (1ull << 32)) te <<= 1;
+    if (te < 4 * w->n_pieces) return false;
     w->table_entries = te;
     w->next_off = 0;
     w->heads_off = align256(w->n_pieces * 4);

@@ -91,9 +91,9 @@ def test_argument_checks_need_no_gpu():
 def test_write_log_work_sizing_limits():
     """cc_apply_log_work_bytes (host arithmetic only): the caller's buffer holds
     a list link and a touched-page slot per piece (the hash table is the
-    engine's, >= 4 entries per piece in a power of two), and a log whose table
-    would need more than 2^32 slots (32-bit slot indices) is refused with 0, not
-    truncated."""
+    engine's: >= 8 entries per piece in a power of two up to 2^32 slots, never
+    fewer than 4 per piece), and a log whose table would need more than 2^32
+    slots at 4 per piece (32-bit slot indices) is refused with 0, not truncated."""
     from curve_amd import _lib
     L = _lib.lib()
     small = L.cc_apply_log_work_bytes(65536, 4096, 4096)  # 2 pieces per write
