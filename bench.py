@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--file-chunks", type=int, default=128, help="datastore read-path leg (0 = skip)")
     p.add_argument("--wal-entries", type=int, default=65536, help="WAL replay leg: entries per batch (0 = skip)")
     p.add_argument("--comm-timeout-ms", type=int, default=60000, help="N>1: bound on the native RCCL init")
+    p.add_argument("--exchange-timeout-ms", type=int, default=120000,
+                   help="N>1: bound on waiting for the steps' digest exchanges (a peer lost after init)")
     p.add_argument("--traffic-json", default=None, help="PMC traffic summary (default: newest profiles/traffic_*.json)")
     return p.parse_args()
 
@@ -589,6 +591,42 @@ def launch_ranks(args):
     sys.exit(subprocess.call(cmd))
 
 
+TIMED = {}
+
+
+def timed_steps(args, step, sync, world, rank, n, chunk, dist):
+    """W untimed warm-up steps (plus the clock floor), then EXACTLY K timed
+    steps bracketed by a barrier and a device sync on both sides.  Results in
+    TIMED (el: seconds of this rank, clock_warm: extra untimed steps)."""
+    for _ in range(args.warmup):
+        step(None)
+    # The GPU needs sustained load before it runs at its steady rate: launches
+    # ramp 2.77 -> 2.51 ms over the first ~30 ms after idle, and the first
+    # process on a fresh box stays ~4 % slow (2.57 ms a step) through 100 ms of
+    # warm-up but settles at 2.47 ms after ~2.5 s of it.  The metric is the
+    # steady state of a continuous scan, so when the W requested warm-up steps
+    # are shorter than --clock-warm-ms of work, extra UNTIMED steps run up to
+    # that, reported as "clock_warmup_steps".  The count follows from the
+    # per-rank bytes only, so every rank runs the same number of steps (each
+    # step holds a collective).  The timed region is still exactly K steps.
+    est_ms = n * chunk / 6.5e12 * 1e3  # ~6.5 TB/s
+    clock_warm = max(0, int(np.ceil(args.clock_warm_ms / est_ms)) - args.warmup) if args.warmup > 0 else 0
+    for _ in range(clock_warm):
+        step(None)
+    sync()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    sync()
+    if world > 1:
+        dist.barrier()
+    TIMED["el"] = time.perf_counter() - t0
+    TIMED["clock_warm"] = clock_warm
+
+
 def main():
     args = parse()
     launch_ranks(args)
@@ -606,10 +644,14 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
+        # collectives outside the native exchange (barriers, timing all-reduces,
+        # the torch.distributed digest path) are bounded by the group's timeout
+        import datetime
+        pg_timeout = datetime.timedelta(seconds=float(os.environ.get("BENCH_DIST_TIMEOUT_S", "600")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=pg_timeout)
 
     from curve_amd import crc as C
     from curve_amd.pool import agreed_comm, copyset_layout, pool_scan, reduce_digests, shard_range
@@ -657,40 +699,46 @@ def main():
         a.record(stream)
         b.record(stream)
 
+    # failure injection (the reference's libfiu failpoints play this role): the
+    # rank named here stops participating in the digest exchange after init, as
+    # a rank whose peer link died would; its peers must give up at the bound
+    # (--exchange-timeout-ms for the native exchange, the group timeout for
+    # torch.distributed) and the run must end with an error line, not a hang
+    skip_exchange = world > 1 and os.environ.get("CC_INJECT_SKIP_EXCHANGE_RANK", "") == str(rank)
+
     def step(k):
         # ONE C call: page CRCs + metapage CRCs + fused epilogue (slice CRCs,
         # file CRCs, digest partials) + the RCCL digest exchange (cc_pool_scan_dev)
-        pool_scan(pool, after_mult, group, digest, comm=comm, stream=stream,
+        pool_scan(pool, after_mult, group, digest, comm=None if skip_exchange else comm, stream=stream,
                   events=ev[k] if k is not None else None)
-        if world > 1 and comm is None:
+        if world > 1 and comm is None and not skip_exchange:
             full_digest[0] = reduce_digests(digest, dist)
 
-    for _ in range(args.warmup):
-        step(None)
-    # The GPU needs sustained load before it runs at its steady rate: launches
-    # ramp 2.77 -> 2.51 ms over the first ~30 ms after idle, and the first
-    # process on a fresh box stays ~4 % slow (2.57 ms a step) through 100 ms of
-    # warm-up but settles at 2.47 ms after ~2.5 s of it.  The metric is the
-    # steady state of a continuous scan, so when the W requested warm-up steps
-    # are shorter than --clock-warm-ms of work, extra UNTIMED steps run up to
-    # that, reported as "clock_warmup_steps".  The count follows from the
-    # per-rank bytes only, so every rank runs the same number of steps (each
-    # step holds a collective).  The timed region is still exactly K steps.
-    est_ms = n * chunk / 6.5e12 * 1e3  # ~6.5 TB/s
-    clock_warm = max(0, int(np.ceil(args.clock_warm_ms / est_ms)) - args.warmup) if args.warmup > 0 else 0
-    for _ in range(clock_warm):
-        step(None)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
+    def sync():
+        # the steps' exchanges complete, or the run ends: cc_comm_wait polls the
+        # stream and the communicator against a deadline and aborts it when a
+        # peer is gone (a plain synchronize would wait forever)
+        if comm is not None:
+            comm.wait(stream, args.exchange_timeout_ms)
+        torch.cuda.synchronize()
+
+    def fail(e):
+        # one JSON error line (every rank: the driver reads rank 0's), then leave
+        # at once -- no barrier, no teardown that could wait for the lost peer
+        print(json.dumps({"error": f"rank {rank}: digest exchange failed: {e}", "n_gpus": world,
+                          "metric": "GiB/s CRC32C over 4KiB pages (device-resident) + % HBM roofline, 1/2/4/8 GPU",
+                          "value": None}), flush=True)
+        sys.stderr.flush()
+        os._exit(3)
+
+    try:
+        timed_steps(args, step, sync, world, rank, n, chunk, dist)
+    except (C.CurveCrcError, RuntimeError) as e:
+        if world == 1:
+            raise
+        fail(e)
+    el = TIMED["el"]
+    clock_warm = TIMED["clock_warm"]
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -11,7 +11,9 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcurvecrc.so")
+# $CURVE_AMD_LIB / $CURVE_AMD_HOST_LIB name another build of the same libraries
+# (scripts/sanitize.sh runs the CPU suite on ASan/UBSan builds)
+LIB_PATH = os.environ.get("CURVE_AMD_LIB") or os.path.join(_HERE, "libcurvecrc.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 CC_OK = 0
@@ -24,6 +26,7 @@ CC_ECOMM = -71
 CC_EIO = -5001
 CC_ESTALE = -116
 CC_ETIMEDOUT = -110
+CC_EFORMAT = -5002
 CC_ENOENT = -2
 CC_COMM_ID_BYTES = 128
 
@@ -93,6 +96,7 @@ SIGNATURES = {
                                    ctypes.POINTER(CcScanDigest)]),
     "cc_engine_init": (_int, [ctypes.POINTER(CcOpts)]),
     "cc_engine_fini": (_int, []),
+    "cc_engine_trim": (_int, []),
     "cc_device_count": (_int, []),
     "cc_strerror": (ctypes.c_char_p, [_int]),
     "cc_version": (ctypes.c_char_p, []),
@@ -125,6 +129,7 @@ SIGNATURES = {
     "cc_comm_abort": (_int, [_vp]),
     "cc_comm_size": (_int, [_vp]),
     "cc_comm_rank": (_int, [_vp]),
+    "cc_comm_wait": (_int, [_vp, _vp, _u32]),
     "cc_digest_allreduce_dev": (_int, [_vp, _vp, _u64, _vp]),
     "cc_pool_scan_dev": (_int, [ctypes.POINTER(CcPoolShard), _vp, _vp]),
     "cc_pcrc_encoded_bytes": (_u64, [_u32]),
@@ -142,7 +147,7 @@ SIGNATURES = {
 }
 
 # ---- the host layer's C ABI (include/curve_integrity.h, curve_amd/host/libcurvehost.so)
-HOST_LIB_PATH = os.path.join(_HERE, "host", "libcurvehost.so")
+HOST_LIB_PATH = os.environ.get("CURVE_AMD_HOST_LIB") or os.path.join(_HERE, "host", "libcurvehost.so")
 
 
 class CcIsvcOpts(ctypes.Structure):

@@ -90,6 +90,24 @@ struct Staging {
 // insert takes the context's table mutex).
 constexpr int kEpiSlots = 16;
 
+// Per-stream state (the page kernel's tail counters, the write log's table) is
+// keyed by stream.  hipStreamPerThread, hipStreamLegacy and the null stream are
+// pseudo-handles: one value standing for a different real stream in each
+// thread (per-thread default streams), so kernels of two threads could run
+// concurrently on one block or table.  Their key is the handle AND the calling
+// thread; a real stream's key is its handle.
+struct StreamKey {
+    hipStream_t s = nullptr;
+    std::thread::id tid;
+    bool operator==(const StreamKey& o) const { return s == o.s && tid == o.tid; }
+};
+inline StreamKey stream_key(hipStream_t s) {
+    StreamKey k;
+    k.s = s;
+    if (s == nullptr || s == hipStreamLegacy || s == hipStreamPerThread) k.tid = std::this_thread::get_id();
+    return k;
+}
+
 struct DevCtx {
     int device = -1;
     bool ready = false;
@@ -104,12 +122,12 @@ struct DevCtx {
     // (kernels.hip tail_reset): zeroed on the stream when created, left zero by
     // every launch that uses it, so a call needs no allocation or memset
     std::mutex tail_mu;
-    std::vector<std::pair<hipStream_t, unsigned long long*>> tails;
+    std::vector<std::pair<StreamKey, unsigned long long*>> tails;
     // the write log's page tables, one per stream (apply_log); log_mu is held
     // over a call's whole enqueue (insert + pages) so calls sharing a stream
     // cannot interleave on its table
     struct LogTable {
-        hipStream_t s;
+        StreamKey s;
         unsigned char* p;
         uint64_t entries;
         bool dirty;
@@ -274,13 +292,15 @@ constexpr size_t kMaxTailBlocks = 256;  // streams with a block of their own
 
 // The stream's self-resetting tail-counter block, created (and zeroed on the
 // stream) on first use; null when kMaxTailBlocks streams already hold one.
-// Keyed by the stream handle: a destroyed stream's handle is only reused for a
-// new stream after hipStreamDestroy, which the caller orders after that
-// stream's work as for any of its buffers.
+// Keyed by the stream (stream_key: a pseudo-handle is per calling thread): a
+// destroyed stream's handle is only reused for a new stream after
+// hipStreamDestroy, which the caller orders after that stream's work as for
+// any of its buffers.
 unsigned long long* tail_block(DevCtx* c, hipStream_t s) {
+    const StreamKey key = stream_key(s);
     std::lock_guard<std::mutex> lk(c->tail_mu);
     for (auto& t : c->tails)
-        if (t.first == s) return t.second;
+        if (t.first == key) return t.second;
     if (c->tails.size() >= kMaxTailBlocks) return nullptr;
     void* p = nullptr;
     if (hipMalloc(&p, kTailBlockBytes) != hipSuccess) return nullptr;
@@ -288,7 +308,7 @@ unsigned long long* tail_block(DevCtx* c, hipStream_t s) {
         (void)hipFree(p);
         return nullptr;
     }
-    c->tails.push_back({s, static_cast<unsigned long long*>(p)});
+    c->tails.push_back({key, static_cast<unsigned long long*>(p)});
     return static_cast<unsigned long long*>(p);
 }
 
@@ -447,6 +467,7 @@ const char* cc_strerror(int code) {
         case CC_EIO: return "I/O error";
         case CC_ESTALE: return "per-page CRC table is stale";
         case CC_ETIMEDOUT: return "timed out";
+        case CC_EFORMAT: return "chunk file size is not metapage + chunk (file format error)";
         default: return "unknown error";
     }
 }
@@ -520,6 +541,19 @@ int cc_engine_fini(void) {
         }
     }
     old.clear();
+    return CC_OK;
+}
+
+int cc_engine_trim(void) {
+    CtxRef c;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->log_mu);  // no write-log call enqueues meanwhile
+    const hipError_t e = hipDeviceSynchronize();  // kernels of earlier calls may still use a table
+    if (e != hipSuccess) return map_err(e);
+    for (auto& t : c->log_tabs)
+        if (t.p) (void)hipFree(t.p);
+    c->log_tabs.clear();
     return CC_OK;
 }
 
@@ -982,12 +1016,21 @@ bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork
 // The stream's write-log table with >= `entries` slots, zero when the call's
 // launches run (caller holds c->log_mu).  Created or grown (stream-ordered
 // free of the old one) with a clear on the stream; a table a failed call left
-// dirty is cleared.  nullptr when kMaxTailBlocks streams already hold one.
+// dirty is cleared.  nullptr when kMaxTailBlocks streams already hold one, or
+// when the log needs more than kLogTableCacheEntries slots (such a call takes a
+// table of its own, freed with it: one huge log must not pin device memory for
+// the rest of the process).  cc_engine_trim frees every cached table.
+#ifndef CC_LOG_TABLE_CACHE_ENTRIES
+#define CC_LOG_TABLE_CACHE_ENTRIES (1ull << 23)  // 64 MiB a stream: logs of up to 1M pieces (512K two-page writes)
+#endif
+constexpr uint64_t kLogTableCacheEntries = CC_LOG_TABLE_CACHE_ENTRIES;
 DevCtx::LogTable* log_table(DevCtx* c, hipStream_t s, uint64_t entries, hipError_t* err) {
     *err = hipSuccess;
+    if (entries > kLogTableCacheEntries) return nullptr;  // a log this big: a table for its call only
+    const StreamKey key = stream_key(s);
     DevCtx::LogTable* t = nullptr;
     for (auto& x : c->log_tabs)
-        if (x.s == s) t = &x;
+        if (x.s == key) t = &x;
     if (t && t->entries < entries) {
         if ((*err = hipFreeAsync(t->p, s)) != hipSuccess) return nullptr;
         t->p = nullptr;
@@ -995,7 +1038,7 @@ DevCtx::LogTable* log_table(DevCtx* c, hipStream_t s, uint64_t entries, hipError
     }
     if (!t) {
         if (c->log_tabs.size() >= kMaxTailBlocks) return nullptr;
-        c->log_tabs.push_back({s, nullptr, 0, false});
+        c->log_tabs.push_back({key, nullptr, 0, false});
         t = &c->log_tabs.back();
     }
     if (!t->p) {

@@ -100,7 +100,7 @@ int64_t now_ns() {
 
 // One tick of the clock file timestamps come from (the kernel's coarse
 // realtime clock: a jiffy, 1-10 ms); at least 1 ms, at most 1 s.
-int64_t mtime_tick_ns() {
+int64_t coarse_tick_ns() {
     static const int64_t tick = [] {
         struct timespec r;
         int64_t t = 0;
@@ -108,6 +108,18 @@ int64_t mtime_tick_ns() {
         return t < 1000000 ? 1000000 : (t > 1000000000 ? 1000000000 : t);
     }();
     return tick;
+}
+
+// The granularity a recorded mtime may have been truncated to.  A filesystem
+// that keeps whole seconds (ext4 with 128-byte inodes, many NFS / FUSE mounts)
+// or FAT's 2 s records an mtime with no sub-second part: a same-size rewrite
+// within that second keeps it, so such a table stays racy for 1 s (2 s when the
+// second is even) after its mtime, not for one coarse-clock tick.
+int64_t mtime_granule_ns(int64_t mtime) {
+    const int64_t tick = coarse_tick_ns();
+    if (mtime % 1000000000ll != 0) return tick;
+    const int64_t g = mtime % 2000000000ll == 0 ? 2000000000ll : 1000000000ll;
+    return g > tick ? g : tick;
 }
 
 // Chunk file identity for staleness: sn from the metapage, mtime + size from stat.
@@ -159,7 +171,7 @@ int cc_pcrc_encode(const cc_pcrc_header* h, const uint32_t* page_crcs, void* out
     put64(p + 32, (uint64_t)h->data_mtime_ns);
     put64(p + 40, h->data_size);
     put64(p + 48, (uint64_t)h->stamp_ns);
-    memcpy(p + CC_PCRC_HEADER_BYTES, page_crcs, 4ull * h->n_pages);
+    if (h->n_pages) memcpy(p + CC_PCRC_HEADER_BYTES, page_crcs, 4ull * h->n_pages);  // page_crcs may be null at 0
     put32(p + 56, crc32c_value(p, 56));
     put32(p + 60, crc32c_value(p + CC_PCRC_HEADER_BYTES, 4ull * h->n_pages));
     return CC_OK;
@@ -212,7 +224,8 @@ int cc_chunk_meta_sn(const void* metapage, uint32_t bytes, uint64_t* sn) {
 
 int cc_pcrc_is_racy(const cc_pcrc_header* h) {
     if (!h) return CC_EINVAL;
-    return h->data_mtime_ns + mtime_tick_ns() > h->stamp_ns ? 1 : 0;
+    // closed boundary (git's >=): the coarse clock may lag a write by a full tick
+    return h->data_mtime_ns + mtime_granule_ns(h->data_mtime_ns) >= h->stamp_ns ? 1 : 0;
 }
 
 int cc_pcrc_load(const char* table_path, cc_pcrc_header* h, uint32_t* page_crcs, uint32_t max_pages) {
@@ -262,7 +275,8 @@ namespace {
 // must still be the one the CRCs were computed under (else CC_ESTALE, nothing
 // written): a write landing between a job's read and its table refresh must not
 // get a table of the bytes before it.  `stamp` is when those bytes were known
-// current (0 = now).
+// current (0 = now: only for a caller holding the chunk's write lock, so no
+// write can land between the bytes it describes and this call).
 int store_table(const char* chunk_path, uint32_t meta_bytes, const char* table_path, const uint32_t* page_crcs,
                 uint32_t n_pages, uint32_t page_bytes, const ChunkId* expect, int64_t stamp = 0) {
     if (!chunk_path || !table_path || (n_pages && !page_crcs) || page_bytes == 0 || meta_bytes == 0)
@@ -304,7 +318,12 @@ int cc_pcrc_store_expect(const char* chunk_path, uint32_t meta_bytes, const char
     e.sn = expect->chunk_sn;
     e.mtime = expect->data_mtime_ns;
     e.size = expect->data_size;
-    return store_table(chunk_path, meta_bytes, table_path, page_crcs, n_pages, page_bytes, &e);
+    // never the store's own clock: a second same-size write in the mtime's tick
+    // keeps the identity, and a table stamped later than that would not be racy
+    // and would condemn the newer bytes.  The caller's stamp (taken before its
+    // pwrite), else the mtime itself -- racy until a check re-stamps the table.
+    const int64_t stamp = expect->stamp_ns ? expect->stamp_ns : expect->data_mtime_ns;
+    return store_table(chunk_path, meta_bytes, table_path, page_crcs, n_pages, page_bytes, &e, stamp);
 }
 
 int cc_integrity_check(const char* const* chunk_paths, const char* const* table_paths, uint64_t n,

@@ -30,11 +30,12 @@
 #include "kernels.h"
 
 struct cc_comm {
-    ncclComm_t nc = nullptr;
+    ncclComm_t nc = nullptr;     // null once aborted by cc_comm_wait (a peer gone)
     int nranks = 0, rank = 0, device = -1;
     uint32_t* gather = nullptr;  // nranks x cap words of all-gather scratch on `device`
     uint64_t cap = 0;
-    std::mutex mu;               // guards the scratch (re)allocation
+    hipEvent_t done = nullptr;   // cc_comm_wait's completion marker
+    std::mutex mu;               // guards the scratch (re)allocation and the event
 };
 
 static_assert(CC_COMM_ID_BYTES == sizeof(ncclUniqueId), "RCCL unique id size");
@@ -81,6 +82,36 @@ int settle(ncclComm_t nc, ncclResult_t r, std::chrono::steady_clock::time_point 
 // (a collective's enqueue never waits for peers, so this is microseconds)
 int settle_call(ncclComm_t nc, ncclResult_t r) {
     return settle(nc, r, std::chrono::steady_clock::now() + std::chrono::seconds(60));
+}
+
+constexpr uint32_t kDefaultWaitTimeoutMs = 60000;
+
+uint32_t wait_timeout_ms(uint32_t asked) {
+    if (asked) return asked;
+    if (const char* e = getenv("CC_COMM_WAIT_TIMEOUT_MS")) {
+        const long v = strtol(e, nullptr, 10);
+        if (v > 0) return (uint32_t)v;
+    }
+    return kDefaultWaitTimeoutMs;
+}
+
+// Failure injection (tests only; the reference's libfiu failpoints play this
+// role, test/failpoint/): $CC_INJECT_EXCHANGE_STALL_MS > 0 makes every digest
+// exchange first spin one wave on the stream for that long (at most 30 s), as
+// a collective whose peer stopped participating after init would sit in its
+// kernel.  cc_comm_wait must then give up at its deadline.
+uint32_t injected_stall_ms() {
+    const char* e = getenv("CC_INJECT_EXCHANGE_STALL_MS");
+    if (!e) return 0;
+    const long v = strtol(e, nullptr, 10);
+    return v <= 0 ? 0u : (uint32_t)(v < 30000 ? v : 30000);
+}
+
+// s_memrealtime runs at a constant 100 MHz on gfx9: 10 ns a tick.  One wave;
+// every exit path is bounded by the tick count.
+__global__ void stall_kernel(uint64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
 }  // namespace
@@ -146,6 +177,7 @@ static int comm_release(cc_comm* comm, bool abort) {
         }
     }
     if (comm->gather) (void)hipFree(comm->gather);
+    if (comm->done) (void)hipEventDestroy(comm->done);
     if (cur >= 0) (void)hipSetDevice(cur);
     delete comm;
     return rc;
@@ -157,8 +189,46 @@ int cc_comm_abort(cc_comm* comm) { return comm_release(comm, true); }
 int cc_comm_size(const cc_comm* comm) { return comm ? comm->nranks : 0; }
 int cc_comm_rank(const cc_comm* comm) { return comm ? comm->rank : -1; }
 
+int cc_comm_wait(cc_comm* comm, void* stream, uint32_t timeout_ms) {
+    if (!comm) return CC_EINVAL;
+    if (!comm->nc) return CC_ECOMM;  // aborted by an earlier wait
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (cur != comm->device && hipSetDevice(comm->device) != hipSuccess) return CC_ENODEV;
+    auto back = [&](int rc) {
+        if (cur >= 0 && cur != comm->device) (void)hipSetDevice(cur);
+        return rc;
+    };
+    hipError_t e;
+    {
+        std::lock_guard<std::mutex> lk(comm->mu);
+        if (!comm->done && (e = hipEventCreateWithFlags(&comm->done, hipEventDisableTiming)) != hipSuccess)
+            return back(map_hip(e));
+        if ((e = hipEventRecord(comm->done, s)) != hipSuccess) return back(map_hip(e));
+    }
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(wait_timeout_ms(timeout_ms));
+    for (;;) {
+        e = hipEventQuery(comm->done);
+        if (e == hipSuccess) return back(CC_OK);
+        if (e != hipErrorNotReady) return back(map_hip(e));
+        ncclResult_t ar = ncclSuccess;
+        const bool failed = ncclCommGetAsyncError(comm->nc, &ar) != ncclSuccess || (ar != ncclSuccess && ar != ncclInProgress);
+        const bool late = std::chrono::steady_clock::now() > deadline;
+        if (failed || late) {
+            // leave without the peers: the abort also releases the collective's
+            // kernels still waiting for them, so the stream drains
+            (void)ncclCommAbort(comm->nc);
+            comm->nc = nullptr;
+            return back(failed ? CC_ECOMM : CC_ETIMEDOUT);
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+}
+
 int cc_digest_allreduce_dev(cc_comm* comm, uint32_t* d_digest, uint64_t n, void* stream) {
     if (!comm || (!d_digest && n)) return CC_EINVAL;
+    if (!comm->nc) return CC_ECOMM;  // aborted: a peer was lost
     if (n == 0) return CC_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     {
@@ -175,6 +245,11 @@ int cc_digest_allreduce_dev(cc_comm* comm, uint32_t* d_digest, uint64_t n, void*
             if (e != hipSuccess) return map_hip(e);
             comm->cap = n;
         }
+    }
+    if (const uint32_t ms = injected_stall_ms()) {
+        hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, s, (uint64_t)ms * 100000ull);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return map_hip(e);
     }
     // ring all-gather of the partials into [rank][n], then out = XOR over ranks
     int rc = settle_call(comm->nc, ncclAllGather(d_digest, comm->gather, n, ncclUint32, comm->nc, s));

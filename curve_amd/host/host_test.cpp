@@ -267,7 +267,8 @@ void PoolScanShardRccl() {  // one rank's shard, native RCCL 
     for (uint64_t i = 0; i < n; i++)
         for (uint64_t k = 0; k < n; k++)
             if (group[k] == group[i] && ChunkFileName(ids[k]) > ChunkFileName(ids[i])) after[i] += chunk + meta;
-    void *d_data, *d_meta, *d_after, *d_mult, *d_group, *d_pc, *d_mc, *d_sc, *d_fc, *d_dig;
+    void *d_data = nullptr, *d_meta = nullptr, *d_after = nullptr, *d_mult = nullptr, *d_group = nullptr;
+    void *d_pc = nullptr, *d_mc = nullptr, *d_sc = nullptr, *d_fc = nullptr, *d_dig = nullptr;
     EXPECT(hipMalloc(&d_data, data.size()) == hipSuccess && hipMalloc(&d_meta, metas.size()) == hipSuccess);
     EXPECT(hipMalloc(&d_after, n * 8) == hipSuccess && hipMalloc(&d_mult, n * 4) == hipSuccess &&
            hipMalloc(&d_group, n * 4) == hipSuccess);
@@ -335,14 +336,14 @@ void WriteLogBothModes() {  // an ordered write log from plai
     }
     std::string want = pool;  // in-order application: later writes win
     for (const cc_update& u : log) want.replace(u.dst, u.len, src.substr(u.src, u.len));
-    void *d_src, *d_log, *d_work;
+    void *d_src = nullptr, *d_log = nullptr, *d_work = nullptr;
     EXPECT(hipMalloc(&d_src, src_bytes) == hipSuccess && hipMalloc(&d_log, n * sizeof(cc_update)) == hipSuccess);
     EXPECT(hipMemcpy(d_src, src.data(), src_bytes, hipMemcpyHostToDevice) == hipSuccess);
     EXPECT(hipMemcpy(d_log, log.data(), n * sizeof(cc_update), hipMemcpyHostToDevice) == hipSuccess);
     const uint64_t work = cc_apply_log_work_bytes(n, max_len, pb);
     EXPECT(work > 0 && hipMalloc(&d_work, work) == hipSuccess);
     for (int delta = 0; delta < 2; delta++) {
-        void *d_pool, *d_pc;
+        void *d_pool = nullptr, *d_pc = nullptr;
         EXPECT(hipMalloc(&d_pool, pool_bytes) == hipSuccess && hipMalloc(&d_pc, pool_bytes / pb * 4) == hipSuccess);
         EXPECT(hipMemcpy(d_pool, pool.data(), pool_bytes, hipMemcpyHostToDevice) == hipSuccess);
         EXPECT(cc_page_crc_dev(d_pool, pool_bytes / pb, pb, (uint32_t*)d_pc, nullptr) == CC_OK);
@@ -370,7 +371,8 @@ void PerRequestWriteAndRead() {
     std::string pool(pool_bytes, '\0'), src(8192, '\0');
     for (auto& c : pool) c = (char)(rng() & 0xFF);
     for (auto& c : src) c = (char)(rng() & 0xFF);
-    void *d_pool, *d_pc, *d_src, *d_log, *d_work, *d_reads, *d_bad, *d_total;
+    void *d_pool = nullptr, *d_pc = nullptr, *d_src = nullptr, *d_log = nullptr, *d_work = nullptr;
+    void *d_reads = nullptr, *d_bad = nullptr, *d_total = nullptr;
     EXPECT(hipMalloc(&d_pool, pool_bytes) == hipSuccess && hipMalloc(&d_pc, pool_bytes / pb * 4) == hipSuccess);
     EXPECT(hipMalloc(&d_src, src.size()) == hipSuccess && hipMalloc(&d_log, sizeof(cc_update)) == hipSuccess);
     EXPECT(hipMemcpy(d_pool, pool.data(), pool_bytes, hipMemcpyHostToDevice) == hipSuccess);
@@ -392,7 +394,7 @@ void PerRequestWriteAndRead() {
     const uint64_t rwork = cc_verify_reads_work_bytes(1);
     EXPECT(rwork > 0 && hipMalloc(&d_reads, sizeof(cc_range)) == hipSuccess && hipMalloc(&d_bad, 4) == hipSuccess &&
            hipMalloc(&d_total, 8) == hipSuccess);
-    void* d_rwork;
+    void *d_rwork = nullptr;
     EXPECT(hipMalloc(&d_rwork, rwork) == hipSuccess);
     for (int i = 0; i < 3; i++) {  // ReadChunk: one read per call
         uint32_t bad = 7;
@@ -479,7 +481,7 @@ void IntegrityWritePath() {
         WriteFile(paths.back(), MetaPage(c + 1) + pool.substr((size_t)c * chunk, chunk));
     }
     // the device pool (data of every chunk) + its CRC table, persisted per chunk
-    void *d_pool, *d_pc, *d_src, *d_log, *d_work;
+    void *d_pool = nullptr, *d_pc = nullptr, *d_src = nullptr, *d_log = nullptr, *d_work = nullptr;
     const uint64_t pool_bytes = pool.size(), n_pages = pool_bytes / pb;
     EXPECT(hipMalloc(&d_pool, pool_bytes) == hipSuccess && hipMalloc(&d_pc, n_pages * 4) == hipSuccess);
     EXPECT(hipMemcpy(d_pool, pool.data(), pool_bytes, hipMemcpyHostToDevice) == hipSuccess);

@@ -33,6 +33,23 @@ std::string TablePath(const std::string& tableDir, const std::string& chunkName)
     return tableDir + "/" + chunkName + ".pcrc";
 }
 
+// FileNameOperator::ParseFileName (datastore/filename_operator.h:55-62):
+// "chunk_<id>" (CHUNK) or "chunk_<id>_snap_<sn>" (SNAPSHOT), decimal ids
+bool IsChunkFileName(const std::string& name) {
+    auto digits = [&](size_t& i) {
+        const size_t s = i;
+        while (i < name.size() && name[i] >= '0' && name[i] <= '9') i++;
+        return i > s;
+    };
+    if (name.compare(0, 6, "chunk_") != 0) return false;
+    size_t i = 6;
+    if (!digits(i)) return false;
+    if (i == name.size()) return true;
+    if (name.compare(i, 6, "_snap_") != 0) return false;
+    i += 6;
+    return digits(i) && i == name.size();
+}
+
 IntegrityService::IntegrityService(const IntegrityOptions& opt) : opt_(opt) {
     worker_ = std::thread([this] { Run(); });
 }
@@ -164,20 +181,33 @@ void IntegrityService::DoJob(IntegrityJob* job) {
         job->error = why;
         cv_.notify_all();
     };
-    // chunk files of the chunk geometry, in std::sort name order (as GetHash lists them)
+    // the copyset's chunk files in std::sort name order (as GetHash lists them):
+    // every regular file of the chunk geometry, and every file NAMED as a chunk
+    // or snapshot (FileNameOperator, datastore/filename_operator.h:55-62) whose
+    // size is not metapage + chunk -- a truncated or extended chunk is exactly
+    // the damage a scan exists to find; CSChunkFile::Open reports it as
+    // FileFormatError (chunkserver_chunkfile.cpp:233-238), so it becomes that
+    // file's result (CC_EFORMAT), not a silent omission
     const uint64_t fileBytes = (uint64_t)opt_.chunkSize + opt_.metaPageSize;
     std::vector<std::string> names;
+    std::vector<std::string> misfit;  // chunk-named, wrong size (sorted below)
     DIR* d = opendir(dataDir.c_str());
     if (!d) return fail("cannot list " + dataDir + ": " + strerror(errno));
     while (struct dirent* e = readdir(d)) {
         if (!strcmp(e->d_name, ".") || !strcmp(e->d_name, "..")) continue;
         struct stat sb;
         const std::string p = dataDir + "/" + e->d_name;
-        if (stat(p.c_str(), &sb) == 0 && S_ISREG(sb.st_mode) && (uint64_t)sb.st_size == fileBytes)
+        if (stat(p.c_str(), &sb) != 0 || !S_ISREG(sb.st_mode)) continue;
+        if ((uint64_t)sb.st_size == fileBytes) {
             names.push_back(e->d_name);
+        } else if (IsChunkFileName(e->d_name)) {
+            names.push_back(e->d_name);
+            misfit.push_back(e->d_name);
+        }
     }
     closedir(d);
     std::sort(names.begin(), names.end());
+    std::sort(misfit.begin(), misfit.end());
     std::sort(done.begin(), done.end());
     std::vector<std::string> todo;
     for (const auto& n : names)
@@ -195,37 +225,53 @@ void IntegrityService::DoJob(IntegrityJob* job) {
             }
         }
         const size_t nb = std::min<size_t>(batch, todo.size() - b0);
-        std::vector<std::string> cp(nb), tp(nb);
-        std::vector<const char*> cpp(nb), tpp(nb);
+        std::vector<IntegrityFileResult> out(nb);
+        std::vector<std::string> cp, tp;
+        std::vector<size_t> at;  // out index of each file checked on the device
         for (size_t k = 0; k < nb; k++) {
-            cp[k] = dataDir + "/" + todo[b0 + k];
-            tp[k] = TablePath(tdir, todo[b0 + k]);
+            out[k].name = todo[b0 + k];
+            if (std::binary_search(misfit.begin(), misfit.end(), out[k].name)) {
+                out[k].status = CC_EFORMAT;
+                out[k].tableState = CC_TABLE_MISSING;  // no table is read or written for it
+                out[k].error = ErrText(CC_EFORMAT);
+                continue;
+            }
+            cp.push_back(dataDir + "/" + out[k].name);
+            tp.push_back(TablePath(tdir, out[k].name));
+            at.push_back(k);
+        }
+        const size_t nc = at.size();
+        std::vector<const char*> cpp(nc), tpp(nc);
+        for (size_t k = 0; k < nc; k++) {
             cpp[k] = cp[k].c_str();
             tpp[k] = tp[k].c_str();
         }
         cc_integrity_opts o = {opt_.chunkSize, opt_.metaPageSize, opt_.pageSize, opt_.ioThreads,
                                opt_.createMissing ? 1u : 0u, opt_.refreshStale ? 1u : 0u};
-        std::vector<cc_integrity_result> res(nb);
-        const uint64_t cap = (uint64_t)nb * n_pages;
+        std::vector<cc_integrity_result> res(nc);
+        const uint64_t cap = (uint64_t)nc * n_pages;
         std::vector<uint64_t> bad(cap);
         uint64_t nbad = 0;
-        const int rc = cc_integrity_check(cpp.data(), tpp.data(), nb, &o, res.data(), bad.data(), cap, &nbad);
-        if (rc) return fail(std::string("cc_integrity_check: ") + ErrText(rc));
-        std::vector<IntegrityFileResult> out(nb);
-        // a file's own failure (metapage header CRC -> CC_ECORRUPT, unreadable,
-        // or -ENOENT: deleted between the listing and the check) is that file's
-        // result, never the job's: the rest of the copyset is still checked
-        for (size_t k = 0; k < nb; k++) {
-            out[k].name = todo[b0 + k];
-            out[k].status = res[k].status;
-            out[k].tableState = res[k].table_state;
-            out[k].badPages = res[k].bad_pages;
-            out[k].firstBad = res[k].first_bad;
-            if (res[k].status) out[k].error = res[k].status == -ENOENT ? "vanished" : ErrText(res[k].status);
+        if (nc) {
+            const int rc = cc_integrity_check(cpp.data(), tpp.data(), nc, &o, res.data(), bad.data(), cap, &nbad);
+            if (rc) return fail(std::string("cc_integrity_check: ") + ErrText(rc));
         }
-        for (uint64_t q = 0; q < std::min(nbad, cap); q++) out[bad[q] >> 32].badList.push_back((uint32_t)bad[q]);
+        // a file's own failure (metapage header CRC -> CC_ECORRUPT, unreadable,
+        // -ENOENT: deleted between the listing and the check, or a size that
+        // changed since the listing -> CC_EINVAL) is that file's result, never
+        // the job's: the rest of the copyset is still checked
+        for (size_t k = 0; k < nc; k++) {
+            IntegrityFileResult& r = out[at[k]];
+            r.status = res[k].status;
+            r.tableState = res[k].table_state;
+            r.badPages = res[k].bad_pages;
+            r.firstBad = res[k].first_bad;
+            if (res[k].status) r.error = res[k].status == -ENOENT ? "vanished" : ErrText(res[k].status);
+        }
+        for (uint64_t q = 0; q < std::min(nbad, cap); q++) out[at[bad[q] >> 32]].badList.push_back((uint32_t)bad[q]);
         std::lock_guard<std::mutex> lk(mu_);
         for (auto& r : out) job->results.push_back(std::move(r));
+        // percent of ALL the listed chunk files, format errors included
         job->progress = (int32_t)(100 * job->results.size() / std::max<size_t>(1, names.size()));
     }
     std::lock_guard<std::mutex> lk(mu_);

@@ -6,7 +6,9 @@
 // forward each RPC to the method of the same name here.
 //
 // A job checks one copyset's data directory: its chunk files, in std::sort name
-// order, in batches of `batch` files, each batch one cc_integrity_check call
+// order (a file named as a chunk whose size is not metapage + chunk is reported
+// as CC_EFORMAT, FileFormatError in the reference), in batches of `batch`
+// files, each batch one cc_integrity_check call
 // (native pread into pinned staging, every data page rehashed on the GPU and
 // compared with the chunk's per-page CRC table under <copyset>/pcrc/).  Pause
 // and Cancel take effect at batch boundaries; a paused job resumes where it
@@ -42,7 +44,8 @@ enum INTEGRITY_OP_STATUS {  // proto/integrity.proto:45-48
 // Outcome of one chunk file (new; the proto carries only job-level fields).
 struct IntegrityFileResult {
     std::string name;
-    int32_t status = 0;        // 0, -errno (-ENOENT: the chunk vanished mid-job), CC_EINVAL, CC_ECORRUPT (metapage)
+    int32_t status = 0;        // 0, -errno (-ENOENT: the chunk vanished mid-job), CC_EINVAL, CC_ECORRUPT (metapage),
+                               // CC_EFORMAT (a chunk-named file whose size is not metapage + chunk)
     std::string error;         // text of a non-zero status ("vanished" for -ENOENT)
     uint32_t tableState = 0;   // CC_TABLE_*
     uint32_t badPages = 0;
@@ -75,6 +78,8 @@ struct IntegrityOptions {
 // <copyset>/data -> <copyset>/pcrc (outside the data directory: GetHash chains every file in it)
 std::string TableDirFor(const std::string& dataDir);
 std::string TablePath(const std::string& tableDir, const std::string& chunkName);
+// chunk_<id> or chunk_<id>_snap_<sn> (FileNameOperator, datastore/filename_operator.h:55-62)
+bool IsChunkFileName(const std::string& name);
 
 class IntegrityService {
  public:

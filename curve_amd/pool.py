@@ -121,6 +121,14 @@ class Comm:
                                                       _stream_handle(stream)), "cc_digest_allreduce_dev")
         return digest
 
+    def wait(self, stream=None, timeout_ms: int = 0):
+        """Bounded wait for the stream's work so far, the digest exchanges
+        included (cc_comm_wait): raises CurveCrcError(CC_ETIMEDOUT) -- the
+        communicator aborted -- when a peer stopped participating."""
+        from . import _lib
+        from .crc import _stream_handle
+        _lib.check(_lib.lib().cc_comm_wait(self._h, _stream_handle(stream), int(timeout_ms)), "cc_comm_wait")
+
     def close(self):
         from . import _lib
         if self._h:

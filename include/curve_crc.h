@@ -36,6 +36,8 @@ extern "C" {
 #define CC_EIO (-5001)    /* reading or writing a file failed (errno is kept where the call says so) */
 #define CC_ESTALE (-116)  /* a per-page CRC table no longer describes its chunk (sn / write generation) */
 #define CC_ETIMEDOUT (-110) /* a bounded wait expired (communicator init whose peers never joined) */
+#define CC_EFORMAT (-5002) /* a chunk file's size is not metapage + chunk (CSErrorCode::FileFormatError,
+                              chunkserver_chunkfile.cpp:233-238) */
 
 /* ------------------------------------------------------------------------
  * CPU primitive -- drop-in for the inline header src/common/crc32.h
@@ -88,6 +90,10 @@ typedef struct cc_opts {
 
 int cc_engine_init(const cc_opts* opts);  /* NULL = defaults */
 int cc_engine_fini(void);
+/* Free the device memory the engine caches per stream for the write log
+ * (cc_apply_log_dev's hash tables) on the calling thread's device; the next
+ * call re-creates what it needs.  Waits for the device to be idle first. */
+int cc_engine_trim(void);
 int cc_device_count(void);
 const char* cc_strerror(int code);
 const char* cc_version(void);
@@ -232,7 +238,12 @@ typedef struct cc_update {
  * takes one.  The hash table is the engine's, one per stream, created (and
  * grown) on the stream on first use and left clear by every call, so no call
  * clears it; calls sharing a stream are serialised by the engine while they
- * enqueue.  Contract per entry: 1 <= len <= max_len and
+ * enqueue.  Retained device memory: 8 B x the next power of two >= 8 x the
+ * pieces (n_updates x ((max_len - 1) / page_bytes + 2)) per stream, at most
+ * 64 MiB a stream (a log needing more takes a table for that call only), for
+ * at most 256 streams; the null stream, hipStreamLegacy and
+ * hipStreamPerThread count once per calling thread (one handle, a different
+ * stream in each thread).  cc_engine_trim releases them.  Contract per entry: 1 <= len <= max_len and
  * dst + len <= pool_bytes -- an entry that breaks it is skipped whole (never
  * half-applied); d_src must not alias d_pool.  page_bytes = 256 * 2^k
  * (k = 0..5).  d_work: >= cc_apply_log_work_bytes(n, max_len, page_bytes) bytes
@@ -378,6 +389,19 @@ int cc_comm_rank(const cc_comm* comm);
  * same order on every rank, from one stream at a time. */
 int cc_digest_allreduce_dev(cc_comm* comm, uint32_t* d_digest, uint64_t n, void* stream);
 
+/* Bounded wait for everything enqueued on `stream` so far -- the digest
+ * exchanges of cc_pool_scan_dev / cc_digest_allreduce_dev included -- with the
+ * communicator's health polled meanwhile (ncclCommGetAsyncError).  CC_OK once
+ * the stream has reached this point; if a peer stopped participating after
+ * init the collective never completes: after `timeout_ms` (0 =
+ * $CC_COMM_WAIT_TIMEOUT_MS, else 60 s) the communicator is aborted (its
+ * kernels released, the stream drains) and CC_ETIMEDOUT is returned; an RCCL
+ * async error aborts it at once with CC_ECOMM.  An aborted communicator
+ * answers CC_ECOMM to every later exchange; free it with cc_comm_abort.  The
+ * reference bounds its exchange the same way (FollowScanMap retry x timeout,
+ * chunk_closure.cpp:82-104).  Blocking (sleep-polls, never spins a core). */
+int cc_comm_wait(cc_comm* comm, void* stream, uint32_t timeout_ms);
+
 /* One rank's shard of the pool and the outputs of one scan pass over it. */
 typedef struct cc_pool_shard {
     const void* d_data;       /* n_chunks x chunk_bytes, chunk c's data at c*chunk_bytes */
@@ -435,14 +459,18 @@ typedef struct cc_pcrc_header {
     int64_t data_mtime_ns;  /* the chunk file's st_mtim then */
     uint64_t data_size;     /* the chunk file's size then */
     int64_t stamp_ns;       /* CLOCK_REALTIME when the CRCs' bytes were known current: a check's
-                               time just before it read the chunk, a store's call time */
+                               time just before it read the chunk; cc_pcrc_store_expect's
+                               expect->stamp_ns (or the mtime); cc_pcrc_store's call time */
 } cc_pcrc_header;
 
 /* Racy tables (git's "racily clean" index entries).  File mtimes come from a
  * coarse clock: a write landing in the same clock tick as data_mtime_ns leaves
  * the identity unchanged.  A table is trusted to condemn data only when that
  * cannot have happened after its CRCs were taken, i.e. when
- *     data_mtime_ns + tick <= stamp_ns     (tick = clock_getres(CLOCK_REALTIME_COARSE))
+ *     data_mtime_ns + tick < stamp_ns      (tick = clock_getres(CLOCK_REALTIME_COARSE);
+ *                                           1 s -- 2 s on an even second -- when the mtime
+ *                                           has no sub-second part: a filesystem keeping
+ *                                           whole seconds, or FAT's 2 s)
  * Otherwise it is RACY: its pages are still compared, a match re-stamps it
  * (the table is rewritten with a later stamp), and a mismatch is reported as
  * STALE -- refreshed by policy -- never as bad pages. */
@@ -470,7 +498,11 @@ int cc_pcrc_store(const char* chunk_path, uint32_t meta_bytes, const char* table
 /* The same, but only if the chunk's identity is still `expect` (its sn,
  * data_mtime_ns and data_size; the caller stats the file right after its
  * pwrite): CC_ESTALE and nothing written otherwise, so a store that runs after
- * a LATER write cannot pair the newer identity with the older CRCs. */
+ * a LATER write cannot pair the newer identity with the older CRCs.  The table
+ * is stamped with expect->stamp_ns -- the caller's CLOCK_REALTIME taken BEFORE
+ * its pwrite -- or, when that is 0, with data_mtime_ns (racy until a check
+ * re-stamps it); never with the store's own clock, which could clear a table
+ * whose chunk took a second same-size write within the mtime's tick. */
 int cc_pcrc_store_expect(const char* chunk_path, uint32_t meta_bytes, const char* table_path,
                          const uint32_t* page_crcs, uint32_t n_pages, uint32_t page_bytes,
                          const cc_pcrc_header* expect);

@@ -40,7 +40,7 @@ for mode, suf in (("full", ""), ("delta", "_delta")):
             c["hbm_read_bytes"] = c["FETCH_SIZE"] * 1024 * 2
         if "WRITE_SIZE" in c:
             c["hbm_write_bytes"] = c["WRITE_SIZE"] * 1024
-        if "pages" in k and "SQ_INSTS_VALU" in c:
+        if ("pages" in k or "quad" in k) and "SQ_INSTS_VALU" in c:
             for n in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
                 c[n + "_per_page"] = round(c[n] / pages, 1)
             c["wait_inst_frac_of_wave_cycles"] = round(c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"], 3)

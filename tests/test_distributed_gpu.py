@@ -159,3 +159,33 @@ def test_digest_fold_dev_any_rank_count(nranks):
         out = C.digest_fold_dev(torch.from_numpy(g.reshape(-1).view(np.int32)).to(dev), nranks)
         want = np.bitwise_xor.reduce(g, axis=0)
         assert (out.cpu().numpy().view(np.uint32) == want).all()
+
+
+def test_bench_rank_lost_after_init_ends_with_an_error_line(tmp_path):
+    """A peer that stops participating in the digest exchange AFTER init (the
+    bench's CC_INJECT_SKIP_EXCHANGE_RANK failpoint: rank 1 skips its exchange
+    every step) must end the N>1 bench with a JSON error line and a non-zero
+    exit within its bound -- not a hang until the driver's limit with no line.
+    Two gloo ranks on cuda:0 (RCCL refuses two ranks on one device, so the
+    ranks agree on the torch.distributed exchange, bounded by the group
+    timeout, BENCH_DIST_TIMEOUT_S; the native exchange's bound, cc_comm_wait,
+    is tested in test_pool_native.py)."""
+    import json
+    import subprocess
+    import sys
+    import time
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, BENCH_DIST_BACKEND="gloo", CC_INJECT_SKIP_EXCHANGE_RANK="1", BENCH_DIST_TIMEOUT_S="15")
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--chunks", "16", "--steps", "3",
+           "--warmup", "1", "--clock-warm-ms", "0", "--comm-timeout-ms", "5000", "--no-cpu-baseline", "--no-e2e",
+           "--no-pmc", "--updates", "0", "--reads", "0", "--wal-entries", "0", "--stream-chunks", "0",
+           "--file-chunks", "0"]
+    t0 = time.perf_counter()
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=240)
+    el = time.perf_counter() - t0
+    assert r.returncode != 0, r.stdout[-2000:]
+    errs = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{") and '"error"' in x]
+    assert errs and all(e["value"] is None and "digest exchange failed" in e["error"] for e in errs), r.stdout[-2000:]
+    assert el < 200, el  # the 15 s group timeout, rendezvous and two torch imports

@@ -868,6 +868,64 @@ def test_write_log_small_logs(dev, oracle, n, page_bytes, delta):
     assert (u32(crcs) == oracle.page_crcs(want, page_bytes)).all()
 
 
+def test_write_log_pseudo_streams_per_thread_and_trim(dev, oracle):
+    """the engine keys its per-stream state (the write log's hash
+    table, the page kernel's tail counters) by stream; the null stream and
+    hipStreamPerThread are ONE handle standing for a different real stream in
+    each thread, so they are keyed per calling thread.  Four threads apply
+    their own logs at the same time through those two handles (two threads
+    each); every page lands as in-order application with the oracle's CRC.
+    Then cc_engine_trim frees the cached tables and the next call rebuilds."""
+    import ctypes
+    import threading
+    from curve_amd import crc as C
+    from curve_amd import _lib
+    L = _lib.lib()
+    pb, per, n_thr, U = 4096, 4 << 20, 4, 3000
+    rng = np.random.default_rng(404)
+    host = rng.integers(0, 256, per * n_thr, dtype=np.uint8)
+    d_pool = to_dev(host, dev)
+    crcs = C.page_crc(d_pool, pb)
+    torch.cuda.synchronize()
+    src = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    d_src = to_dev(src, dev)
+    jobs = []
+    for t in range(n_thr):  # thread t writes only into its own 4 MiB
+        lens = rng.integers(1, 3 * pb, U).astype(np.uint32)
+        dst = (t * per + rng.integers(0, per - 3 * pb, U)).astype(np.uint64)
+        so = rng.integers(0, (1 << 20) - 3 * pb, U).astype(np.uint64)
+        rec = C.log_records(dst, so, lens)
+        need = int(L.cc_apply_log_work_bytes(U, 3 * pb, pb))
+        jobs.append((dst, so, lens, torch.from_numpy(rec.view(np.uint8)).to(dev),
+                     torch.empty(need, dtype=torch.uint8, device=dev)))
+    torch.cuda.synchronize()
+    errs = []
+
+    def run(t, handle):
+        _, _, _, d_log, work = jobs[t]
+        for _ in range(3):  # re-applying a log is idempotent
+            rc = L.cc_apply_log_dev(d_pool.data_ptr(), d_pool.numel(), pb, d_src.data_ptr(), d_log.data_ptr(), U,
+                                    3 * pb, crcs.data_ptr(), work.data_ptr(), work.numel(), ctypes.c_void_p(handle))
+            if rc:
+                errs.append((t, rc))
+
+    ths = [threading.Thread(target=run, args=(t, 2 if t % 2 else 0)) for t in range(n_thr)]
+    [x.start() for x in ths]
+    [x.join() for x in ths]
+    torch.cuda.synchronize()
+    assert not errs, errs
+    want = host.copy()
+    for dst, so, lens, _, _ in jobs:
+        for i in range(U):
+            want[dst[i]:dst[i] + lens[i]] = src[so[i]:so[i] + lens[i]]
+    assert (d_pool.cpu().numpy() == want).all()
+    assert (u32(crcs) == oracle.page_crcs(want, pb)).all()
+    assert L.cc_engine_trim() == 0
+    run(0, 0)  # tables rebuilt after the trim
+    torch.cuda.synchronize()
+    assert not errs and (u32(crcs) == oracle.page_crcs(want, pb)).all()
+
+
 @pytest.mark.parametrize("seed", range(40))
 def test_write_log_random_configs(dev, oracle, seed):
     """Randomised write logs across the geometry space -- page size 256 B..8 KiB,

@@ -116,8 +116,10 @@ def test_service_at_product_geometry(dev, oracle, tmp_path):
     cc_scan_files spans two staging batches (7 files a slot) -- with, in one
     job: bit rot in the LAST page (4095) of a chunk in the second batch, a
     stale table (a write that skipped it), a corrupt table, a chunk whose
-    metapage header fails its CRC and an unreadable chunk.  The per-file
-    failures are those files' results; the job still checks every chunk."""
+    metapage header fails its CRC and an unreadable chunk; then a truncated
+    and an extended chunk file (CC_EFORMAT, FileFormatError in the reference).
+    The per-file failures are those files' results; the job still checks
+    every chunk."""
     import time
     from curve_amd import _lib
     from curve_amd import integrity as I
@@ -179,6 +181,24 @@ def test_service_at_product_geometry(dev, oracle, tmp_path):
                 assert (tab == oracle.page_crcs(np.frombuffer(f.read()[meta:], dtype=np.uint8), pb)).all()
         if unreadable:
             os.chmod(paths[10], 0o644)
+        # a truncated and an extended chunk file (CSChunkFile::Open: FileFormatError,
+        # chunkserver_chunkfile.cpp:233-238): each is its own CC_EFORMAT result, the
+        # job still checks the rest, and progress counts them among the listed files
+        with open(paths[2], "r+b") as f:
+            f.truncate(meta + chunk - 4096)         # chunk_3: lost its last page
+        with open(paths[3], "ab") as f:
+            f.write(b"x" * 100)                     # chunk_4: 100 bytes too long
+        (d / "LOG").write_bytes(b"not a chunk")     # not chunk-named, wrong size: not listed
+        svc.ScheduleJob(3, 1, str(d))
+        j = svc.wait(3, 180)
+        assert j.state == I.IntegrityJobState.FINISHED and j.progress == 100, j.error
+        res = {r.name: r for r in j.results}
+        assert sorted(res) == names
+        for c in (3, 4):
+            assert (res[chunk_file_name(c)].status, res[chunk_file_name(c)].bad_pages) == (_lib.CC_EFORMAT, 0)
+        assert all(x.status == 0 and x.bad_pages == 0 for k, x in res.items()
+                   if k not in {chunk_file_name(c) for c in (3, 4, 5, 9)})
+        assert (res[chunk_file_name(9)].bad_pages, res[chunk_file_name(9)].bad_list) == (1, [4095])
         # a file that vanishes between a job's listing and its check: that file's -ENOENT
         got = I.check_files([paths[0], str(d / "chunk_999")],
                             [I.sidecar_path(paths[0]), I.sidecar_path(str(d / "chunk_999"))], chunk, meta, pb)

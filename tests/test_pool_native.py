@@ -31,6 +31,7 @@ def test_pool_scan_rejects_bad_arguments():
     assert L.cc_comm_init(ctypes.byref(h), 2, 2, ctypes.create_string_buffer(128), 128) == _lib.CC_EINVAL
     assert L.cc_comm_destroy(None) == _lib.CC_OK
     assert L.cc_comm_size(None) == 0 and L.cc_comm_rank(None) == -1
+    assert L.cc_comm_wait(None, None, 0) == _lib.CC_EINVAL
     assert L.cc_strerror(_lib.CC_ECOMM) == b"RCCL communication error"
 
 
@@ -136,3 +137,36 @@ def test_pool_scan_empty_shard_still_exchanges(dev):
         assert _lib.lib().cc_pool_scan_dev(ctypes.byref(s), comm.handle, stream) == _lib.CC_EINVAL
     finally:
         comm.close()
+
+
+@pytest.mark.gpu
+def test_comm_wait_bounds_an_exchange_stuck_after_init(dev, monkeypatch):
+    """cc_comm_wait: the bounded wait for a step's digest exchange.  A
+    collective whose peer stopped participating after init never completes; the
+    failpoint CC_INJECT_EXCHANGE_STALL_MS makes the exchange's stream sit that
+    long first, as such a collective would.  The wait returns CC_ETIMEDOUT at
+    its deadline (not the stall's end), the communicator is aborted -- later
+    exchanges answer CC_ECOMM, nothing is enqueued -- and the stream still
+    drains.  Without the stall the same wait returns CC_OK."""
+    import time
+    from curve_amd import _lib
+    from curve_amd.pool import Comm
+    comm = Comm(1, 0, Comm.unique_id())
+    x = torch.arange(64, dtype=torch.int32, device=dev)
+    comm.allreduce_digest(x)
+    comm.wait(timeout_ms=5000)
+    assert torch.equal(x, torch.arange(64, dtype=torch.int32, device=dev))
+    monkeypatch.setenv("CC_INJECT_EXCHANGE_STALL_MS", "4000")
+    try:
+        comm.allreduce_digest(x)
+        t0 = time.perf_counter()
+        with pytest.raises(_lib.CurveCrcError) as ei:
+            comm.wait(timeout_ms=500)
+        el = time.perf_counter() - t0
+        assert ei.value.code == _lib.CC_ETIMEDOUT and 0.45 < el < 3.0, (ei.value.code, el)
+        assert _lib.lib().cc_digest_allreduce_dev(comm.handle, x.data_ptr(), 64, None) == _lib.CC_ECOMM
+        assert _lib.lib().cc_comm_wait(comm.handle, None, 100) == _lib.CC_ECOMM
+        torch.cuda.synchronize()  # the stall ends; nothing of the aborted comm is left running
+    finally:
+        monkeypatch.delenv("CC_INJECT_EXCHANGE_STALL_MS")
+        comm.abort()

@@ -1,0 +1,28 @@
+"""The CPU parsers of untrusted bytes under hostile input:
+tests/native/parser_fuzz.cpp drives cc_pcrc_decode / cc_pcrc_load (the per-page
+CRC sidecar) and cc_chunk_meta_sn / cchost::ChunkFileMetaPage::decode (the chunk
+metapage, chunkserver_chunkfile.cpp:90-130) with every truncation, extensions,
+header bit flips, forged self-consistent headers and byte storms.  Here it runs
+as a plain build; scripts/sanitize.sh runs it (and host_test's CPU cases and
+this whole CPU suite) on ASan/UBSan builds.  No GPU."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_parser_fuzz_plain(tmp_path):
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("no g++")
+    lib = os.path.join(ROOT, "curve_amd")
+    exe = str(tmp_path / "parser_fuzz")
+    subprocess.run([cxx, "-O1", "-std=c++17", "-o", exe, os.path.join(ROOT, "tests", "native", "parser_fuzz.cpp"),
+                    os.path.join(ROOT, "curve_amd", "host", "libcurvehost.a"), f"-L{lib}", "-lcurvecrc",
+                    f"-Wl,-rpath,{lib}", "-lpthread"], check=True)
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "parser_fuzz: ok" in r.stdout
