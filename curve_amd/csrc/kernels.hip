@@ -1977,6 +1977,7 @@ __global__ __launch_bounds__(64 * kQuadWaves) void log_quad_kernel(LogLaunch a) 
         const uint32_t first = hb0 + (uint32_t)((uint64_t)Hb * wprefix(wave) / wsum);
         const uint32_t H = hb0 + (uint32_t)((uint64_t)Hb * wprefix(wave + 1) / wsum);
         const uint64_t pool = (uint64_t)(uintptr_t)a.pool;
+        const uint64_t dummy = (uint64_t)(uintptr_t)a.image + 4096ull * ((blockIdx.x * WV + wave) % (kLdsBytes / 4096));
         for (uint32_t base = first; base < H; base += 64u) {
             // metadata of up to 64 heads, lane k <- head base + k (clamped: every
             // lane holds a real page and piece, so any lane's values address memory)
@@ -2003,16 +2004,18 @@ __global__ __launch_bounds__(64 * kQuadWaves) void log_quad_kernel(LogLaunch a) 
                 // loads (their waits would hold the loads back)
                 __builtin_amdgcn_sched_barrier(0);
                 // a set past the batch (t >= nq) issues the same loads, all into
-                // pool page 0 (L2-resident after the first): nothing else is read
+                // 4 KiB of the device LDS image (L2-resident: the workgroups filled
+                // their LDS from it), a different 4 KiB per wave so no L2 line is
+                // a hot spot; it stores nothing
                 const bool live = t < nq;
                 const uint32_t h = (4u * t + g) & 63u;
                 Y.pg = live ? bperm(h, key) : 0u;
-                Y.rr = live ? bperm(h, hrr) : 0x10000000u;  // [0, 4096): every row whole from P
+                Y.rr = live ? bperm(h, hrr) : 0u;  // empty piece: every row from P, no edge needed
                 Y.sp = live ? (uint64_t)bperm(h, (uint32_t)hsp) | (uint64_t)bperm(h, (uint32_t)(hsp >> 32)) << 32
-                            : pool;
+                            : dummy;
                 Y.valid = live && ((singles >> h) & 1ull);
                 const QuadGeo q = quad_geo(Y.rr);
-                const uint64_t P = pool + (uint64_t)Y.pg * 4096u + 16u * i;
+                const uint64_t P = (live ? pool + (uint64_t)Y.pg * 4096u : dummy) + 16u * i;
                 const uint64_t S = Y.sp + 16u * i;
                 const uint32_t len = q.rhi - q.rlo, l15 = len >= 16u ? len - 15u : 0u;
                 const uint32_t x0 = 16u * i - q.rlo;  // wrapping: chunk i of row j is whole in the piece
