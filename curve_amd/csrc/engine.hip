@@ -261,10 +261,7 @@ inline uint32_t kconst_for(uint32_t page_bytes) { return ~shift_bytes(0xFFFFFFFF
 // largest power of two <= 64 that still gives every wave of the grid a tile.
 void geometry_for(const DevCtx* c, uint64_t n_pages, PageLaunch* a) {
     const uint64_t waves = (uint64_t)c->cus * kWavesPerBlock;
-#ifndef CC_MAX_TSHIFT
-#define CC_MAX_TSHIFT 6
-#endif
-    uint32_t ts = CC_MAX_TSHIFT;
+    uint32_t ts = 6;
     while (ts > 0 && (n_pages >> ts) < waves) ts--;
     const uint64_t tiles = (n_pages + (1ull << ts) - 1) >> ts;
     const uint64_t need = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -272,19 +269,19 @@ void geometry_for(const DevCtx* c, uint64_t n_pages, PageLaunch* a) {
     a->tile_shift = ts;
 }
 
-#ifndef CC_PAGE_DYN_DIV
-#define CC_PAGE_DYN_DIV 16  // 1/16 of a large launch's tiles form the dynamic tail (0: static only; A/B 2.464 ms vs 2.474-2.478 at 1/8, 2.474 at 1/12, 2.51 at 1/24 and 1/32)
-#endif
+// 1/16 of a large launch's tiles form the dynamic tail (A/B 2.464 ms vs
+// 2.474-2.478 at 1/8, 2.474 at 1/12, 2.51 at 1/24 and 1/32)
+constexpr uint64_t kPageDynDiv = 16;
 // Tile schedule of a page launch: geometry, and (true) a dynamic tail of the
-// last 1/CC_PAGE_DYN_DIV of the tiles when the batch is large and the page size
+// last 1/kPageDynDiv of the tiles when the batch is large and the page size
 // has a fixed-M instantiation.
 bool plan_tail(const DevCtx* c, PageLaunch& a) {
     geometry_for(c, a.n_pages, &a);
     const uint32_t m = a.words_per_lane;
     const uint64_t tiles = (a.n_pages + (1ull << a.tile_shift) - 1) >> a.tile_shift;
     const uint64_t waves = (uint64_t)a.blocks * kWavesPerBlock;
-    if (!CC_PAGE_DYN_DIV || m > 32 || (m & (m - 1)) || tiles < waves * 8) return false;
-    a.static_tiles = tiles - tiles / CC_PAGE_DYN_DIV;
+    if (m > 32 || (m & (m - 1)) || tiles < waves * 8) return false;
+    a.static_tiles = tiles - tiles / kPageDynDiv;
     return true;
 }
 
@@ -501,13 +498,6 @@ int cc_page_load_probe_dev(const void* d_pages, uint64_t n_pages, uint32_t* d_ou
     a.out = d_out;
     return map_err(launch_page_tail(c.get(), a, false, static_cast<hipStream_t>(stream), true));
 }
-
-#if CC_WAVE_TRACE
-int cc_debug_wave_trace(uint64_t* host) { return map_err(wave_trace_read(host)); }
-#endif
-#if CC_LOG_TRACE
-int cc_debug_log_trace(uint64_t* host) { return map_err(log_trace_read(host)); }
-#endif
 
 int cc_device_count(void) {
     int n = 0;
@@ -999,12 +989,11 @@ bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork
     if (!log_page_ok(page_bytes) || max_len == 0 || n_updates == 0) return false;
     w->n_pieces = n_updates * log_slots(max_len, page_bytes);
     if (w->n_pieces >= (1ull << 31)) return false;
-#ifndef CC_LOG_TABLE_FACTOR
-#define CC_LOG_TABLE_FACTOR 8  // table entries >= 8 x pieces (2 x -> 4 x: insert 15.8 -> 11.2 us; 8 x cost a 5 us memset until the engine-owned table needed none: round 3, 8 x -1.1 % a batch)
-#endif
-    // load <= 1 / factor, up to the 2^32 slots 32-bit slot indices reach; never above 1/4
+    // table entries >= 8 x pieces (2 x -> 4 x: insert 15.8 -> 11.2 us; 8 x cost a
+    // 5 us memset until the engine-owned table needed none: round 3, 8 x -1.1 % a
+    // batch): load <= 1/8, up to the 2^32 slots 32-bit slot indices reach; never above 1/4
     uint64_t te = 1024;
-    while (te < CC_LOG_TABLE_FACTOR * w->n_pieces && te < (1ull << 32)) te <<= 1;
+    while (te < 8 * w->n_pieces && te < (1ull << 32)) te <<= 1;
     if (te < 4 * w->n_pieces) return false;
     w->table_entries = te;
     w->next_off = 0;
@@ -1020,10 +1009,7 @@ bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork
 // when the log needs more than kLogTableCacheEntries slots (such a call takes a
 // table of its own, freed with it: one huge log must not pin device memory for
 // the rest of the process).  cc_engine_trim frees every cached table.
-#ifndef CC_LOG_TABLE_CACHE_ENTRIES
-#define CC_LOG_TABLE_CACHE_ENTRIES (1ull << 23)  // 64 MiB a stream: logs of up to 1M pieces (512K two-page writes)
-#endif
-constexpr uint64_t kLogTableCacheEntries = CC_LOG_TABLE_CACHE_ENTRIES;
+constexpr uint64_t kLogTableCacheEntries = 1ull << 23;  // 64 MiB a stream: logs of up to 1M pieces (512K two-page writes)
 DevCtx::LogTable* log_table(DevCtx* c, hipStream_t s, uint64_t entries, hipError_t* err) {
     *err = hipSuccess;
     if (entries > kLogTableCacheEntries) return nullptr;  // a log this big: a table for its call only
@@ -1098,10 +1084,8 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
     const uint64_t blocks = (lw.n_pieces + kLogWaves - 1) / kLogWaves;
     a.blocks = (int)(blocks < (uint64_t)c->cus ? (blocks ? blocks : 1) : (uint64_t)c->cus);
     hipError_t e;
-#ifndef CC_LOG_SMALL
-#define CC_LOG_SMALL 64  // logs of up to this many writes (each within one page's length) take the one-launch path
-#endif
-    if (n_updates <= (uint64_t)CC_LOG_SMALL && n_updates <= 64 && a.slots <= 2) return map_err(launch_log_small(a, s));
+    // logs of up to 64 writes (each within one page's length) take the one-launch path
+    if (n_updates <= 64 && a.slots <= 2) return map_err(launch_log_small(a, s));
     // (memset + insert + pages as ONE cooperative launch with two grid barriers
     // measured 0.221 vs 0.162 ms a batch: not kept)
     std::lock_guard<std::mutex> lk(c->log_mu);
@@ -1188,11 +1172,9 @@ int cc_verify_reads_dev(const void* d_pool, uint64_t pool_bytes, uint32_t page_b
     a.kconst = kconst_for(page_bytes);
     a.blocks = c->cus;  // every wave takes an equal share of the (device-computed) page slots
     hipError_t e;
-#ifndef CC_RV_SMALL
-#define CC_RV_SMALL 64  // batches of up to this many reads take the one-launch path
-#endif
-    // (page counts summed in 32 bits there: pools of < 2^26 pages keep 64 reads' sum exact)
-    if (n_reads <= (uint64_t)CC_RV_SMALL && n_reads <= 64 && pool_bytes / page_bytes < (1ull << 26))
+    // batches of up to 64 reads take the one-launch path (page counts summed in
+    // 32 bits there: pools of < 2^26 pages keep 64 reads' sum exact)
+    if (n_reads <= 64 && pool_bytes / page_bytes < (1ull << 26))
         return map_err(launch_read_verify_small(a, s));
     if ((e = launch_read_counts(a, s)) != hipSuccess) return map_err(e);
     if ((e = exclusive_scan_u64(temp, temp_bytes, a.counts, a.start, n_reads, s)) != hipSuccess)

@@ -13,15 +13,9 @@ constexpr uint32_t kLdsBytes = 163840;  // all 160 KiB of a CU's LDS
 constexpr uint32_t kFinBase = 131072;   // per-lane final-shift nibble tables [128K, 160K)
 constexpr uint32_t kWordsPerWaveStep = 64;  // one dword per lane per step
 constexpr uint32_t kWaveBytes = 256;        // bytes consumed per wave step
-#ifndef CC_WAVES
-#define CC_WAVES 8  // waves per CU (one workgroup per CU: the LDS image fills it); 8 beat 16 by 4-5 %
-#endif
-constexpr int kWavesPerBlock = CC_WAVES;
+constexpr int kWavesPerBlock = 8;  // waves per CU (one workgroup per CU: the LDS image fills it); 8 beat 16 by 4-5 %
 constexpr int kBlockThreads = 64 * kWavesPerBlock;
-#ifndef CC_PAGE_DYN_HEADS
-#define CC_PAGE_DYN_HEADS 8  // dynamic-tail counters of the page kernel: 1, or one per XCD (8)
-#endif
-constexpr uint32_t kDynHeads = CC_PAGE_DYN_HEADS;
+constexpr uint32_t kDynHeads = 8;  // dynamic-tail counters of the page kernel: one per XCD
 constexpr uint32_t kDynHeadStride = 16;  // 128 bytes between heads: one cache line each
 constexpr uint32_t kDynCtrBytes = kDynHeads * kDynHeadStride * 8;
 constexpr uint32_t kDynCtrWords64 = kDynHeads * kDynHeadStride;  // the heads as uint64 words
@@ -114,22 +108,13 @@ struct UpdateDesc {
 // pieces in log order in registers, stores the changed rows and rehashes it.
 // A page with more than 64 pieces is finished by its wave replaying the log.
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
-#ifndef CC_LOG_WAVES
-#define CC_LOG_WAVES 12  // waves per CU of the write-log page kernel at 8 KiB pages (A/B at 4 KiB, round 1: 12 beats 8 by ~6 %)
-#endif
-constexpr int kLogWaves = CC_LOG_WAVES;
-#ifndef CC_LOG_WAVES_FULL
-#define CC_LOG_WAVES_FULL 16  // full mode, pages <= 4 KiB: 103 VGPRs since the row offsets went into the offset field
-#endif
-#ifndef CC_LOG_WAVES_DELTA
-#define CC_LOG_WAVES_DELTA 16  // delta mode, pages <= 4 KiB: 120 VGPRs at 16 waves (was 12 waves: 129 would spill)
-#endif
+constexpr int kLogWaves = 12;  // waves per CU of the write-log page kernel at 8 KiB pages (A/B at 4 KiB, round 1: 12 beats 8 by ~6 %)
+constexpr int kLogWavesFull = 16;   // full mode, pages <= 4 KiB: 103 VGPRs since the row offsets went into the offset field
+constexpr int kLogWavesDelta = 16;  // delta mode, pages <= 4 KiB: 120 VGPRs at 16 waves (was 12 waves: 129 would spill)
 // waves per workgroup of log_pages_kernel<M, Delta>
-constexpr int log_waves(int m, bool delta) {
-    return m > 16 ? CC_LOG_WAVES : (delta ? CC_LOG_WAVES_DELTA : CC_LOG_WAVES_FULL);
-}
+constexpr int log_waves(int m, bool delta) { return m > 16 ? kLogWaves : (delta ? kLogWavesDelta : kLogWavesFull); }
 // waves per workgroup of log_small_kernel<M, Delta>
-constexpr int log_small_waves(int m, bool delta) { return (!delta && m <= 16) ? CC_LOG_WAVES_FULL : CC_LOG_WAVES; }
+constexpr int log_small_waves(int m, bool delta) { return (!delta && m <= 16) ? kLogWavesFull : kLogWaves; }
 struct LogLaunch {
     unsigned char* pool;
     uint64_t pool_bytes;
@@ -199,8 +184,6 @@ hipError_t launch_read_verify_small(const ReadVerifyLaunch& a, hipStream_t s);
 // tile_blocks: kRangeTiles + kDynCtrWords64 uint64 of stream-ordered scratch (the last: the
 // dynamic-tail chunk counter).
 constexpr uint32_t kRangeTiles = 1024;
-hipError_t wave_trace_read(uint64_t* host);  // CC_WAVE_TRACE builds only: [4][8192]
-hipError_t log_trace_read(uint64_t* host);   // CC_LOG_TRACE builds only: [6][4096]
 hipError_t launch_range_flat(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, uint64_t* tile_blocks,
                              const void* image, uint32_t* out, int blocks, hipStream_t s);
 // x^(-8t) mod P for t = 0..kXinvEntries-1 (undoing the zero pad after a range in its last 4 KiB block)

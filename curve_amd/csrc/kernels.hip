@@ -36,39 +36,6 @@ namespace {
 
 constexpr uint32_t kPolyDev = 0x82F63B78u;
 
-#ifndef CC_NT_LOADS
-#define CC_NT_LOADS 1
-#endif
-#ifndef CC_STORE
-#define CC_STORE 2  // 0 plain, 1 none (diagnostic), 2 nontemporal
-#endif
-#ifndef CC_ABLATE
-#define CC_ABLATE 0  // diagnostic builds only (wrong CRCs): 1 no G lookups, 2 no final map, 3 no loads
-#endif
-
-#ifndef CC_WAVE_TRACE
-#define CC_WAVE_TRACE 0  // diagnostic builds: per-wave start/end wall clock of the page and range kernels
-#endif
-#ifndef CC_LOG_TRACE
-#define CC_LOG_TRACE 0  // diagnostic builds: per-wave phase clocks of the write-log page kernel
-#endif
-#if CC_LOG_TRACE
-// wave w: start, LDS filled, first metadata batch in registers, end,
-// pages | several-piece pages << 16 | hw id << 32, clock after its 12th page
-__device__ uint64_t g_ltrace[6][4096];
-#endif
-#if CC_WAVE_TRACE
-__device__ uint64_t g_rtrace[4][8192];  // start, end, block, cu
-__device__ __forceinline__ void wave_trace(uint64_t w, uint64_t t_start) {
-    if ((threadIdx.x & 63u) == 0 && w < 8192) {
-        g_rtrace[0][w] = t_start;
-        g_rtrace[1][w] = __builtin_amdgcn_s_memrealtime();
-        g_rtrace[2][w] = blockIdx.x;
-        g_rtrace[3][w] = __smid();
-    }
-}
-#endif
-
 __device__ __forceinline__ uint32_t lds_u32(const uint32_t* tab, uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + byte_addr);
 }
@@ -94,9 +61,6 @@ __device__ __forceinline__ uint32_t apply_g_xor(const uint32_t* tab, uint32_t s,
 
 // Lane-specific final shift F^(64-l) via 8 nibble lookups.  cf = kFinBase + 4*lane.
 __device__ __forceinline__ uint32_t apply_fin(const uint32_t* tab, uint32_t s, uint32_t cf) {
-#if CC_ABLATE == 2
-    return s ^ cf;
-#endif
     uint32_t r = 0;
 #pragma unroll
     for (int n = 0; n < 8; n++) {
@@ -133,17 +97,8 @@ __device__ __forceinline__ void fill_lds(uint32_t* tab, const uint4* __restrict_
 template <int M>
 __device__ __forceinline__ void load_page(uint32_t (&w)[M], const uint32_t* __restrict__ p) {
 #pragma unroll
-    for (int j = 0; j < M; j++) {
-#if CC_ABLATE == 3
-        w[j] = (uint32_t)(uintptr_t)(p + 64 * j) * 0x9E3779B1u;  // no memory traffic: compute ceiling
-        continue;
-#endif
-#if CC_NT_LOADS
+    for (int j = 0; j < M; j++)
         w[j] = __builtin_nontemporal_load(p + 64 * j);  // read-once stream: nt (probe: +12 % read BW)
-#else
-        w[j] = p[64 * j];
-#endif
-    }
     // keep the whole page's loads ahead of the chain that follows (the
     // machine scheduler otherwise sinks them into it, shrinking the prefetch)
     __builtin_amdgcn_sched_barrier(0);
@@ -153,13 +108,7 @@ template <int M>
 __device__ __forceinline__ uint32_t chain(const uint32_t* tab, const uint32_t (&w)[M], uint32_t c0, uint32_t c1) {
     uint32_t s = w[0];
 #pragma unroll
-    for (int j = 1; j < M; j++) {
-#if CC_ABLATE == 1
-        s = ((s << 1) | (s >> 31)) ^ w[j];
-#else
-        s = apply_g_xor(tab, s, w[j], c0, c1);
-#endif
-    }
+    for (int j = 1; j < M; j++) s = apply_g_xor(tab, s, w[j], c0, c1);
     return s;
 }
 
@@ -188,15 +137,9 @@ __device__ __forceinline__ void flush_tile(uint32_t acc, uint64_t tile_first, ui
                                            uint32_t* __restrict__ out, const uint32_t* __restrict__ expected,
                                            const VerifySink& vs) {
     if (MODE != 1) {  // compute (0; 3 = the metapage pass) and the load-only probe (2) store the tile
-#if CC_STORE == 1  // diagnostic: no store (wrong output), keeps acc live
-        asm volatile("" ::"v"(acc));
-#elif CC_STORE == 2
         // nt: the CRC stream must not interleave cached partial-line writes with
         // the 16 GiB nt read stream (plain stores cost 3 % of HBM throughput)
         if (lane < cnt) __builtin_nontemporal_store(acc, out + tile_first + lane);
-#else
-        if (lane < cnt) out[tile_first + lane] = acc;
-#endif
     } else {
         const uint32_t want = lane < cnt ? __builtin_nontemporal_load(expected + tile_first + lane) : acc;
         const uint64_t bad = __ballot(want != acc);
@@ -215,12 +158,7 @@ __device__ __forceinline__ void flush_tile(uint32_t acc, uint64_t tile_first, ui
     }
 }
 
-#ifndef CC_PREFETCH
-#define CC_PREFETCH 2  // wave steps in flight ahead of the one being hashed (2..4 measured equal)
-#endif
-#ifndef CC_MAX_TSHIFT
-#define CC_MAX_TSHIFT 6
-#endif
+constexpr int kPrefetch = 2;  // wave steps in flight ahead of the one being hashed (2..4 measured equal)
 
 // Page sequence of one wave: its k-th page is wfirst + (k >> ts) * wstride + (k & tmask),
 // strictly increasing in k.
@@ -232,24 +170,16 @@ struct Walk {
     }
 };
 
-#ifndef CC_PAIR
-#define CC_PAIR 1  // pages hashed together per wave step (independent chains interleave)
-#endif
+constexpr int kPair = 1;  // pages hashed together per wave step (2 measured equal)
 
 template <int M, int P>
 __device__ __forceinline__ void load_pages(uint32_t (&w)[P][M], const uint32_t* __restrict__ base, const Walk& W,
                                            uint64_t k, uint64_t last) {
-#if CC_PRIO_LOADS
-    __builtin_amdgcn_s_setprio(2);
-#endif
 #pragma unroll
     for (int q = 0; q < P; q++) {
         const uint64_t pg = W.page(k + q);
         load_page<M>(w[q], base + (pg < last ? pg : last) * (64u * M));
     }
-#if CC_PRIO_LOADS
-    __builtin_amdgcn_s_setprio(0);
-#endif
 }
 
 // P independent Horner chains, interleaved step by step so each wave keeps
@@ -266,7 +196,7 @@ __device__ __forceinline__ void chains(const uint32_t* tab, const uint32_t (&w)[
     for (int j = 1; j < M; j++) {
 #pragma unroll
         for (int q = 0; q < P; q++) {
-            if (LOADS_ONLY || CC_ABLATE == 1)
+            if (LOADS_ONLY)
                 s[q] = ((s[q] << 1) | (s[q] >> 31)) ^ w[q][j];
             else
                 s[q] = apply_g_xor(tab, s[q], w[q][j], c0, c1);
@@ -276,18 +206,16 @@ __device__ __forceinline__ void chains(const uint32_t* tab, const uint32_t (&w)[
 
 // MODE 0: compute CRCs into out[]; MODE 1: verify against expected[].
 // Wave w walks tiles w, w+W, w+2W, ... (W = waves in the grid) of 2^ts pages,
-// P pages per step.  CC_PREFETCH+1 register buffers rotate so CC_PREFETCH
+// P pages per step.  kPrefetch+1 register buffers rotate so kPrefetch
 // steps' loads are in flight while the current step is hashed.  Loads are
 // unconditional (index clamped to the item's last page) so hipcc counts vmcnt
 // exactly.
 // Dynamic tail (dyn_ctr != null): the strided walk covers tiles [0, static_tiles)
-// only; the remaining tiles are handed out CC_PAGE_DYN_TILES at a time through
+// only; the remaining tiles are handed out kPageDynPages pages at a time through
 // the atomic counter *dyn_ctr (zeroed by the caller) to whichever waves finish
 // first.  Per-wave rates differ by XCD (a kernel trace shows odd XCDs ~10 %
 // slower on the same work), so a purely static split waits for the slowest.
-#ifndef CC_PAGE_DYN_PAGES
-#define CC_PAGE_DYN_PAGES 64  // pages per dynamic chunk (A/B: 64 beats 128)
-#endif
+constexpr uint64_t kPageDynPages = 64;  // pages per dynamic chunk (A/B: 64 beats 128)
 // Dynamic-tail heads (kernels.h kDynHeads): 1 = one counter for the whole grid;
 // 8 = one per XCD (MI355X_MICROARCH.md "dequeue": one word saturates at ~88
 // dequeues/us, shard above 64 pullers).  With 8 heads the tail's chunks are cut
@@ -373,16 +301,13 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if CC_WAVE_TRACE
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-#endif
     const uint32_t c0 = lane << 2 & 0x7Cu;
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
     const uint32_t* base = pages + lane;
     uint32_t* dst = out;
-    constexpr int D = CC_PREFETCH;
-    constexpr int P = (M <= 16) ? CC_PAIR : 1;  // register budget: P*(D+1)*M data VGPRs
+    constexpr int D = kPrefetch;
+    constexpr int P = (M <= 16) ? kPair : 1;  // register budget: P*(D+1)*M data VGPRs
     // item 0: the strided static walk over tiles [0, static_tiles); then dynamic chunks
     Walk W;
     W.tshift = tshift;
@@ -431,34 +356,31 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
             }
         }
         if (!dyn_ctr) break;
-        // next dynamic chunk: CC_PAGE_DYN_PAGES consecutive pages of the fused
+        // next dynamic chunk: kPageDynPages consecutive pages of the fused
         // metapages (the first chunk indices: pulled early, so the tail's last
         // chunks stay data chunks that even out as before), then of the data
         const uint64_t tail0 = static_tiles << tshift;
-        const uint64_t mchunks = (ex.n + CC_PAGE_DYN_PAGES - 1) / CC_PAGE_DYN_PAGES;
-        const uint64_t chunks = mchunks + (n_pages - tail0 + CC_PAGE_DYN_PAGES - 1) / CC_PAGE_DYN_PAGES;
+        const uint64_t mchunks = (ex.n + kPageDynPages - 1) / kPageDynPages;
+        const uint64_t chunks = mchunks + (n_pages - tail0 + kPageDynPages - 1) / kPageDynPages;
         const uint64_t chunk = tail_pull(dyn_ctr, chunks, dyn_head, dyn_tried, lane);
         if (chunk >= chunks) break;
         uint64_t p0, end;
         if (chunk >= mchunks) {
             base = pages + lane;
             dst = out;
-            p0 = tail0 + (chunk - mchunks) * CC_PAGE_DYN_PAGES;
+            p0 = tail0 + (chunk - mchunks) * kPageDynPages;
             end = n_pages;
         } else {
             base = ex.pages + lane;
             dst = ex.out;
-            p0 = chunk * CC_PAGE_DYN_PAGES;
+            p0 = chunk * kPageDynPages;
             end = ex.n;
         }
         W.wfirst = p0;
         W.wstride = 1ull << tshift;  // consecutive tiles: page(k) = p0 + k
-        lim = p0 + CC_PAGE_DYN_PAGES < end ? p0 + CC_PAGE_DYN_PAGES : end;
+        lim = p0 + kPageDynPages < end ? p0 + kPageDynPages : end;
     }
     if (dyn_ctr && ex.done) tail_reset(dyn_ctr, ex.done, lane);
-#if CC_WAVE_TRACE
-    wave_trace((uint64_t)blockIdx.x * kWavesPerBlock + wave, t_start);
-#endif
 }
 
 // Any M (page_bytes = 256*M): no register prefetch, dynamic chain length.
@@ -485,45 +407,11 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel_dyn(
     }
 }
 
-#ifndef CC_INSERT_ABLATE
-#define CC_INSERT_ABLATE 0  // timing ablations of log_insert_kernel (wrong results): 1 no CAS, 2 no head append
-#endif
-#ifndef CC_LOG_ABLATE
-#define CC_LOG_ABLATE 0  // timing ablations of log_pages_kernel (wrong results): 1 no stores, 2 no source loads, 3 no page loads, 4 no CRC chain, 5 no loads/stores of data
-#endif
-#ifndef CC_LOG_SKIP_COVERED
-#define CC_LOG_SKIP_COVERED 1  // full mode: do not read page rows the page's only piece overwrites whole
-#endif
-#ifndef CC_LOG_SRC_AUX
-#define CC_LOG_SRC_AUX 0  // cache policy bits of the write-log source loads
-#endif
-#ifndef CC_LOG_CRC_NT
-#define CC_LOG_CRC_NT 0  // nontemporal page-CRC stores in the write-log kernels
-#endif
-#ifndef CC_LOG_ROWSEL
-#define CC_LOG_ROWSEL 1  // full mode: one-piece pages through the per-row source/page select (merge_edges)
-#endif
-#ifndef CC_LOG_SKEW
-#define CC_LOG_SKEW 1  // write-log page kernel: heads cut among a workgroup's waves by SIMD age (weights below)
-#endif
-#ifndef CC_LOG_SKEW_W0
-#define CC_LOG_SKEW_W0 33  // A/B (profiles/write_log_skew_ab_r03.txt): 33/27/22/18 = 32/28/22/18 =
-#endif                     // 34/26/22/18 < 30/26/23/21 < 28/26/24/22 < 36/28/21/15 < equal
-#ifndef CC_LOG_SKEW_W1
-#define CC_LOG_SKEW_W1 27
-#endif
-#ifndef CC_LOG_SKEW_W2
-#define CC_LOG_SKEW_W2 22
-#endif
-#ifndef CC_LOG_SKEW_W3
-#define CC_LOG_SKEW_W3 18
-#endif
-#ifndef CC_LOG_ROW_AUX
-#define CC_LOG_ROW_AUX 2  // cache policy bits of the write-log row loads (full mode; 2 = nontemporal)
-#endif
-#ifndef CC_LOG_STORE_AUX
-#define CC_LOG_STORE_AUX 2  // cache policy bits of the write-log row stores (2 = nontemporal: -20 us a batch)
-#endif
+// cache policy bits (aux) of the write log's buffer instructions: 2 = nontemporal.
+// Row loads nt (A/B of 0-3 within 1 %); row stores nt (-20 us a batch); source
+// loads default (nt measured 6 % slower).
+constexpr int kLogRowAux = 2;
+constexpr int kLogStoreAux = 2;
 constexpr uint32_t kBufOOB = 0x80000000u;   // offset past num_records: load 0 / store dropped
 constexpr uint32_t kBufFlags = 0x00020000u;  // buffer resource dword 3 for gfx9-family (CDNA)
 // A per-row buffer offset is `sel + 256 j` with sel = (lane's dword wanted ?
@@ -531,13 +419,8 @@ constexpr uint32_t kBufFlags = 0x00020000u;  // buffer resource dword 3 for gfx9
 // of the select and keeps 2 x M loop-invariant row constants in VGPRs (32 at
 // 4 KiB pages); with sel opaque the 256 j goes into the instruction's 12-bit
 // offset field (kBufOOB + 256 j is still past num_records).
-#ifndef CC_ROW_OPAQUE
-#define CC_ROW_OPAQUE 1
-#endif
 __device__ __forceinline__ uint32_t row_sel(uint32_t v) {
-#if CC_ROW_OPAQUE
     asm("" : "+v"(v));
-#endif
     return v;
 }
 
@@ -725,32 +608,18 @@ __device__ __forceinline__ uint64_t wave_scan_incl(uint64_t v, uint32_t lane) {
     return v;
 }
 
-#ifndef CC_RANGE_ABLATE
-#define CC_RANGE_ABLATE 0  // timing ablations (wrong CRCs): 1 no per-range multiply, 2 no per-range finish
-#endif
-#ifndef CC_FLAT_WAVES
-#define CC_FLAT_WAVES 8  // waves per CU of the flat range kernel (A/B on WAL sizes: 8 beats 12 by ~4 %, 16 by ~10 %)
-#endif
-constexpr int kFlatWaves = CC_FLAT_WAVES;
-#ifndef CC_RANGE_ROUNDS
-#define CC_RANGE_ROUNDS 2  // static pieces per wave (A/B: 2 best; 1 loses on equal sizes, 8 on random)
-#endif
-#ifndef CC_RANGE_DYN_DIV
-#define CC_RANGE_DYN_DIV 32  // 1/32 of the blocks go to the dynamic tail (0: none; A/B: 1/8 and 1/16 lose to
-                             // the one counter's atomics, 1/64 leaves tail)
-#endif
-#ifndef CC_RANGE_HEADS
-#define CC_RANGE_HEADS 1  // tail heads (A/B round 3: 8 per-XCD heads = one counter at 1/32)
-#endif
-#ifndef CC_RANGE_DYN_BLOCKS
-#define CC_RANGE_DYN_BLOCKS 16  // blocks per dynamic chunk (A/B: 8 slower, 16 = 32)
-#endif
+constexpr int kFlatWaves = 8;  // waves per CU of the flat range kernel (A/B on WAL sizes: 8 beats 12 by ~4 %, 16 by ~10 %)
+constexpr uint32_t kRangeRounds = 2;  // static pieces per wave (A/B: 2 best; 1 loses on equal sizes, 8 on random)
+constexpr uint64_t kRangeDynDiv = 32;  // 1/32 of the blocks go to the dynamic tail (A/B: 1/8 and 1/16 lose to
+                                       // the one counter's atomics, 1/64 leaves tail)
+constexpr uint32_t kRangeHeads = 1;    // tail heads (A/B round 3: 8 per-XCD heads = one counter at 1/32)
+constexpr uint64_t kRangeDynBlocks = 16;  // blocks per dynamic chunk (A/B: 8 slower, 16 = 32)
 __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsigned char* __restrict__ buf,
                                                                    const RangeDesc* __restrict__ ranges, uint64_t n,
                                                                    uint64_t* __restrict__ tile_blocks,
                                                                    const uint4* __restrict__ image,
                                                                    uint32_t* __restrict__ out) {
-    constexpr uint32_t rounds = CC_RANGE_ROUNDS;
+    constexpr uint32_t rounds = kRangeRounds;
     __shared__ uint32_t tab[kLdsBytes / 4];
     fill_lds<64 * kFlatWaves>(tab, image);
     const uint32_t lane = threadIdx.x & 63u;
@@ -760,9 +629,6 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsig
     const uint32_t cf = kFinBase + (lane << 2);
     const uint64_t W = (uint64_t)gridDim.x * kFlatWaves;
     const uint64_t w = (uint64_t)blockIdx.x * kFlatWaves + wave;
-#if CC_WAVE_TRACE
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-#endif
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint4*>(image) + kLdsBytes / 16, 0, kXinvEntries * 128u, kBufFlags);
 
@@ -773,11 +639,11 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsig
     for (int j = 0; j < kTpl; j++) lsum += (tb[j] = tile_blocks[kTpl * lane + j]);
     const uint64_t cum = wave_scan_incl(lsum, lane);
     const uint64_t B = readlane64(cum, 63);
-    const uint64_t Bs = CC_RANGE_DYN_DIV ? B - B / CC_RANGE_DYN_DIV : B;  // statically dealt blocks
-    const uint64_t n_dyn = (B - Bs + CC_RANGE_DYN_BLOCKS - 1) / CC_RANGE_DYN_BLOCKS;
+    const uint64_t Bs = kRangeDynDiv ? B - B / kRangeDynDiv : B;  // statically dealt blocks
+    const uint64_t n_dyn = (B - Bs + kRangeDynBlocks - 1) / kRangeDynBlocks;
     unsigned long long* dyn_ctr = reinterpret_cast<unsigned long long*>(tile_blocks + kRangeTiles);
     uint32_t dyn_head, dyn_tried;
-    tail_cursor<CC_RANGE_HEADS>(dyn_head, dyn_tried);
+    tail_cursor<kRangeHeads>(dyn_head, dyn_tried);
 
     // work items: static pieces item < rounds, then dynamic chunks until the counter runs out
 #pragma unroll 1
@@ -789,10 +655,10 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsig
             b1 = Bs * (c + 1) / RW;
             if (b0 >= b1) continue;
         } else {
-            const uint64_t c = tail_pull<CC_RANGE_HEADS>(dyn_ctr, n_dyn, dyn_head, dyn_tried, lane);
+            const uint64_t c = tail_pull<kRangeHeads>(dyn_ctr, n_dyn, dyn_head, dyn_tried, lane);
             if (c >= n_dyn) break;
-            b0 = Bs + c * CC_RANGE_DYN_BLOCKS;
-            b1 = b0 + CC_RANGE_DYN_BLOCKS < B ? b0 + CC_RANGE_DYN_BLOCKS : B;
+            b0 = Bs + c * kRangeDynBlocks;
+            b1 = b0 + kRangeDynBlocks < B ? b0 + kRangeDynBlocks : B;
         }
         // tile holding block b0: lane tl's tiles, then the first of them whose running count passes b0
         const uint32_t tl = (uint32_t)__builtin_ctzll(__ballot(cum > b0));
@@ -906,14 +772,7 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsig
             for (int j = 1; j < 16; j++) s = apply_g_xor(tab, s, X[j], c0, c1);
             const bool end = kx + 1 == gx.nb;
             if (end || px.last) {
-#if CC_RANGE_ABLATE == 2
-                const uint32_t raw_pad = __builtin_amdgcn_readfirstlane(s);
-#else
                 const uint32_t raw_pad = wave_xor(apply_fin(tab, s, cf));
-#endif
-#if CC_RANGE_ABLATE
-                const uint32_t v = raw_pad ^ gx.nb;
-#else
                 // the item ends inside the range: shift over the range's bytes
                 // after this block; a range of < 4 bytes: its K(len) (no folded init)
                 const bool pw_needed = !end || gx.len < 4;
@@ -924,7 +783,6 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsig
                 const uint32_t bit = lane < 32u ? (raw_pad >> (31u - lane)) & 1u : 0u;
                 uint32_t v = end ? wave_xor(bit ? X[16] : 0u) : mulmod_small(pw, raw_pad);
                 if (end) v ^= gx.len >= 4 ? 0xFFFFFFFFu : ~mulmod_small(pw, 0xFFFFFFFFu);
-#endif
                 if (lane == 0) {
                     if (end && seg0)
                         out[px.r] = v;
@@ -948,9 +806,6 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsig
             step(Dq, pD, Cq, pC);
         }
     }
-#if CC_WAVE_TRACE
-    wave_trace(w, t_start);
-#endif
 }
 
 // Fast path: per_group = 64*q.  One wave per group, grid-stride over groups;
@@ -1111,10 +966,7 @@ __device__ __forceinline__ uint32_t page_hash(uint32_t page, uint32_t mask) {
     return (page * 2654435761u) & mask;  // Fibonacci hashing; sequential pages spread
 }
 
-#ifndef CC_INSERT_THREADS
-#define CC_INSERT_THREADS 1024
-#endif
-constexpr uint32_t kInsertThreads = CC_INSERT_THREADS;  // one head-list atomic per 1024 pieces (a per-wave atomic on the one
+constexpr uint32_t kInsertThreads = 1024;  // one head-list atomic per 1024 pieces (a per-wave atomic on the one
                                           // counter serialised 2048 waves: 26 of the kernel's 31 us)
 // Piece t of the log (t >= n_pieces: none) into the table.  Every thread of
 // the block calls it; `wcount` = LDS scratch of blockDim/64 + 1 words, free
@@ -1138,13 +990,6 @@ __device__ __forceinline__ void insert_piece(const LogLaunch& a, uint64_t t, uin
             // CAS first (one atomic for a page seen first, the common case);
             // next[] is only read by later kernels, so it can follow the CAS
             unsigned long long cur = 0ull;
-#if CC_INSERT_ABLATE == 1  // timing only (wrong grouping): a plain store instead of the CAS
-            tab[slot] = tag | (unsigned long long)(t + 1);
-            a.next[t] = kNoPiece;
-            fresh = true;
-            if (true) {
-            } else
-#endif
             for (;;) {
                 const unsigned long long old = atomicCAS(tab + slot, cur, tag | (unsigned long long)(t + 1));
                 if (old == cur) {  // claimed (cur == 0) or pushed onto the page's list
@@ -1162,10 +1007,6 @@ __device__ __forceinline__ void insert_piece(const LogLaunch& a, uint64_t t, uin
         }
     }
     const uint64_t m = __ballot(fresh);
-#if CC_INSERT_ABLATE == 2  // timing only: heads written at the table slot, no block aggregation or counter
-    if (fresh) a.heads[slot] = slot;
-    return;
-#endif
     if (lane == 0) wcount[wv] = (uint32_t)__popcll(m);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1265,7 +1106,7 @@ __device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint
     for (int j = 0; j < M; j++) {
         const bool full = pl.o + 256u * j < pl.l3;
         r.S[j] = __builtin_amdgcn_raw_buffer_load_b32(
-            rw, row_sel(full && CC_LOG_ABLATE != 2 && CC_LOG_ABLATE != 5 ? l4 : kBufOOB) + 256u * j, 0, CC_LOG_SRC_AUX);
+            rw, row_sel(full ? l4 : kBufOOB) + 256u * j, 0, 0);
     }
     uint32_t e[2];
     piece_edges(p, e);
@@ -1275,9 +1116,8 @@ __device__ __forceinline__ void fetch_piece(PieceSrc<M>& r, const Piece& p, uint
         const bool mine = e[k] != 0xffffffffu && lane == (e[k] & 63u);
         const uint32_t k0 = p.rlo > b ? p.rlo - b : 0u;
         const uint32_t k1 = p.rhi < b + 4 ? p.rhi - b : 4u;
-        r.ea[k] = __builtin_amdgcn_raw_buffer_load_b32(re, (mine && k0 < 4u - sh) ? b : kBufOOB, 0, CC_LOG_SRC_AUX);
-        r.eb[k] =
-            __builtin_amdgcn_raw_buffer_load_b32(re, (mine && sh && k1 > 4u - sh) ? b + 4 : kBufOOB, 0, CC_LOG_SRC_AUX);
+        r.ea[k] = __builtin_amdgcn_raw_buffer_load_b32(re, (mine && k0 < 4u - sh) ? b : kBufOOB, 0, 0);
+        r.eb[k] = __builtin_amdgcn_raw_buffer_load_b32(re, (mine && sh && k1 > 4u - sh) ? b + 4 : kBufOOB, 0, 0);
     }
 }
 
@@ -1351,7 +1191,7 @@ __device__ __forceinline__ void load_rows_sel(uint32_t (&w)[M], const unsigned c
 #pragma unroll
     for (int j = 0; j < M; j++)
         w[j] = __builtin_amdgcn_raw_buffer_load_b32(((cov >> j) & 1u) ? rs : rp, row_sel(4u * lane) + 256u * j, 0,
-                                                    CC_LOG_ROW_AUX);
+                                                    kLogRowAux);
 }
 
 template <int M>
@@ -1445,42 +1285,29 @@ __device__ __forceinline__ void load_rows(uint32_t (&w)[M], const unsigned char*
 template <int M, bool Delta>
 __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab) {
     constexpr int WV = log_waves(M, Delta);
-#if CC_LOG_SKEW
     // an equal share of the heads per workgroup: [hb0, hb1); a workgroup without
     // one (a small log) leaves before filling its 160 KiB of LDS
     const uint32_t Hall = *a.head_count;
     const uint32_t hb0 = (uint32_t)((uint64_t)Hall * blockIdx.x / gridDim.x);
     const uint32_t hb1 = (uint32_t)((uint64_t)Hall * (blockIdx.x + 1) / gridDim.x);
     if (hb0 >= hb1) return;
-#else
-    // a block whose waves own no head (a small log) leaves before filling its
-    // 160 KiB of LDS (uniform per block)
-    if ((uint64_t)blockIdx.x * WV >= *a.head_count) return;
-#endif
-#if CC_LOG_TRACE
-    const uint64_t tt0 = __builtin_amdgcn_s_memrealtime();
-#endif
     fill_lds<64 * WV>(tab, static_cast<const uint4*>(a.image));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if CC_LOG_TRACE
-    const uint64_t tt1 = __builtin_amdgcn_s_memrealtime();
-    uint64_t tt2 = 0, tpages = 0, tmid = 0;
-#endif
     const uint32_t c0 = lane << 2 & 0x7Cu;
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
-    const uint32_t* pages = reinterpret_cast<const uint32_t*>(a.pool) + lane;
     const uint32_t pb = a.page_bytes;
-#if CC_LOG_SKEW
     // The workgroup's heads are cut among its waves by age.  Its waves sit 4 to a
     // SIMD (wave t on SIMD t % 4, the (t / 4)-th oldest there) and the SIMD
     // issues oldest-first: with equal shares the four age groups ended at 80, 92,
     // 103 and 113 us (per-wave clocks, scripts/trace_log.py) and the workgroup
     // ran its last ~30 us with fewer waves than pages in flight.  Shares
     // weighted by age group (kSkew[t / 4]) end them within ~10 us of each other:
-    // -3 % a batch (a priority that rotates every step instead: -1.5 %).
-    constexpr uint32_t kSkew[4] = {CC_LOG_SKEW_W0, CC_LOG_SKEW_W1, CC_LOG_SKEW_W2, CC_LOG_SKEW_W3};
+    // -3 % a batch (a priority that rotates every step instead: -1.5 %).  A/B
+    // (profiles/write_log_skew_ab_r03.txt): 33/27/22/18 = 32/28/22/18 =
+    // 34/26/22/18 < 30/26/23/21 < 28/26/24/22 < 36/28/21/15 < equal.
+    constexpr uint32_t kSkew[4] = {33, 27, 22, 18};
     auto wprefix = [&](uint32_t t) {  // sum of the weights of waves 0 .. t-1
         uint32_t p = 0;
         for (uint32_t u = 0; u < t; u++) p += kSkew[(u / 4) & 3];
@@ -1490,11 +1317,6 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
     const uint32_t H = hb0 + (uint32_t)((uint64_t)Hb * wprefix(wave + 1) / wsum);  // this wave: [first, H)
     const uint32_t first = hb0 + (uint32_t)((uint64_t)Hb * wprefix(wave) / wsum);
     constexpr uint32_t W = 1;  // lane k <- head base + k
-#else
-    const uint32_t H = *a.head_count;
-    const uint32_t W = gridDim.x * WV;
-    const uint32_t first = blockIdx.x * WV + wave;
-#endif
     // static shares only: a dynamic tail (the last 1/8 or 1/16 of the heads in
     // chunks of 4-16 through one atomic counter, as the page kernel does) measured
     // 7-19 % slower here (0.177-0.197 vs 0.165 ms a batch)
@@ -1519,18 +1341,13 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         const uint32_t u1 = single ? 0u : nxt / a.slots;  // several pieces: the second one's update
         const uint64_t singles = __ballot(single);
         const uint32_t cnt = (uint32_t)__popcll(__ballot(hv));  // valid lanes are 0 .. cnt-1
-#if CC_LOG_TRACE
-        asm volatile("" ::"v"(u1), "v"(hsp));  // the metadata has arrived
-        if (!tt2) tt2 = __builtin_amdgcn_s_memrealtime();
-        tpages += cnt | (uint64_t)__popcll(~singles & __ballot(hv)) << 16;
-#endif
         // two pages in flight: k (being merged + hashed) and k+1.  (A third
         // bought nothing, round 3: 0.1488 vs 0.1454 ms in a timing ablation.  A
         // page iteration issues ~39 VMEM instructions in full mode -- 16 row
         // loads, 6 edge loads, 16 row stores, the CRC -- and ~53 on the generic
         // path; gfx950's 6-bit vmcnt counts at most 63 outstanding.)
         uint32_t A[M], B[M];
-        constexpr bool kRowSel = CC_LOG_ROWSEL && !Delta && CC_LOG_ABLATE == 0;
+        constexpr bool kRowSel = !Delta;  // full mode: one-piece pages through the per-row source/page select
         using Src = typename std::conditional<kRowSel, PieceEdges, PieceSrc<M>>::type;
         Src S0, S1;
         auto fetch = [&](Src& r, const Piece& p) {
@@ -1558,29 +1375,15 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
                 uint32_t vz = 0;
                 asm volatile("" : "+v"(vz));
                 ocy = a.page_crcs[pgy + vz];
-            } else if constexpr (kRowSel) {
+            } else {
                 // rows the page's only piece covers whole come straight from the source
                 load_rows_sel<M>(Y, a.pool + (uint64_t)pgy * pb, py.sp, ((singles >> h) & 1ull) ? covered_rows(py) : 0u,
                                  lane);
-            } else if constexpr (CC_LOG_ABLATE == 3 || CC_LOG_ABLATE == 5) {
-                load_rows<M>(Y, a.pool + (uint64_t)pgy * pb, 0u, lane);  // timing ablation: no page reads
-            } else if constexpr (CC_LOG_SKIP_COVERED) {
-                // rows the page's only piece covers whole come from the source:
-                // not read (out-of-range offset, no memory traffic)
-                const uint32_t f0 = (py.rlo + 255u) >> 8, f1 = py.rhi >> 8;  // whole rows [f0, f1)
-                const uint32_t full =
-                    f1 > f0 ? ((f1 >= 32u ? 0xFFFFFFFFu : (1u << f1) - 1u) & ~((1u << f0) - 1u)) : 0u;
-                load_rows<M>(Y, a.pool + (uint64_t)pgy * pb, ((singles >> h) & 1ull) ? ~full : 0xFFFFFFFFu, lane);
-            } else {
-                load_page<M>(Y, pages + (uint64_t)pgy * (64u * M));
             }
         };
         auto step = [&](uint32_t (&X)[M], Src& SX, const Piece& px, uint32_t pg, uint32_t hh, uint32_t ocx,
                         uint32_t (&Y)[M], Src& SY, Piece& py, uint32_t& pgy, uint32_t& ocy) {
             const bool more = hh + 1 < cnt;
-#if CC_LOG_TRACE
-            if (hh == 12) tmid = __builtin_amdgcn_s_memrealtime();
-#endif
             // next page + its first piece's source bytes in flight (clamped to the
             // last page: a harmless re-read, so every step issues the same loads
             // and the vmcnt waits stay exact)
@@ -1677,30 +1480,17 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
                 for (int j = 0; j < M; j++)
                     __builtin_amdgcn_raw_buffer_store_b32(
                         X[j], rp,
-                        row_sel(((dirty >> j) & 1u) && CC_LOG_ABLATE != 1 && CC_LOG_ABLATE != 5 ? 4u * lane : kBufOOB) +
-                            256u * j,
-                        0, CC_LOG_STORE_AUX);
+                        row_sel(((dirty >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j, 0, kLogStoreAux);
             }
             uint32_t crc;
             if constexpr (Delta) {
 #pragma unroll
                 for (int j = 0; j < M; j++) O[j] ^= X[j];  // old ^ new: 0 outside the changed bytes
                 crc = wave_xor(apply_fin(tab, chain<M>(tab, O, c0, c1), cf)) ^ ocx;
-            } else if constexpr (CC_LOG_ABLATE == 4) {
-                uint32_t x = 0;  // timing ablation: no chain
-#pragma unroll
-                for (int j = 0; j < M; j++) x ^= X[j];
-                crc = wave_xor(x);
             } else {
                 crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
             }
-            if (lane == 0) {
-#if CC_LOG_CRC_NT
-                __builtin_nontemporal_store(crc, a.page_crcs + pg);
-#else
-                a.page_crcs[pg] = crc;
-#endif
-            }
+            if (lane == 0) a.page_crcs[pg] = crc;
             return more;
         };
         // the two register sets alternate (no copies): page k in one while page
@@ -1715,17 +1505,6 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
             if (!step(B, S1, pB, pgB, h + 1, ocB, A, S0, pA, pgA, ocA)) break;
         }
     }
-#if CC_LOG_TRACE
-    const uint32_t wv = blockIdx.x * WV + wave;
-    if (lane == 0 && wv < 4096) {
-        g_ltrace[0][wv] = tt0;
-        g_ltrace[1][wv] = tt1;
-        g_ltrace[2][wv] = tt2;
-        g_ltrace[3][wv] = __builtin_amdgcn_s_memrealtime();
-        g_ltrace[4][wv] = tpages | (uint64_t)__smid() << 32;
-        g_ltrace[5][wv] = tmid;
-    }
-#endif
 }
 
 template <int M, bool Delta>
@@ -1856,7 +1635,7 @@ __device__ __forceinline__ void log_page_multi(const LogLaunch& a, const uint32_
 #pragma unroll
     for (int j = 0; j < M; j++)
         __builtin_amdgcn_raw_buffer_store_b32(X[j], rp, row_sel(((dirty >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j,
-                                              0, CC_LOG_STORE_AUX);
+                                              0, kLogStoreAux);
     uint32_t crc;
     if constexpr (Delta) {
 #pragma unroll
@@ -2258,25 +2037,12 @@ __global__ void read_counts_kernel(ReadVerifyLaunch a) {
 // stored CRCs come in with VECTOR loads (an opaque zero in the address) so
 // they never share lgkmcnt with the chain's LDS lookups.  A mismatch is
 // counted on its read (rare: atomics).
-#ifndef CC_RV_WAVES
-#define CC_RV_WAVES 8  // waves per CU of the verify-on-read kernel
-#endif
-constexpr int kRvWaves = CC_RV_WAVES;
-#ifndef CC_RV_DYN_DIV
-#define CC_RV_DYN_DIV 16  // 1/16 of the slots form the dynamic tail (A/B: 2-3 % over none; 1/8, 1/32 less)
-#endif
-#ifndef CC_RV_HEADS
-#define CC_RV_HEADS 1  // tail heads (A/B round 3: 8 per-XCD heads = one counter at 1/16)
-#endif
-#ifndef CC_RV_DYN_SLOTS
-#define CC_RV_DYN_SLOTS 32  // slots (pages) per dynamic chunk (64: -1 %, 128: -5 %, 256: -18 % -- too coarse)
-#endif
-#ifndef CC_RV_MIN_SLOTS
-#define CC_RV_MIN_SLOTS 8  // a small batch goes to the fewest waves that give each >= 8 page slots
-#endif
-#ifndef CC_RV_SMALL_MIN_SLOTS
-#define CC_RV_SMALL_MIN_SLOTS 2  // the one-launch path (<= 64 reads): >= 2 pages per wave
-#endif
+constexpr int kRvWaves = 8;  // waves per CU of the verify-on-read kernel
+constexpr uint64_t kRvDynDiv = 16;  // 1/16 of the slots form the dynamic tail (A/B: 2-3 % over none; 1/8, 1/32 less)
+constexpr uint32_t kRvHeads = 1;  // tail heads (A/B round 3: 8 per-XCD heads = one counter at 1/16)
+constexpr uint64_t kRvDynSlots = 32;  // slots (pages) per dynamic chunk (64: -1 %, 128: -5 %, 256: -18 % -- too coarse)
+constexpr uint64_t kRvMinSlots = 8;  // a small batch goes to the fewest waves that give each >= 8 page slots
+constexpr uint32_t kRvSmallMinSlots = 2;  // the one-launch path (<= 64 reads): >= 2 pages per wave
 template <int M>
 __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLaunch a) {
     __shared__ uint32_t tab[kLdsBytes / 4];
@@ -2284,7 +2050,7 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
     const uint64_t T = a.start[n - 1] + a.counts[n - 1];
     // W waves share the slots: all of the grid for a large batch, fewer for a
     // small one, and the blocks left without a share exit before filling LDS
-    const uint64_t Wg = (uint64_t)gridDim.x * kRvWaves, Wt = (T + CC_RV_MIN_SLOTS - 1) / CC_RV_MIN_SLOTS;
+    const uint64_t Wg = (uint64_t)gridDim.x * kRvWaves, Wt = (T + kRvMinSlots - 1) / kRvMinSlots;
     const uint64_t W = Wt < Wg ? (Wt ? Wt : 1) : Wg;
     if ((uint64_t)blockIdx.x * kRvWaves >= W) return;  // uniform per block
     fill_lds<64 * kRvWaves>(tab, static_cast<const uint4*>(a.image));
@@ -2318,11 +2084,11 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
         return lo;
     };
     auto stored_crc = [&](uint64_t g) { return a.page_crcs[g + vz]; };
-    // static shares of the first Ts slots, then dynamic chunks of CC_RV_DYN_SLOTS
+    // static shares of the first Ts slots, then dynamic chunks of kRvDynSlots
     // slots (the page kernel's tail: the XCDs run at different rates)
-    const uint64_t Ts = T - T / CC_RV_DYN_DIV;
+    const uint64_t Ts = T - T / kRvDynDiv;
     uint32_t dyn_head, dyn_tried;
-    tail_cursor<CC_RV_HEADS>(dyn_head, dyn_tried);
+    tail_cursor<kRvHeads>(dyn_head, dyn_tried);
     uint64_t lo_slot = w < W ? Ts * w / W : Ts, hi_slot = w < W ? Ts * (w + 1) / W : Ts;  // waves past W: tail only
 #pragma unroll 1
     for (;;) {
@@ -2382,11 +2148,11 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
                 if (!step(Cq, sC, oC, k + 2, B, gB, sB, oB)) break;
             }
         }
-        const uint64_t n_dyn = (T - Ts + CC_RV_DYN_SLOTS - 1) / CC_RV_DYN_SLOTS;
-        const uint64_t c = tail_pull<CC_RV_HEADS>(a.dyn_ctr, n_dyn, dyn_head, dyn_tried, lane);
+        const uint64_t n_dyn = (T - Ts + kRvDynSlots - 1) / kRvDynSlots;
+        const uint64_t c = tail_pull<kRvHeads>(a.dyn_ctr, n_dyn, dyn_head, dyn_tried, lane);
         if (c >= n_dyn) break;
-        lo_slot = Ts + c * CC_RV_DYN_SLOTS;
-        hi_slot = lo_slot + CC_RV_DYN_SLOTS < T ? lo_slot + CC_RV_DYN_SLOTS : T;
+        lo_slot = Ts + c * kRvDynSlots;
+        hi_slot = lo_slot + kRvDynSlots < T ? lo_slot + kRvDynSlots : T;
     }
 }
 
@@ -2395,7 +2161,7 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
 // latency of the read path: no count kernel and no scan.  Every wave loads the
 // batch's descriptors, computes the pages per read (a read past the pool is
 // marked as read_counts_kernel marks it) and their wave prefix sum; the P pages
-// are split evenly over the fewest waves that give each >= CC_RV_MIN_SLOTS, at
+// are split evenly over the fewest waves that give each >= kRvMinSlots, at
 // PAGE granularity (a 32-page read is verified by 4 waves), and the blocks left
 // without pages exit before filling LDS.
 template <int M>
@@ -2419,7 +2185,7 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_small_kernel(ReadVe
         if (lane >= (uint32_t)d) cum += o;
     }
     const uint32_t P = __builtin_amdgcn_readlane(cum, 63);
-    const uint32_t Wg = gridDim.x * kRvWaves, Wt = (P + CC_RV_SMALL_MIN_SLOTS - 1) / CC_RV_SMALL_MIN_SLOTS;
+    const uint32_t Wg = gridDim.x * kRvWaves, Wt = (P + kRvSmallMinSlots - 1) / kRvSmallMinSlots;
     const uint32_t W = Wt < Wg ? Wt : Wg;
     if (blockIdx.x * (uint32_t)kRvWaves >= W) return;  // uniform per block (P == 0: every block)
     fill_lds<64 * kRvWaves>(tab, static_cast<const uint4*>(a.image));
@@ -2595,12 +2361,6 @@ hipError_t launch_fold(const FoldLaunch& a, hipStream_t s) {
 }
 
 
-#if CC_LOG_TRACE
-hipError_t log_trace_read(uint64_t* host) { return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ltrace), sizeof(g_ltrace)); }
-#endif
-#if CC_WAVE_TRACE
-hipError_t wave_trace_read(uint64_t* host) { return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rtrace), sizeof(g_rtrace)); }
-#endif
 
 hipError_t launch_range_flat(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, uint64_t* tile_blocks,
                              const void* image, uint32_t* out, int blocks, hipStream_t s) {
