@@ -74,7 +74,6 @@ struct Staging {
     void* dev[2] = {nullptr, nullptr};
     uint32_t* dcrc[2] = {nullptr, nullptr};
     uint32_t* hcrc[2] = {nullptr, nullptr};
-    uint64_t* tiles[2] = {nullptr, nullptr};  // range batches: per-tile block counts (kRangeTiles)
     hipStream_t stream[2] = {nullptr, nullptr};
     hipEvent_t done[2] = {nullptr, nullptr};
     SlotSignal sig[2];
@@ -134,6 +133,18 @@ struct DevCtx {
     };
     std::mutex log_mu;
     std::vector<LogTable> log_tabs;
+    // the range kernel's scratch, one per stream (range_work): tile words, the
+    // tail block and the split-range accumulators; range_mu is held over a
+    // call's enqueue so the epoch order is the stream order
+    struct RangeWork {
+        StreamKey s;
+        unsigned char* p;
+        uint64_t cap;    // accumulator pairs (ranges a call may have)
+        uint32_t epoch;  // the last call's
+        bool dirty;
+    };
+    std::mutex range_mu;
+    std::vector<RangeWork> range_works;
     DevCtx() {
         for (int i = 0; i < kEpiSlots; i++) {
             epi_key[i].store(0);
@@ -166,8 +177,6 @@ void staging_free(Staging& st) {
         if (st.dev[i]) hipFree(st.dev[i]);
         if (st.dcrc[i]) hipFree(st.dcrc[i]);
         if (st.hcrc[i]) hipHostFree(st.hcrc[i]);
-        if (st.tiles[i]) hipFree(st.tiles[i]);
-        st.tiles[i] = nullptr;
         if (st.stream[i]) hipStreamDestroy(st.stream[i]);
         if (st.done[i]) hipEventDestroy(st.done[i]);
         st.host[i] = st.dev[i] = nullptr;
@@ -199,6 +208,7 @@ DevCtx::~DevCtx() {
             if (void* p = epi_ptr[i].load()) hipFree(p);
         for (auto& t : tails) hipFree(t.second);
         for (auto& t : log_tabs) (void)hipFreeAsync(t.p, nullptr);
+        for (auto& t : range_works) (void)hipFreeAsync(t.p, nullptr);
         (void)hipDeviceSynchronize();
     }
     if (cur >= 0) (void)hipSetDevice(cur);
@@ -346,8 +356,6 @@ int staging_init(DevCtx* c) {
         if ((e = hipMalloc(&st.dev[i], per)) != hipSuccess) return map_err(e);
         if ((e = hipMalloc(&st.dcrc[i], per / 256 * 4)) != hipSuccess) return map_err(e);
         if ((e = hipHostMalloc(&st.hcrc[i], per / 256 * 4, hipHostMallocDefault)) != hipSuccess) return map_err(e);
-        if ((e = hipMalloc(&st.tiles[i], (kRangeTiles + kDynCtrWords64) * sizeof(uint64_t))) != hipSuccess)
-            return map_err(e);
         if ((e = hipStreamCreateWithFlags(&st.stream[i], hipStreamNonBlocking)) != hipSuccess) return map_err(e);
         if ((e = hipEventCreateWithFlags(&st.done[i], hipEventDisableTiming)) != hipSuccess) return map_err(e);
     }
@@ -539,11 +547,15 @@ int cc_engine_trim(void) {
     int rc = get_ctx(&c);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(c->log_mu);  // no write-log call enqueues meanwhile
+    std::lock_guard<std::mutex> lr(c->range_mu);  // nor a range call
     const hipError_t e = hipDeviceSynchronize();  // kernels of earlier calls may still use a table
     if (e != hipSuccess) return map_err(e);
     for (auto& t : c->log_tabs)
         if (t.p) (void)hipFree(t.p);
     c->log_tabs.clear();
+    for (auto& t : c->range_works)
+        if (t.p) (void)hipFree(t.p);
+    c->range_works.clear();
     return CC_OK;
 }
 
@@ -676,22 +688,103 @@ int cc_shift_dev(const uint32_t* d_crcs, const uint64_t* d_shift_bytes, uint64_t
     return map_err(launch_shift(d_crcs, d_shift_bytes, n, d_out, static_cast<hipStream_t>(stream)));
 }
 
+namespace {
+// The stream's range scratch: kRangeTiles tile words, the tail block, then the
+// accumulator pairs of up to `cap` ranges; zero when created (cleared on the
+// stream), kept so by every launch (kernels.h RangeLaunch).  A call with more
+// ranges than kRangeCacheRanges, or past kMaxTailBlocks streams, gets scratch
+// of its own for the call (nullptr here).  Caller holds c->range_mu.
+constexpr uint64_t kRangeHeader = (kRangeTiles * 8 + kTailBlockBytes + 255) & ~255ull;
+constexpr uint64_t kRangeCacheRanges = 1ull << 22;  // 32 MiB of accumulators a stream at most
+DevCtx::RangeWork* range_work(DevCtx* c, hipStream_t s, uint64_t n, hipError_t* err) {
+    *err = hipSuccess;
+    if (n > kRangeCacheRanges) return nullptr;
+    const StreamKey key = stream_key(s);
+    DevCtx::RangeWork* t = nullptr;
+    for (auto& x : c->range_works)
+        if (x.s == key) t = &x;
+    if (t && t->cap < n) {
+        if ((*err = hipFreeAsync(t->p, s)) != hipSuccess) return nullptr;
+        t->p = nullptr;
+        t->cap = 0;
+    }
+    if (!t) {
+        if (c->range_works.size() >= kMaxTailBlocks) return nullptr;
+        c->range_works.push_back({key, nullptr, 0, 0, false});
+        t = &c->range_works.back();
+    }
+    if (!t->p) {
+        uint64_t cap = 1ull << 16;
+        while (cap < n) cap <<= 1;
+        void* p = nullptr;
+        if ((*err = hipMallocAsync(&p, kRangeHeader + cap * 8, s)) != hipSuccess) return nullptr;
+        t->p = static_cast<unsigned char*>(p);
+        t->cap = cap;
+        t->dirty = true;
+    }
+    if (t->dirty) {
+        if ((*err = hipMemsetAsync(t->p, 0, kRangeHeader + t->cap * 8, s)) != hipSuccess) return nullptr;
+        t->dirty = false;
+    }
+    return t;
+}
+
+// One range batch (the flat kernel, kernels.h launch_range_flat) on stream s.
+hipError_t range_batch(DevCtx* c, const unsigned char* buf, const RangeDesc* rd, uint64_t n, uint32_t* out,
+                       hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    RangeLaunch a = {};
+    a.buf = buf;
+    a.ranges = rd;
+    a.n = n;
+    a.image = c->image;
+    a.out = out;
+    a.blocks = c->cus;
+    std::lock_guard<std::mutex> lk(c->range_mu);
+    hipError_t e;
+    DevCtx::RangeWork* w = range_work(c, s, n, &e);
+    if (e != hipSuccess) return e;
+    unsigned char* base = nullptr;
+    unsigned char* tmp = nullptr;
+    if (w) {
+        base = w->p;
+        // 24-bit epochs; the wrap keeps the parity alternating (2^24 - 1 is odd:
+        // next 2), as the tail's counter slots need
+        w->epoch = w->epoch + 1 < (1u << 24) ? w->epoch + 1 : 2u;
+        a.epoch = w->epoch;
+    } else {  // scratch of this call's own, cleared
+        const uint64_t bytes = kRangeHeader + n * 8;
+        if ((e = hipMallocAsync(reinterpret_cast<void**>(&tmp), bytes, s)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(tmp, 0, bytes, s)) != hipSuccess) {
+            (void)hipFreeAsync(tmp, s);
+            return e;
+        }
+        base = tmp;
+        a.epoch = 1;
+    }
+    a.tiles = reinterpret_cast<uint64_t*>(base);
+    a.tail = reinterpret_cast<unsigned long long*>(base + kRangeTiles * 8);
+    a.acc = reinterpret_cast<uint32_t*>(base + kRangeHeader);
+    e = launch_range_flat(a, s);
+    if (w && e != hipSuccess) w->dirty = true;  // may have run in part: clear before the next use
+    if (tmp) {
+        const hipError_t f = hipFreeAsync(tmp, s);
+        if (e == hipSuccess) e = f;
+    }
+    return e;
+}
+}  // namespace
+
 int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, uint32_t* d_out, void* stream) {
     if (n == 0) return CC_OK;
     if (!d_buf || !d_ranges || !d_out) return CC_EINVAL;
     CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    const RangeDesc* rd = reinterpret_cast<const RangeDesc*>(d_ranges);
-    // every wave an equal share of the batch's 4 KiB blocks; stream-ordered
-    // scratch of this call for the tile counts (calls on different streams may overlap)
-    uint64_t* tiles = nullptr;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&tiles), (kRangeTiles + kDynCtrWords64) * sizeof(uint64_t), s);
-    if (e != hipSuccess) return map_err(e);
-    e = launch_range_flat(static_cast<const unsigned char*>(d_buf), rd, n, tiles, c->image, d_out, c->cus, s);
-    const hipError_t f = hipFreeAsync(tiles, s);
-    return map_err(e != hipSuccess ? e : f);
+    // every wave an equal share of the batch's 4 KiB blocks, in one launch
+    return map_err(range_batch(c.get(), static_cast<const unsigned char*>(d_buf),
+                               reinterpret_cast<const RangeDesc*>(d_ranges), n, d_out,
+                               static_cast<hipStream_t>(stream)));
 }
 
 int cc_crc_bufs_host(const void* const* h_bufs, const uint64_t* h_lens, uint64_t n, uint32_t* h_out) {
@@ -775,8 +868,8 @@ int cc_crc_bufs_host(const void* const* h_bufs, const uint64_t* h_lens, uint64_t
             return ring.fail(map_err(e));
         if ((e = hipMemcpyAsync(drecs, recs, k * sizeof(RangeDesc), hipMemcpyHostToDevice, strm)) != hipSuccess)
             return ring.fail(map_err(e));
-        if ((e = launch_range_flat(static_cast<const unsigned char*>(st.dev[s]), drecs, k, st.tiles[s], c->image,
-                                   st.dcrc[s], c->cus, strm)) != hipSuccess)
+        if ((e = range_batch(c.get(), static_cast<const unsigned char*>(st.dev[s]), drecs, k, st.dcrc[s], strm)) !=
+            hipSuccess)
             return ring.fail(map_err(e));
         if ((e = hipMemcpyAsync(st.hcrc[s], st.dcrc[s], k * 4, hipMemcpyDeviceToHost, strm)) != hipSuccess)
             return ring.fail(map_err(e));

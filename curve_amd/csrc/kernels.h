@@ -177,15 +177,28 @@ hipError_t launch_read_verify(const ReadVerifyLaunch& a, hipStream_t s);
 // <= 64 reads in one launch (no counts / scan; pages split over waves)
 hipError_t launch_read_verify_small(const ReadVerifyLaunch& a, hipStream_t s);
 // CRC32C (butil Value) of arbitrary byte ranges of one device buffer, on the
-// flat block schedule: range_tiles_kernel writes the 4 KiB-block
-// count of each of kRangeTiles contiguous tiles of the batch (and zeroes
-// out[]); range_flat_kernel gives every wave an equal share of the blocks,
-// ranges cut by a share boundary XOR their segments into out[].
-// tile_blocks: kRangeTiles + kDynCtrWords64 uint64 of stream-ordered scratch (the last: the
-// dynamic-tail chunk counter).
+// flat block schedule, ONE launch: range_flat_kernel counts the
+// 4 KiB blocks of kRangeTiles contiguous tiles of the batch itself (epoch-tagged
+// words in `tiles`), gives every wave an equal share of the blocks, and ranges
+// cut by a share boundary meet in their accumulator pair (acc[2r], acc[2r+1]).
+// The per-stream scratch (engine.hip range_work) is zero on first use and left
+// so by every launch: tiles are overwritten each call (the epoch tells this
+// call's words), the accumulators self-reset and each call zeroes the tail
+// counter slot the next call uses.
 constexpr uint32_t kRangeTiles = 1024;
-hipError_t launch_range_flat(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, uint64_t* tile_blocks,
-                             const void* image, uint32_t* out, int blocks, hipStream_t s);
+struct RangeLaunch {
+    const unsigned char* buf;
+    const RangeDesc* ranges;
+    uint64_t n;
+    uint64_t* tiles;             // [kRangeTiles] epoch << 40 | blocks of the tile
+    unsigned long long* tail;    // dynamic-tail counter slots (epoch % 2: this call's; the other zeroed for the next)
+    uint32_t* acc;               // [2 n] split-range XOR / block-count pairs, zero at rest
+    uint32_t epoch;              // 1 .. 2^24 - 1, the next one (parity alternating) per call on the scratch
+    const void* image;
+    uint32_t* out;
+    int blocks;
+};
+hipError_t launch_range_flat(const RangeLaunch& a, hipStream_t s);
 // x^(-8t) mod P for t = 0..kXinvEntries-1 (undoing the zero pad after a range in its last 4 KiB block)
 constexpr uint32_t kXinvEntries = 4100;  // x^(-8t), t < 4096 + 4: the zero pad after a range in its last 4 KiB block
 

@@ -563,40 +563,48 @@ __device__ __forceinline__ void mask_range_block(uint32_t (&w)[17], const RangeG
 }
 
 // ---------------------------------------------------------------------------
-// Flat block schedule of a range batch (WAL replay, raw-file hashes).  The
-// batch is one stream of 4 KiB blocks (range 0's blocks, then range 1's, ...),
-// B blocks in all.  The first Bs = B - B/kDynDiv are dealt out statically:
-// rounds * W equal pieces, wave w taking pieces w, w + W, ... whatever the
-// range sizes.  The last B/kDynDiv blocks are kDynBlocks-block chunks handed
-// out through an atomic counter to whichever waves finish first (per-wave
-// rates differ by ~7 % -- some XCDs run slower -- so a purely static split
-// waits for the slowest wave).  A range cut by a piece or chunk boundary is
-// hashed in segments: segment [kb, ke) of the range contributes
-// raw(segment || 0-pad) * x^(8 * (lim - 4096*ke)) (x^(-8t) for the one that
-// ends the range), XORed into out[] (zeroed by the tile pass); a range hashed
-// whole by one wave is stored directly.  Where a piece starts comes from
-// kRangeTiles per-tile block counts (range_tiles_kernel, one launch before),
-// held in registers by every wave.
+// Flat block schedule of a range batch (WAL replay, raw-file hashes), ONE
+// launch.  The batch is one stream of 4 KiB blocks (range 0's blocks, then
+// range 1's, ...), B blocks in all.  The first Bs = B - B/kDynDiv are dealt
+// out statically: rounds * W equal pieces, wave w taking pieces w, w + W, ...
+// whatever the range sizes.  The last B/kDynDiv blocks are kDynBlocks-block
+// chunks handed out through an atomic counter to whichever waves finish first
+// (per-wave rates differ by ~7 % -- some XCDs run slower -- so a purely static
+// split waits for the slowest wave).
+// Where a piece starts comes from kRangeTiles per-tile block counts, held in
+// registers by every wave.  The launch computes them itself: wave g counts
+// tiles g, g + W, ... and publishes each as one epoch-tagged word (a plain
+// device-coherent store: the word carries its own data, so no fence); every
+// wave then polls the words of the call's epoch while its workgroup's LDS
+// fills.  No wave ever waits on another without a bound: a tile word still
+// missing after kTileWaitTicks (a workgroup not resident -- CUs taken by other
+// work) is counted by the waiting wave itself from the descriptors.
+// A range cut by a piece or chunk boundary is hashed in segments: segment
+// [kb, ke) of the range contributes raw(segment || 0-pad) * x^(8 * (lim -
+// 4096*ke)) (x^(-8t) for the one that ends the range).  Segments meet in the
+// range's accumulator pair acc[2r] (XOR of the contributions) / acc[2r+1]
+// (blocks arrived): a segment XORs in, then adds its block count; the one
+// whose count completes the range takes the XOR, stores out[r] and leaves the
+// pair zero for the next call.  The tail's chunk counter alternates between
+// two slots by epoch, each call zeroing the one the next call uses.  A range hashed whole by one wave is stored
+// directly; an empty range (V = 0) by the wave that counts its tile.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void range_tiles_kernel(const RangeDesc* __restrict__ ranges, uint64_t n,
-                                                          uint64_t* __restrict__ tile_blocks,
-                                                          uint32_t* __restrict__ out) {
-    __shared__ uint64_t part[4];
-    const uint64_t lo = n * blockIdx.x / kRangeTiles, hi = n * (blockIdx.x + 1) / kRangeTiles;
+constexpr uint64_t kTileWaitTicks = 10000;  // 100 us of s_memrealtime (100 MHz) before a wave counts a tile itself
+constexpr uint32_t kEpochShift = 40;        // tile word: epoch << 40 | blocks
+
+// Blocks of tile t (ranges [n t / T, n (t+1) / T)), uniform; zero_empty: store
+// V = 0 for the tile's empty ranges.
+__device__ __forceinline__ uint64_t range_tile_count(const RangeLaunch& a, uint32_t t, uint32_t lane, bool zero_empty) {
+    const uint64_t lo = a.n * t / kRangeTiles, hi = a.n * (t + 1) / kRangeTiles;
     uint64_t sum = 0;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += 256) {
-        const RangeDesc d = ranges[i];
+    for (uint64_t i = lo + lane; i < hi; i += 64) {
+        const RangeDesc d = a.ranges[i];
         sum += d.len ? range_geo(d.off, d.len).nb : 0u;
-        out[i] = 0u;  // V(empty) = 0; split ranges XOR their segments into it
+        if (zero_empty && !d.len) a.out[i] = 0u;
     }
 #pragma unroll
     for (int d = 32; d; d >>= 1) sum += __shfl_xor(sum, d, 64);
-    if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = sum;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        tile_blocks[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
-    }
-    if (blockIdx.x == 0 && threadIdx.x < kDynCtrWords64) tile_blocks[kRangeTiles + threadIdx.x] = 0;  // tail heads
+    return sum;
 }
 
 __device__ __forceinline__ uint64_t wave_scan_incl(uint64_t v, uint32_t lane) {
@@ -614,34 +622,76 @@ constexpr uint64_t kRangeDynDiv = 32;  // 1/32 of the blocks go to the dynamic t
                                        // the one counter's atomics, 1/64 leaves tail)
 constexpr uint32_t kRangeHeads = 1;    // tail heads (A/B round 3: 8 per-XCD heads = one counter at 1/32)
 constexpr uint64_t kRangeDynBlocks = 16;  // blocks per dynamic chunk (A/B: 8 slower, 16 = 32)
-__global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsigned char* __restrict__ buf,
-                                                                   const RangeDesc* __restrict__ ranges, uint64_t n,
-                                                                   uint64_t* __restrict__ tile_blocks,
-                                                                   const uint4* __restrict__ image,
-                                                                   uint32_t* __restrict__ out) {
+__global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(RangeLaunch a) {
     constexpr uint32_t rounds = kRangeRounds;
     __shared__ uint32_t tab[kLdsBytes / 4];
-    fill_lds<64 * kFlatWaves>(tab, image);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t W = (uint64_t)gridDim.x * kFlatWaves;
+    const uint64_t w = (uint64_t)blockIdx.x * kFlatWaves + wave;
+    const uint64_t tag = (uint64_t)a.epoch << kEpochShift;
+    // this wave's tile counts, published before the LDS fill (which hides the
+    // stores' and the other workgroups' latency)
+    for (uint64_t t = w; t < kRangeTiles; t += W) {
+        const uint64_t cnt = range_tile_count(a, (uint32_t)t, lane, true);
+        if (lane == 0) __hip_atomic_store(a.tiles + t, tag | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    fill_lds<64 * kFlatWaves>(tab, static_cast<const uint4*>(a.image));
+    const unsigned char* __restrict__ buf = a.buf;
+    const RangeDesc* __restrict__ ranges = a.ranges;
+    const uint64_t n = a.n;
+    uint32_t* __restrict__ out = a.out;
     const uint32_t c0 = lane << 2 & 0x7Cu;
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
-    const uint64_t W = (uint64_t)gridDim.x * kFlatWaves;
-    const uint64_t w = (uint64_t)blockIdx.x * kFlatWaves + wave;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint4*>(image) + kLdsBytes / 16, 0, kXinvEntries * 128u, kBufFlags);
+        const_cast<uint4*>(static_cast<const uint4*>(a.image)) + kLdsBytes / 16, 0, kXinvEntries * 128u, kBufFlags);
 
-    // tile block counts: lane l holds tiles kTpl*l .. kTpl*l + kTpl-1, cum = inclusive prefix of the lane sums
+    // every tile count of this call: lane l holds tiles kTpl*l .. kTpl*l + kTpl-1,
+    // cum = inclusive prefix of the lane sums
     constexpr int kTpl = kRangeTiles / 64;
-    uint64_t tb[kTpl], lsum = 0;
+    constexpr uint64_t kCountMask = (1ull << kEpochShift) - 1;
+    uint64_t tb[kTpl];
+    {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t have = 0;  // bit j: tb[j] holds this call's count
+        for (;;) {
 #pragma unroll
-    for (int j = 0; j < kTpl; j++) lsum += (tb[j] = tile_blocks[kTpl * lane + j]);
+            for (int j = 0; j < kTpl; j++) {
+                const uint64_t v =
+                    __hip_atomic_load(a.tiles + kTpl * lane + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const bool ok = (v & ~kCountMask) == tag;
+                tb[j] = ok ? v & kCountMask : tb[j];
+                have |= ok ? 1u << j : 0u;
+            }
+            if (!__ballot(have != (1u << kTpl) - 1u)) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kTileWaitTicks) {
+                // a tile's wave is not running: count the missing tiles here
+#pragma unroll
+                for (int j = 0; j < kTpl; j++) {
+                    for (uint64_t m = __ballot(!((have >> j) & 1u)); m; m &= m - 1) {
+                        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                        const uint64_t cnt = range_tile_count(a, kTpl * l + j, lane, false);
+                        tb[j] = lane == l ? cnt : tb[j];
+                    }
+                }
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    uint64_t lsum = 0;
+#pragma unroll
+    for (int j = 0; j < kTpl; j++) lsum += tb[j];
     const uint64_t cum = wave_scan_incl(lsum, lane);
     const uint64_t B = readlane64(cum, 63);
     const uint64_t Bs = kRangeDynDiv ? B - B / kRangeDynDiv : B;  // statically dealt blocks
     const uint64_t n_dyn = (B - Bs + kRangeDynBlocks - 1) / kRangeDynBlocks;
-    unsigned long long* dyn_ctr = reinterpret_cast<unsigned long long*>(tile_blocks + kRangeTiles);
+    // the tail's counter: slot epoch % 2 of the block; this call zeroes the
+    // other slot for the stream's next call (nobody here touches it), so no
+    // wave has to count arrivals at the end to reset it
+    unsigned long long* dyn_ctr = a.tail + (a.epoch & 1u) * kDynHeadStride;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(a.tail + ((a.epoch + 1u) & 1u) * kDynHeadStride, 0ull);
     uint32_t dyn_head, dyn_tried;
     tail_cursor<kRangeHeads>(dyn_head, dyn_tried);
 
@@ -759,14 +809,14 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsig
         load_range_block(Cq, buf, pC.g, pC.k, lane, xr, pC.real);
         Pos pD = pC;
         uint32_t s = 0;
-        bool seg0 = false;  // the current segment began at block 0 of its range
+        uint32_t segk = 0;  // block of the range the current segment began at
         auto step = [&](uint32_t (&X)[17], const Pos& px, uint32_t (&Y)[17], const Pos& py) {
             load_range_block(Y, buf, py.g, py.k, lane, xr, py.real);
             const RangeGeo& gx = px.g;
             const uint32_t kx = px.k;
             mask_range_block(X, gx, kx, lane);
             const bool start = kx == 0 || px.first;
-            if (start) seg0 = kx == 0;
+            if (start) segk = kx;
             s = start ? X[0] : apply_g_xor(tab, s, X[0], c0, c1);
 #pragma unroll
             for (int j = 1; j < 16; j++) s = apply_g_xor(tab, s, X[j], c0, c1);
@@ -784,10 +834,18 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(const unsig
                 uint32_t v = end ? wave_xor(bit ? X[16] : 0u) : mulmod_small(pw, raw_pad);
                 if (end) v ^= gx.len >= 4 ? 0xFFFFFFFFu : ~mulmod_small(pw, 0xFFFFFFFFu);
                 if (lane == 0) {
-                    if (end && seg0)
+                    if (end && segk == 0) {
                         out[px.r] = v;
-                    else
-                        atomicXor(out + px.r, v);
+                    } else {  // one segment of a split range (rare: <= 2 an item)
+                        uint32_t* acc = a.acc + 2 * px.r;
+                        const uint32_t nblk = kx + 1 - segk;
+                        const uint32_t x = atomicXor(acc, v);
+                        asm volatile("" ::"v"(x) : "memory");  // the XOR is performed before the count says so
+                        if (atomicAdd(acc + 1, nblk) + nblk == gx.nb) {  // the range's last segment
+                            out[px.r] = atomicExch(acc, 0u);
+                            atomicExch(acc + 1, 0u);
+                        }
+                    }
                 }
             }
         };
@@ -2362,14 +2420,9 @@ hipError_t launch_fold(const FoldLaunch& a, hipStream_t s) {
 
 
 
-hipError_t launch_range_flat(const unsigned char* buf, const RangeDesc* ranges, uint64_t n, uint64_t* tile_blocks,
-                             const void* image, uint32_t* out, int blocks, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(range_tiles_kernel, dim3(kRangeTiles), dim3(256), 0, s, ranges, n, tile_blocks, out);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(range_flat_kernel, dim3(blocks), dim3(64 * kFlatWaves), 0, s, buf, ranges, n,
-                       tile_blocks, static_cast<const uint4*>(image), out);
+hipError_t launch_range_flat(const RangeLaunch& a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(range_flat_kernel, dim3(a.blocks), dim3(64 * kFlatWaves), 0, s, a);
     return hipGetLastError();
 }
 

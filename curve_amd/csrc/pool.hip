@@ -35,7 +35,8 @@ struct cc_comm {
     uint32_t* gather = nullptr;  // nranks x cap words of all-gather scratch on `device`
     uint64_t cap = 0;
     hipEvent_t done = nullptr;   // cc_comm_wait's completion marker
-    std::mutex mu;               // guards the scratch (re)allocation and the event
+    uint32_t* stall_abort = nullptr;  // failpoint only: host-mapped word the stall kernel polls
+    std::mutex mu;               // guards the scratch (re)allocation, the event and the failpoint word
 };
 
 static_assert(CC_COMM_ID_BYTES == sizeof(ncclUniqueId), "RCCL unique id size");
@@ -99,7 +100,10 @@ uint32_t wait_timeout_ms(uint32_t asked) {
 // role, test/failpoint/): $CC_INJECT_EXCHANGE_STALL_MS > 0 makes every digest
 // exchange first spin one wave on the stream for that long (at most 30 s), as
 // a collective whose peer stopped participating after init would sit in its
-// kernel.  cc_comm_wait must then give up at its deadline.
+// kernel.  cc_comm_wait must then give up at its deadline.  Like RCCL's own
+// kernels, which poll the communicator's abort flag, the stall also ends as
+// soon as cc_comm_wait raises the comm's host-mapped abort word (an abort
+// cannot preempt a kernel: without the word it would wait out the stall).
 uint32_t injected_stall_ms() {
     const char* e = getenv("CC_INJECT_EXCHANGE_STALL_MS");
     if (!e) return 0;
@@ -109,9 +113,11 @@ uint32_t injected_stall_ms() {
 
 // s_memrealtime runs at a constant 100 MHz on gfx9: 10 ns a tick.  One wave;
 // every exit path is bounded by the tick count.
-__global__ void stall_kernel(uint64_t ticks) {
+__global__ void stall_kernel(uint64_t ticks, const uint32_t* abort_word) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks &&
+           __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u)
+        __builtin_amdgcn_s_sleep(127);
 }
 
 }  // namespace
@@ -178,6 +184,7 @@ static int comm_release(cc_comm* comm, bool abort) {
     }
     if (comm->gather) (void)hipFree(comm->gather);
     if (comm->done) (void)hipEventDestroy(comm->done);
+    if (comm->stall_abort) (void)hipHostFree(comm->stall_abort);
     if (cur >= 0) (void)hipSetDevice(cur);
     delete comm;
     return rc;
@@ -218,6 +225,10 @@ int cc_comm_wait(cc_comm* comm, void* stream, uint32_t timeout_ms) {
         if (failed || late) {
             // leave without the peers: the abort also releases the collective's
             // kernels still waiting for them, so the stream drains
+            {
+                std::lock_guard<std::mutex> lk(comm->mu);
+                if (comm->stall_abort) __atomic_store_n(comm->stall_abort, 1u, __ATOMIC_RELEASE);
+            }
             (void)ncclCommAbort(comm->nc);
             comm->nc = nullptr;
             return back(failed ? CC_ECOMM : CC_ETIMEDOUT);
@@ -247,7 +258,23 @@ int cc_digest_allreduce_dev(cc_comm* comm, uint32_t* d_digest, uint64_t n, void*
         }
     }
     if (const uint32_t ms = injected_stall_ms()) {
-        hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, s, (uint64_t)ms * 100000ull);
+        uint32_t* word = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(comm->mu);
+            if (!comm->stall_abort) {
+                void* p = nullptr;
+                const hipError_t e = hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent);
+                if (e != hipSuccess) return map_hip(e);
+                comm->stall_abort = static_cast<uint32_t*>(p);
+                *comm->stall_abort = 0u;
+            }
+            void* d = nullptr;
+            const hipError_t e = hipHostGetDevicePointer(&d, comm->stall_abort, 0);
+            if (e != hipSuccess) return map_hip(e);
+            word = static_cast<uint32_t*>(d);
+        }
+        hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, s, (uint64_t)ms * 100000ull,
+                           static_cast<const uint32_t*>(word));
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return map_hip(e);
     }

@@ -24,7 +24,5 @@ case $P in
   page) timeout -k 10 300 python -u scripts/ab_bench.py $L ;;
   pool) timeout -k 10 300 python -u scripts/pool_ab.py $L ;;
   reads) timeout -k 10 300 python -u scripts/reads_ab.py $L ;;
-  wal) for rep in 1 2; do for lib in $L; do echo "$lib"
-         timeout -k 10 120 python3 scripts/prof_wal.py --lib "$lib" | grep -o "median [0-9.]* GB/s [0-9.]* spot_ok [A-Za-z]*" || exit 1
-       done; done ;;
+  wal) timeout -k 10 300 python -u scripts/wal_ab.py $L ;;
 esac

@@ -20,7 +20,8 @@ p.add_argument("--lib", default=None, help="libcurvecrc variant to load instead 
 a = p.parse_args()
 if a.lib:
     from curve_amd import _lib
-    _lib.LIB_PATH = os.path.abspath(a.lib)
+    # relative to the repo root (the profilers run these from /tmp)
+    _lib.LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), a.lib)
 dev = torch.device("cuda", 0)
 pb = 4096
 pool = torch.empty(a.gib << 30, dtype=torch.uint8, device=dev).random_(0, 256)

@@ -190,3 +190,59 @@ def range_crc_model(buf: np.ndarray, off: int, length: int, img: np.ndarray) -> 
         r ^= lds_read(img, ((v << np.uint32(8)) | cf) + np.uint32(4096 * n))
     raw_pad = int(np.bitwise_xor.reduce(r))
     return mulmod(xinv_bytes(t), raw_pad) ^ C.zeros(length)
+
+
+def range_flat_items(B: int, waves: int, rounds: int = 2, dyn_div: int = 32, dyn_blocks: int = 16):
+    """Work items of range_flat_kernel over a stream of B blocks: `rounds`
+    static pieces per wave ([Bs c / RW, Bs (c+1) / RW), c < rounds * waves,
+    empty ones skipped), then the dynamic tail's chunks of dyn_blocks blocks."""
+    Bs = B - B // dyn_div if dyn_div else B
+    RW = rounds * waves
+    items = [(Bs * c // RW, Bs * (c + 1) // RW) for c in range(RW)]
+    items = [it for it in items if it[0] < it[1]]
+    n_dyn = (B - Bs + dyn_blocks - 1) // dyn_blocks
+    items += [(Bs + c * dyn_blocks, min(Bs + (c + 1) * dyn_blocks, B)) for c in range(n_dyn)]
+    return items
+
+
+def range_flat_segments(nbs, waves: int, **kw):
+    """Segments (range, first block, blocks) the kernel hashes for ranges of
+    nbs[r] blocks: each item cut at the range boundaries it crosses."""
+    starts = np.concatenate([[0], np.cumsum(nbs)]).astype(np.int64)
+    segs = []
+    for b0, b1 in range_flat_items(int(starts[-1]), waves, **kw):
+        r = int(np.searchsorted(starts, b0, side="right")) - 1
+        b = b0
+        while b < b1:
+            while nbs[r] == 0 or starts[r + 1] <= b:
+                r += 1
+            e = min(b1, int(starts[r + 1]))
+            segs.append((r, b - int(starts[r]), e - b))
+            b = e
+    return segs
+
+
+def range_accumulate(segs, nbs, contrib, rng):
+    """The split-range meeting point, in a random arrival order: a segment that
+    is its range whole stores; any other XORs into the range's pair, adds its
+    blocks, and the one whose add completes nb takes the XOR, stores and clears
+    the pair.  Returns (out, pairs left non-zero, stores per range)."""
+    out, stores = {}, {}
+    acc = {}
+    for i in rng.permutation(len(segs)):
+        r, kb, cnt = segs[i]
+        v = contrib[i]
+        if kb == 0 and cnt == nbs[r]:
+            out[r] = v
+            stores[r] = stores.get(r, 0) + 1
+            continue
+        x, c = acc.get(r, (0, 0))
+        x ^= v
+        if c + cnt == nbs[r]:
+            out[r] = x
+            stores[r] = stores.get(r, 0) + 1
+            acc[r] = (0, 0)
+        else:
+            acc[r] = (x, c + cnt)
+    left = [r for r, p in acc.items() if p != (0, 0)]
+    return out, left, stores

@@ -1139,6 +1139,129 @@ def test_crc_ranges_arbitrary(dev, oracle):
     assert [int(x) for x in got] == want
 
 
+def _range_batch(rng, size, shape):
+    """Offsets / lengths of a range batch: "giants" (ranges of MiBs cut into
+    segments by many wave shares, next to 0-3 byte ranges), "wal" (1-128 KiB),
+    "tiny" (0-40 bytes, many empties)."""
+    if shape == "giants":
+        n = 3000
+        lens = rng.integers(0, 4, n)
+        lens[::300] = rng.integers(1 << 20, 6 << 20, lens[::300].size)
+    elif shape == "wal":
+        n = 20000
+        lens = rng.integers(1, (128 << 10) + 1, n)
+    else:
+        n = 50000
+        lens = rng.integers(0, 41, n)
+        lens[::7] = 0
+    offs = rng.integers(0, size - lens)
+    return offs, lens
+
+
+def test_crc_ranges_scratch_left_clean_between_calls(dev, oracle):
+    """cc_crc_ranges_dev is ONE launch: the tile counts are epoch-tagged words
+    the launch computes itself, split ranges meet in per-range accumulator
+    pairs, and the tail counters self-reset -- all in the stream's engine-owned
+    scratch, never cleared between calls.  Batches of different shapes (split-
+    heavy giants, WAL-sized, tiny with empties) run back to back on one stream,
+    twice over, each == the oracle: no call sees a previous call's tile words,
+    partial XORs or counters.  Then a batch past the cached scratch's size
+    (4 Mi + 7 ranges: scratch of its own, allocated and cleared for the call)
+    and the cached path again after it; then cc_engine_trim and one more batch."""
+    from curve_amd import crc as C
+    from curve_amd import _lib
+    rng = np.random.default_rng(0xF01D)
+    size = 24 << 20
+    buf = rng.integers(0, 256, size, dtype=np.uint8)
+    d = to_dev(buf, dev)
+
+    def check(offs, lens, sample=None):
+        got = u32(C.crc_ranges(d, offs, lens))
+        idx = np.arange(len(offs)) if sample is None else sample
+        want = np.array([oracle.crc32c(buf[offs[i]:offs[i] + lens[i]].tobytes()) for i in idx], dtype=np.uint32)
+        bad = idx[got[idx] != want]
+        assert bad.size == 0, (bad[:10], offs[bad[:3]], lens[bad[:3]])
+
+    batches = [_range_batch(rng, size, sh) for sh in ("giants", "wal", "tiny")]
+    for _ in range(2):
+        for offs, lens in batches:
+            check(offs, lens)
+    n = (4 << 20) + 7  # past kRangeCacheRanges
+    lens = rng.integers(0, 17, n)
+    lens[-1] = 5 << 20  # one range cut by many shares
+    offs = rng.integers(0, size - lens)
+    sample = np.unique(np.concatenate([np.arange(0, n, 211), np.arange(n - 3000, n)]))
+    check(offs, lens, sample)
+    check(*batches[0])
+    assert _lib.lib().cc_engine_trim() == 0
+    check(*batches[2])
+
+
+def test_crc_ranges_streams_and_threads(dev, oracle):
+    """Per-stream range scratch: four threads, two on streams of their own and
+    two on the null stream (one handle, keyed per calling thread), run batches
+    at the same time; every CRC == the oracle."""
+    import threading
+    from curve_amd import crc as C
+    rng = np.random.default_rng(77)
+    size = 16 << 20
+    buf = rng.integers(0, 256, size, dtype=np.uint8)
+    d = to_dev(buf, dev)
+    jobs = [_range_batch(rng, size, ("giants", "wal", "tiny", "giants")[t]) for t in range(4)]
+    want = [np.array([oracle.crc32c(buf[o:o + l].tobytes()) for o, l in zip(*j)], dtype=np.uint32) for j in jobs]
+    torch.cuda.synchronize()
+    res, errs = [None] * 4, []
+
+    def run(t):
+        try:
+            s = torch.cuda.Stream(dev) if t < 2 else None  # None: the null stream, keyed per thread
+            for _ in range(3):
+                out = C.crc_ranges(d, *jobs[t], stream=s)
+            torch.cuda.synchronize()
+            res[t] = u32(out)
+        except Exception as e:  # surfaced below
+            errs.append((t, repr(e)))
+
+    ths = [threading.Thread(target=run, args=(t,)) for t in range(4)]
+    [x.start() for x in ths]
+    [x.join() for x in ths]
+    assert not errs, errs
+    for t in range(4):
+        assert (res[t] == want[t]).all(), t
+
+
+def test_crc_ranges_without_every_workgroup_resident(dev, oracle):
+    """The launch's tile counts come from every workgroup; a wave never waits
+    for one without a bound.  With the process's queues limited to 8 CUs
+    (HSA_CU_MASK) the grid of one workgroup per CU cannot be resident at once:
+    the running waves give up on the missing tile words after their wait and
+    count those tiles themselves.  Results still == the oracle (run in a child
+    process so the mask applies to its queues only)."""
+    import subprocess
+    import sys
+    code = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, %r)
+from curve_amd import crc as C
+from oracle import oracle as O
+rng = np.random.default_rng(5)
+size = 8 << 20
+buf = rng.integers(0, 256, size, dtype=np.uint8)
+d = torch.from_numpy(buf).to("cuda:0")
+lens = rng.integers(0, 70000, 4000); lens[::400] = 3 << 20
+offs = rng.integers(0, size - lens)
+for _ in range(2):
+    got = C.crc_ranges(d, offs, lens).cpu().numpy().view(np.uint32)
+want = np.array([O.crc32c(buf[o:o + l].tobytes()) for o, l in zip(offs, lens)], dtype=np.uint32)
+bad = np.flatnonzero(got != want)
+print("bad", bad.size)
+sys.exit(1 if bad.size else 0)
+""" % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HSA_CU_MASK="0:0-7")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+
+
 def test_wal_segment_replay_verify(dev, oracle):
     """Synthetic CurveSegment file: header walk on the host, every entry's data
     checksum verified in one device call; a flipped data byte is caught."""

@@ -78,3 +78,41 @@ def test_div_x_inverts_mul_x():
     for b in rng.integers(0, 2**32, 200, dtype=np.uint64).tolist():
         assert km.div_x(km.mulmod(0x40000000, b)) == b  # (b * x) / x
     assert km.mulmod(km.xinv_bytes(3), km.mulmod(0x80000000 >> 24, 0xDEADBEEF)) == 0xDEADBEEF  # x^-24 * x^24
+
+
+@pytest.mark.parametrize("shape", ["wal", "giants", "tiny", "few"])
+@pytest.mark.parametrize("waves", [2048, 256, 7])
+def test_range_flat_schedule_and_split_meeting(shape, waves):
+    """range_flat_kernel's schedule (static block shares + dynamic chunks) cuts
+    every range into segments covering each of its blocks once; the split
+    ranges' accumulator pairs (XOR, then block count) end with exactly one
+    store per non-empty range, of the XOR of its segments, and leave every pair
+    zero for the next call -- in any arrival order."""
+    rng = np.random.default_rng(len(shape) * 1000 + waves)
+    n = {"wal": 20000, "giants": 300, "tiny": 30000, "few": 3}[shape]
+    if shape == "wal":
+        nbs = (rng.integers(1, 131073, n) + 28 + 4095) // 4096
+    elif shape == "giants":
+        nbs = rng.integers(0, 2, n)
+        nbs[::30] = rng.integers(256, 6000, nbs[::30].size)
+    elif shape == "tiny":
+        nbs = rng.integers(0, 3, n)
+    else:
+        nbs = np.array([4097, 0, 1])
+    segs = km.range_flat_segments(nbs, waves)
+    cover = {}
+    for r, kb, cnt in segs:
+        assert cnt >= 1 and kb + cnt <= nbs[r]
+        cover.setdefault(r, []).append((kb, cnt))
+    for r in range(n):
+        parts = sorted(cover.get(r, []))
+        assert sum(c for _, c in parts) == nbs[r]
+        assert all(a + c == b for (a, c), (b, _) in zip(parts, parts[1:]))  # contiguous, disjoint
+    contrib = rng.integers(0, 2**32, len(segs)).tolist()
+    want = {}
+    for (r, _, _), v in zip(segs, contrib):
+        want[r] = want.get(r, 0) ^ v
+    for _ in range(3):
+        out, left, stores = km.range_accumulate(segs, nbs, contrib, rng)
+        assert out == want and not left
+        assert all(c == 1 for c in stores.values()) and set(stores) == {r for r in range(n) if nbs[r]}
