@@ -117,11 +117,18 @@ struct DevCtx {
     std::mutex tab_mu;  // epilogue-table inserts
     std::atomic<uint64_t> epi_key[kEpiSlots];  // key + 1 (0 = empty); published after epi_ptr
     std::atomic<void*> epi_ptr[kEpiSlots];
-    // the page kernel's self-resetting tail counters, one block per stream
-    // (kernels.hip tail_reset): zeroed on the stream when created, left zero by
-    // every launch that uses it, so a call needs no allocation or memset
+    // the page kernel's tail counters, one block of two slot sets per stream:
+    // zeroed on the stream when created; a launch pulls from slot set `parity`
+    // and zeroes the other for the stream's next launch, so a call needs no
+    // allocation or memset.  tail_mu is held over the flip and the enqueue.
+    struct TailBlock {
+        StreamKey s;
+        unsigned long long* p;
+        uint32_t parity;  // the slot set the stream's next launch pulls from
+        bool dirty;       // a launch may not have zeroed the next slot set: clear first
+    };
     std::mutex tail_mu;
-    std::vector<std::pair<StreamKey, unsigned long long*>> tails;
+    std::vector<TailBlock> tails;
     // the write log's page tables, one per stream (apply_log); log_mu is held
     // over a call's whole enqueue (insert + pages) so calls sharing a stream
     // cannot interleave on its table
@@ -206,7 +213,7 @@ DevCtx::~DevCtx() {
         if (image) hipFree(image);
         for (int i = 0; i < kEpiSlots; i++)
             if (void* p = epi_ptr[i].load()) hipFree(p);
-        for (auto& t : tails) hipFree(t.second);
+        for (auto& t : tails) hipFree(t.p);
         for (auto& t : log_tabs) (void)hipFreeAsync(t.p, nullptr);
         for (auto& t : range_works) (void)hipFreeAsync(t.p, nullptr);
         (void)hipDeviceSynchronize();
@@ -297,17 +304,22 @@ bool plan_tail(const DevCtx* c, PageLaunch& a) {
 
 constexpr size_t kMaxTailBlocks = 256;  // streams with a block of their own
 
-// The stream's self-resetting tail-counter block, created (and zeroed on the
-// stream) on first use; null when kMaxTailBlocks streams already hold one.
-// Keyed by the stream (stream_key: a pseudo-handle is per calling thread): a
-// destroyed stream's handle is only reused for a new stream after
-// hipStreamDestroy, which the caller orders after that stream's work as for
-// any of its buffers.
-unsigned long long* tail_block(DevCtx* c, hipStream_t s) {
+// The stream's tail-counter block, created (and zeroed on the stream) on first
+// use; null when kMaxTailBlocks streams already hold one.  Caller holds
+// c->tail_mu.  Keyed by the stream (stream_key: a pseudo-handle is per calling
+// thread): a destroyed stream's handle is only reused for a new stream after
+// hipStreamDestroy, which the caller orders after that stream's work as for any
+// of its buffers.
+DevCtx::TailBlock* tail_block(DevCtx* c, hipStream_t s) {
     const StreamKey key = stream_key(s);
-    std::lock_guard<std::mutex> lk(c->tail_mu);
     for (auto& t : c->tails)
-        if (t.first == key) return t.second;
+        if (t.s == key) {
+            if (t.dirty) {
+                if (hipMemsetAsync(t.p, 0, kTailBlockBytes, s) != hipSuccess) return nullptr;
+                t.dirty = false;
+            }
+            return &t;
+        }
     if (c->tails.size() >= kMaxTailBlocks) return nullptr;
     void* p = nullptr;
     if (hipMalloc(&p, kTailBlockBytes) != hipSuccess) return nullptr;
@@ -315,22 +327,31 @@ unsigned long long* tail_block(DevCtx* c, hipStream_t s) {
         (void)hipFree(p);
         return nullptr;
     }
-    c->tails.push_back({key, static_cast<unsigned long long*>(p)});
-    return static_cast<unsigned long long*>(p);
+    c->tails.push_back({key, static_cast<unsigned long long*>(p), 0u, false});
+    return &c->tails.back();
 }
 
 // Page kernel launch (kernels.hip, page_crc_kernel) with its dynamic tail when
-// plan_tail() gives one: the tail's counters are the stream's self-resetting
-// block, or (no block free) a counter allocated + zeroed for this launch.
+// plan_tail() gives one: the tail's counters are one slot set of the stream's
+// block (the launch zeroes the other for the next), or (no block free) a
+// counter allocated + zeroed for this launch.
 hipError_t launch_page_tail(DevCtx* c, PageLaunch& a, bool verify, hipStream_t s, bool load_probe = false) {
     auto launch = [&]() {
         return load_probe ? launch_page_load_probe(a, s) : verify ? launch_page_verify(a, s) : launch_page_crc(a, s);
     };
     if (!plan_tail(c, a)) return launch();
-    if (unsigned long long* blk = tail_block(c, s)) {
-        a.dyn_ctr = blk;
-        a.done_ctr = blk + kDynCtrWords64;
-        return launch();
+    {
+        std::lock_guard<std::mutex> lk(c->tail_mu);
+        if (DevCtx::TailBlock* t = tail_block(c, s)) {
+            a.dyn_ctr = t->p + t->parity * kDynCtrWords64;
+            a.dyn_next = t->p + (t->parity ^ 1u) * kDynCtrWords64;
+            const hipError_t e = launch();
+            if (e == hipSuccess)
+                t->parity ^= 1u;
+            else
+                t->dirty = true;  // may or may not have run: clear both slot sets before the next use
+            return e;
+        }
     }
     unsigned long long* ctr = nullptr;
     hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&ctr), kDynCtrBytes, s);

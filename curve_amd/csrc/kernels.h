@@ -19,9 +19,9 @@ constexpr uint32_t kDynHeads = 8;  // dynamic-tail counters of the page kernel: 
 constexpr uint32_t kDynHeadStride = 16;  // 128 bytes between heads: one cache line each
 constexpr uint32_t kDynCtrBytes = kDynHeads * kDynHeadStride * 8;
 constexpr uint32_t kDynCtrWords64 = kDynHeads * kDynHeadStride;  // the heads as uint64 words
-// A self-resetting counter block (page kernel): the heads, then the launch's
-// wave-arrival counter on a line of its own.
-constexpr uint32_t kTailBlockWords64 = kDynCtrWords64 + kDynHeadStride;
+// A stream's tail-counter block: two slot sets of heads; a launch pulls from
+// one and zeroes the other for the stream's next launch (engine.hip tail_block).
+constexpr uint32_t kTailBlockWords64 = 2 * kDynCtrWords64;
 constexpr uint32_t kTailBlockBytes = kTailBlockWords64 * 8;
 
 // Host builder of the 160 KiB LDS image (engine.hip).
@@ -51,10 +51,9 @@ struct PageLaunch {
     // [static_tiles, all) are handed out through this zeroed counter
     unsigned long long* dyn_ctr;  // kDynHeads counters, kDynHeadStride words apart (zeroed before the launch)
     uint64_t static_tiles;
-    // self-reset (non-null = dyn_ctr is a kTailBlockWords64 block, this is its
-    // arrival word): the last wave out of the launch zeroes the heads and this
-    // word, so the block is zero again for the stream's next launch
-    unsigned long long* done_ctr;
+    // non-null: dyn_ctr is one slot set of the stream's tail block and this the
+    // other, which the launch zeroes for the stream's next launch
+    unsigned long long* dyn_next;
     // fused metapages (cc_pool_scan_dev when metapage size == page size): n_meta
     // more pages of the same size, appended to the dynamic tail as chunks of their own
     const uint32_t* meta_pages;

@@ -267,27 +267,20 @@ struct ZeroRanges {
             for (uint64_t i = threadIdx.x; i < n[k]; i += blockDim.x) p[k][i] = 0u;
     }
 };
-// The dynamic tail's extras (PageLaunch::meta_pages / done_ctr): a second page
-// array appended to the tail as chunks of its own, and the arrival word of a
-// self-resetting counter block.
+// The dynamic tail's extras (PageLaunch::meta_pages / dyn_next): a second page
+// array appended to the tail as chunks of its own, and the other slot set of
+// the stream's tail block, which this launch zeroes for the stream's next one.
+// (Round 3 reset the counters at the END: every wave added to an arrival word
+// and the last one zeroed the heads -- 2,048 returning atomics on one word in
+// the kernel's last microseconds, ~12 ns each when they queue.)
 struct TailExtra {
     const uint32_t* pages;
     uint64_t n;
     uint32_t* out;
-    unsigned long long* done;
+    unsigned long long* next;
 };
-// Self-reset: every wave arrives once, after its last pull; the last to arrive
-// zeroes the heads and the arrival word (device-scope atomics, like the pulls),
-// so the block is zero for the next launch on the stream.  A wave's pulls have
-// returned before it arrives (its exit depends on their values), so no pull can
-// follow the reset -- and no fence is needed: a device-scope fence here would
-// write back the XCD's L2 once per wave (A/B: +1.7 % on the page kernel).
-__device__ __forceinline__ void tail_reset(unsigned long long* ctr, unsigned long long* done, uint32_t lane) {
-    if (lane != 0) return;
-    const unsigned long long waves = (unsigned long long)gridDim.x * kWavesPerBlock;
-    if (atomicAdd(done, 1ull) != waves - 1) return;
-    for (uint32_t h = 0; h < kDynHeads; h++) atomicExch(ctr + h * kDynHeadStride, 0ull);
-    atomicExch(done, 0ull);
+__device__ __forceinline__ void tail_clear_next(const TailExtra& ex) {
+    if (ex.next && blockIdx.x == 0 && threadIdx.x < kDynHeads) atomicExch(ex.next + threadIdx.x * kDynHeadStride, 0ull);
 }
 
 template <int M, int MODE>
@@ -297,6 +290,7 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
     uint32_t tshift, unsigned long long* __restrict__ dyn_ctr, uint64_t static_tiles, ZeroRanges zr, TailExtra ex) {
     __shared__ uint32_t tab[kLdsBytes / 4];
     if (blockIdx.x == 0) zr.clear();
+    tail_clear_next(ex);
     fill_lds(tab, image);
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -380,7 +374,6 @@ __global__ __launch_bounds__(kBlockThreads) void page_crc_kernel(
         W.wstride = 1ull << tshift;  // consecutive tiles: page(k) = p0 + k
         lim = p0 + kPageDynPages < end ? p0 + kPageDynPages : end;
     }
-    if (dyn_ctr && ex.done) tail_reset(dyn_ctr, ex.done, lane);
 }
 
 // Any M (page_bytes = 256*M): no register prefetch, dynamic chain length.
@@ -2318,7 +2311,7 @@ __global__ void xor_fold_kernel(const uint32_t* __restrict__ gathered, uint32_t 
 TailExtra tail_extra(const PageLaunch& a) {
     const bool meta = a.dyn_ctr && a.meta_pages && a.n_meta;
     return {meta ? a.meta_pages : nullptr, meta ? a.n_meta : 0, meta ? a.meta_out : nullptr,
-            a.dyn_ctr ? a.done_ctr : nullptr};
+            a.dyn_ctr ? a.dyn_next : nullptr};
 }
 
 template <int MODE>
