@@ -1573,410 +1573,6 @@ __global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(Log
     }
 }
 
-// ---------------------------------------------------------------------------
-// Write log, 4 KiB pages, full rehash: 16 lanes per page, 4 pages per wave.
-// ---------------------------------------------------------------------------
-// Layout.  Lane L = 16 g + i of a wave holds page g's 16-byte chunks i of every
-// 256-byte row j: page bytes [256 j + 16 i, +16) in X[j] (one dwordx4 per row:
-// a row of 4 pages is ONE load / store instruction instead of four).  The CRC
-// needs no transpose: lane L runs four Horner chains, k = 0..3, over dwords
-// 4i + k + 64 j -- exactly the chain of lane v = 4i + k of the one-page-per-wave
-// layout (the 256-byte jump G = F^64, the same LDS tables, lane L reading slot
-// L mod 32), and its share is XOR_k F^(64 - v)(s_k) from the same per-lane final
-// maps (column v).  The 16 lanes of a page XOR their shares with 4 DPP steps
-// inside their row of 16.  Final-map reads are made conflict-free by rotating
-// the order of k per lane (kk = k + g + 2 (i >> 3)): within a 32-lane bank group
-// the 32 lanes then read 32 distinct columns mod 32.
-// What moves into vector registers: the piece geometry (per page, i.e. per 16
-// lanes).  A page's single piece [rlo, rhi) covers some chunks whole -- those
-// rows are loaded straight from the source (one 64-bit address select per row;
-// every byte of such a chunk is inside the update's source) -- touches at most
-// two partially ("edge" chunks, containing rlo and rhi - 1), and leaves the rest.
-// An edge chunk's source bytes come as the aligned dwords holding them (five
-// dword loads per edge; an unneeded dword loads a dword that holds a byte of the
-// piece instead, so no load leaves the update's source range) and are spliced
-// in under their byte mask.  Pages with several pieces (~1 % of a random batch)
-// are deferred to the end of the wave's batch and finished one per wave by
-// log_page_multi.  Two sets of 4 pages are in flight per wave: set t+1's loads
-// while set t is merged, stored and hashed.
-#ifndef CC_LOG_QUAD
-#define CC_LOG_QUAD 0  // 4 KiB pages, full mode: log_quad_kernel (1) or log_pages_kernel (0); A/B in DESIGN §6a
-#endif
-#ifndef CC_QUAD_WAVES
-#define CC_QUAD_WAVES 8  // waves per CU (two register sets of 4 pages: ~180 VGPRs, 2 waves per SIMD)
-#endif
-#ifndef CC_QUAD_SKEW_W0
-#define CC_QUAD_SKEW_W0 54  // head shares of the older / younger wave on each SIMD
-#endif
-#ifndef CC_QUAD_SKEW_W1
-#define CC_QUAD_SKEW_W1 46
-#endif
-#ifndef CC_QUAD_ROW_NT
-#define CC_QUAD_ROW_NT 1  // row loads (page and covered source chunks) nontemporal
-#endif
-constexpr int kQuadWaves = CC_QUAD_WAVES;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-// global (not flat) address space: flat loads would count against lgkmcnt too and
-// force full waits
-typedef __attribute__((address_space(1))) u32x4 gu32x4;
-typedef __attribute__((address_space(1))) uint32_t gu32;
-
-// A page with several pieces, by one wave, not pipelined: the list (head piece
-// of update u0h, second piece p1) is ranked by update index and applied in log
-// order; a list longer than 64 makes the wave replay the whole log for the page.
-template <int M, bool Delta>
-__device__ __forceinline__ void log_page_multi(const LogLaunch& a, const uint32_t* tab, uint32_t pg, uint32_t u0h,
-                                            uint32_t p1, uint32_t lane) {
-    const uint32_t c0 = lane << 2 & 0x7Cu, c1 = c0 | 0x10000u, cf = kFinBase + (lane << 2);
-    const uint32_t pb = a.page_bytes;
-    const uint64_t pbase = (uint64_t)pg * pb;
-    uint32_t X[M], O[Delta ? M : 1];
-    load_rows<M>(X, a.pool + pbase, 0xFFFFFFFFu, lane);
-    uint32_t vz = 0;
-    asm volatile("" : "+v"(vz));
-    const uint32_t oc = Delta ? a.page_crcs[pg + vz] : 0u;
-    if constexpr (Delta) {
-#pragma unroll
-        for (int j = 0; j < M; j++) O[j] = X[j];
-    }
-    uint32_t dirty = 0;
-    const uint32_t u1h = p1 / a.slots;
-    uint32_t cnt = 2, mu = lane == 0 ? u0h : (lane == 1 ? u1h : 0xFFFFFFFFu);  // update of lane's piece
-    const UpdateDesc dq = a.upd[(lane < 2 ? mu : u0h) + vz];
-    uint32_t q = a.next[p1 + vz];
-    uint64_t dd = dq.dst, ds = dq.src;
-    uint32_t dn = dq.len;
-    while (q != kNoPiece && cnt < 64u) {
-        mu = lane == cnt ? q / a.slots : mu;
-        cnt++;
-        q = a.next[q + vz];
-    }
-    if (cnt > 2 && q == kNoPiece) {
-        const UpdateDesc dr = a.upd[(lane < cnt ? mu : u0h) + vz];
-        dd = dr.dst, ds = dr.src, dn = dr.len;
-    }
-    if (q != kNoPiece) {  // > 64 pieces: replay the whole log for this page, 64 records a round
-        for (uint64_t b = 0; b < a.n_updates; b += 64) {
-            const uint64_t i = b + lane;
-            const UpdateDesc dr = a.upd[(i < a.n_updates ? i : b) + vz];
-            const bool ok = i < a.n_updates && dr.len >= 1 && dr.len <= a.max_len && dr.dst < a.pool_bytes &&
-                            dr.len <= a.pool_bytes - dr.dst && dr.dst < pbase + pb && dr.dst + dr.len > pbase;
-            for (uint64_t m = __ballot(ok); m; m &= m - 1) {
-                const uint32_t l = (uint32_t)__builtin_ctzll(m);
-                const Piece pq = piece_in_page(pbase, pb, readlane64(dr.dst, l), readlane64(dr.src, l),
-                                               __builtin_amdgcn_readlane(dr.len, l), a.src);
-                PieceSrc<M> T;
-                fetch_piece<M>(T, pq, lane);
-                merge_piece<M>(X, dirty, T, pq, lane);
-            }
-        }
-    } else {
-        uint32_t rank = lane < cnt ? 0u : 0xFFFFu;  // lanes < cnt: distinct updates
-        for (uint32_t j = 0; j < cnt; j++) rank += (uint32_t)__builtin_amdgcn_readlane(mu, j) < mu;
-        for (uint32_t r = 0; r < cnt; r++) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(__ballot(rank == r));
-            const Piece pq = piece_in_page(pbase, pb, readlane64(dd, l), readlane64(ds, l),
-                                           __builtin_amdgcn_readlane(dn, l), a.src);
-            PieceSrc<M> T;
-            fetch_piece<M>(T, pq, lane);
-            merge_piece<M>(X, dirty, T, pq, lane);
-        }
-    }
-    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(a.pool + pbase, 0, 256u * M, kBufFlags);
-#pragma unroll
-    for (int j = 0; j < M; j++)
-        __builtin_amdgcn_raw_buffer_store_b32(X[j], rp, row_sel(((dirty >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j,
-                                              0, kLogStoreAux);
-    uint32_t crc;
-    if constexpr (Delta) {
-#pragma unroll
-        for (int j = 0; j < M; j++) O[j] ^= X[j];
-        crc = wave_xor(apply_fin(tab, chain<M>(tab, O, c0, c1), cf)) ^ oc;
-    } else {
-        crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
-    }
-    if (lane == 0) a.page_crcs[pg] = crc;
-}
-
-// byte mask of chunk dword k (chunk bytes 4k .. 4k+3) inside [pa, pb), 0 <= pa < pb <= 16
-__device__ __forceinline__ uint32_t chunk_dword_mask(uint32_t pa, uint32_t pb, int k) {
-    const int32_t lo = min(max((int32_t)pa - 4 * k, 0), 4), hi = min(max((int32_t)pb - 4 * k, 0), 4);
-    return (uint32_t)(((1ull << (8 * hi)) - 1ull) & ~((1ull << (8 * lo)) - 1ull));
-}
-
-// The geometry of a page's single piece [rlo, rhi) in the chunk layout.
-struct QuadGeo {
-    uint32_t rlo, rhi;
-    uint32_t ce[2];      // edge chunks' page byte offsets
-    bool ex[2];          // edge chunk e exists
-    uint32_t pa[2], pz[2];  // the piece's bytes in edge chunk e: [pa, pz) chunk-relative
-};
-__device__ __forceinline__ QuadGeo quad_geo(uint32_t rr) {
-    QuadGeo q;
-    q.rlo = rr & 0xFFFFu;
-    q.rhi = rr >> 16;
-    q.ce[0] = q.rlo & ~15u;
-    q.ex[0] = (q.rlo & 15u) || q.rhi < q.ce[0] + 16u;
-    q.ce[1] = (q.rhi - 1u) & ~15u;
-    q.ex[1] = q.ce[1] != q.ce[0] && (q.rhi & 15u);
-    q.pa[0] = q.rlo - q.ce[0];
-    q.pz[0] = (q.rhi < q.ce[0] + 16u ? q.rhi : q.ce[0] + 16u) - q.ce[0];
-    q.pa[1] = 0;
-    q.pz[1] = q.rhi - q.ce[1];
-    return q;
-}
-
-struct QuadSet {
-    u32x4 X[16];
-    u32x4 D[2][2];     // edge chunks: the 16-byte-aligned source blocks around their bytes
-    uint64_t sp;       // the piece's source of page byte 0 (only [rlo, rhi) dereferenced)
-    uint32_t pg, rr;   // page; rlo | rhi << 16
-    bool valid;        // a single-piece head of this batch (stores and the CRC enabled)
-};
-
-// Stores under a lane mask WITHOUT a branch around them: the compiler keeps an
-// s_cbranch_execz around any masked memory instruction, after which its vmcnt
-// waits turn conservative; an exec-masked store in one asm statement leaves
-// the control flow straight.  (The waitcnt pass does not see these stores: a
-// later wait can only over-wait for them, never under-wait.)
-template <int OFF>
-__device__ __forceinline__ void store_x4_if(bool c, u32x4 v, uint64_t addr) {
-    const uint64_t m = __ballot(c);
-    uint64_t sv;
-    asm volatile(
-        "s_and_saveexec_b64 %0, %1\n\t"
-        "global_store_dwordx4 %2, %3, off offset:%4 nt\n\t"
-        "s_mov_b64 exec, %0"
-        : "=&s"(sv)
-        : "s"(m), "v"(addr), "v"(v), "i"(OFF)
-        : "memory");
-}
-// rows J.. of a set: chunk stored iff the set's page is valid and the chunk
-// overlaps the piece (y0 + 256 J < lim)
-template <int J>
-__device__ __forceinline__ void store_rows(const u32x4 (&X)[16], bool valid, uint32_t y0, uint32_t lim, uint64_t P) {
-    if constexpr (J < 16) {
-        store_x4_if<256 * J>(valid && y0 + 256u * J < lim, X[J], P);
-        store_rows<J + 1>(X, valid, y0, lim, P);
-    }
-}
-__device__ __forceinline__ void store_x1_if(bool c, uint32_t v, uint64_t addr) {
-    const uint64_t m = __ballot(c);
-    uint64_t sv;
-    asm volatile(
-        "s_and_saveexec_b64 %0, %1\n\t"
-        "global_store_dword %2, %3, off\n\t"
-        "s_mov_b64 exec, %0"
-        : "=&s"(sv)
-        : "s"(m), "v"(addr), "v"(v)
-        : "memory");
-}
-
-__device__ __forceinline__ uint32_t bperm(uint32_t src_lane, uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
-}
-
-__global__ __launch_bounds__(64 * kQuadWaves) void log_quad_kernel(LogLaunch a) {
-    __shared__ uint32_t tab[kLdsBytes / 4];
-    constexpr int WV = kQuadWaves;
-    // an equal share of the heads per workgroup; a workgroup without one leaves
-    // before filling LDS
-    const uint32_t Hall = *a.head_count;
-    const uint32_t hb0 = (uint32_t)((uint64_t)Hall * blockIdx.x / gridDim.x);
-    const uint32_t hb1 = (uint32_t)((uint64_t)Hall * (blockIdx.x + 1) / gridDim.x);
-    if (hb0 < hb1) {
-        fill_lds<64 * WV>(tab, static_cast<const uint4*>(a.image));
-        const uint32_t lane = threadIdx.x & 63u;
-        const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        const uint32_t g = lane >> 4, i = lane & 15u;
-        const uint32_t c0 = lane << 2 & 0x7Cu, c1 = c0 | 0x10000u;
-        const uint32_t rot = (g + 2u * (i >> 3)) & 3u;  // final-map order: conflict-free columns
-        const uint32_t rot1 = 0u - (rot & 1u), rot2 = 0u - ((rot >> 1) & 1u);
-        uint32_t cfq[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) cfq[k] = kFinBase + 4u * (4u * i + ((k + rot) & 3u));
-        // the workgroup's heads cut among its waves by SIMD age (wave t: the
-        // (t / 4)-th oldest on SIMD t % 4; the SIMD issues oldest-first)
-        constexpr uint32_t kSkew[2] = {CC_QUAD_SKEW_W0, CC_QUAD_SKEW_W1};
-        auto wprefix = [&](uint32_t t) {
-            uint32_t p = 0;
-            for (uint32_t u = 0; u < t; u++) p += kSkew[(u / 4) & 1];
-            return p;
-        };
-        const uint32_t Hb = hb1 - hb0, wsum = wprefix(WV);
-        const uint32_t first = hb0 + (uint32_t)((uint64_t)Hb * wprefix(wave) / wsum);
-        const uint32_t H = hb0 + (uint32_t)((uint64_t)Hb * wprefix(wave + 1) / wsum);
-        const uint64_t pool = (uint64_t)(uintptr_t)a.pool;
-        const uint64_t dummy = (uint64_t)(uintptr_t)a.image + 4096ull * ((blockIdx.x * WV + wave) % (kLdsBytes / 4096));
-        for (uint32_t base = first; base < H; base += 64u) {
-            // metadata of up to 64 heads, lane k <- head base + k (clamped: every
-            // lane holds a real page and piece, so any lane's values address memory)
-            const uint32_t ih = base + lane;
-            const bool hv = ih < H;
-            const uint32_t hslot = a.heads[hv ? ih : base];
-            const unsigned long long ent = reinterpret_cast<const unsigned long long*>(a.table)[hslot];
-            if (a.done && hv) a.table[hslot] = 0ull;  // one head per page: the slot is this lane's alone
-            const uint32_t key = (uint32_t)(ent >> 32) - 1u;
-            const uint32_t pfirst = (uint32_t)ent - 1u;
-            const uint32_t nxt = a.next[pfirst];
-            const uint32_t u0 = pfirst / a.slots;
-            const UpdateDesc d = a.upd[u0];
-            const Piece hp = piece_in_page((uint64_t)key * 4096u, 4096u, d.dst, d.src, d.len, a.src);
-            const uint32_t hrr = hp.rlo | hp.rhi << 16;
-            const uint64_t hsp = (uint64_t)(uintptr_t)hp.sp;
-            const uint32_t cnt = (uint32_t)__popcll(__ballot(hv));
-            const uint64_t singles = __ballot(hv && nxt == kNoPiece);
-            const uint64_t multis = __ballot(hv && nxt != kNoPiece);
-            const uint32_t nq = (cnt + 3u) / 4u;
-
-            auto issue = [&](QuadSet& Y, uint32_t t) {
-                // nothing of the other set's merge/hash is scheduled into the
-                // loads (their waits would hold the loads back)
-                __builtin_amdgcn_sched_barrier(0);
-                // a set past the batch (t >= nq) issues the same loads, all into
-                // 4 KiB of the device LDS image (L2-resident: the workgroups filled
-                // their LDS from it), a different 4 KiB per wave so no L2 line is
-                // a hot spot; it stores nothing
-                const bool live = t < nq;
-                const uint32_t h = (4u * t + g) & 63u;
-                Y.pg = live ? bperm(h, key) : 0u;
-                Y.rr = live ? bperm(h, hrr) : 0u;  // empty piece: every row from P, no edge needed
-                Y.sp = live ? (uint64_t)bperm(h, (uint32_t)hsp) | (uint64_t)bperm(h, (uint32_t)(hsp >> 32)) << 32
-                            : dummy;
-                Y.valid = live && ((singles >> h) & 1ull);
-                const QuadGeo q = quad_geo(Y.rr);
-                const uint64_t P = (live ? pool + (uint64_t)Y.pg * 4096u : dummy) + 16u * i;
-                const uint64_t S = Y.sp + 16u * i;
-                const uint32_t len = q.rhi - q.rlo, l15 = len >= 16u ? len - 15u : 0u;
-                const uint32_t x0 = 16u * i - q.rlo;  // wrapping: chunk i of row j is whole in the piece
-#pragma unroll                                       //   iff x0 + 256 j < len - 15
-                for (int j = 0; j < 16; j++) {
-                    uint64_t b = x0 + 256u * j < l15 ? S : P;
-                    asm("" : "+v"(b));  // the row offset goes into the instruction's offset field
-#if CC_QUAD_ROW_NT
-                    Y.X[j] = __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(b) + 16 * j);
-#else
-                    Y.X[j] = reinterpret_cast<const gu32x4*>(b)[16 * j];
-#endif
-                }
-                // edge chunks: the two 16-byte-aligned source blocks around the
-                // chunk's source bytes; a block holding none of the piece's bytes
-                // loads the block holding its first byte instead (an aligned block
-                // never crosses a page, so no load leaves the pages of the source)
-                const uint64_t safe = (Y.sp + q.rlo) & ~15ull;
-#pragma unroll
-                for (int e = 0; e < 2; e++) {
-                    const uint64_t sc = Y.sp + q.ce[e];
-                    const uint32_t sh = (uint32_t)sc & 15u;
-                    const uint64_t B = sc - sh;
-#pragma unroll
-                    for (int m = 0; m < 2; m++) {
-                        const int32_t lo = 16 * m - (int32_t)sh;  // chunk-relative start of block m
-                        const bool need = q.ex[e] && lo + 16 > (int32_t)q.pa[e] && lo < (int32_t)q.pz[e];
-                        uint64_t ad = need ? B + 16u * m : safe;
-                        Y.D[e][m] = *reinterpret_cast<const gu32x4*>(ad);
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            };
-            auto compute = [&](QuadSet& Y) {
-                const QuadGeo q = quad_geo(Y.rr);
-                // edge chunks spliced in under their byte masks (lane owning edge e only)
-#pragma unroll
-                for (int e = 0; e < 2; e++) {
-                    const uint32_t sh = ((uint32_t)Y.sp + q.ce[e]) & 15u;
-                    const bool own = q.ex[e] && ((q.ce[e] >> 4) & 15u) == i;
-                    const uint32_t row = own ? q.ce[e] >> 8 : 0xFFu;
-                    // the 8 source dwords, shifted down by sh >> 2 dwords (two select
-                    // stages), then by sh & 3 bytes
-                    const uint32_t F[8] = {Y.D[e][0].x, Y.D[e][0].y, Y.D[e][0].z, Y.D[e][0].w,
-                                           Y.D[e][1].x, Y.D[e][1].y, Y.D[e][1].z, Y.D[e][1].w};
-                    // masks, not conditions: `c ? F[m + 1] : F[m]` becomes a dynamic
-                    // index (a scratch array)
-                    const uint32_t s4 = 0u - ((sh >> 2) & 1u), s8 = 0u - ((sh >> 3) & 1u);
-                    uint32_t F1[7], F2[5];
-#pragma unroll
-                    for (int m = 0; m < 7; m++) F1[m] = (F[m + 1] & s4) | (F[m] & ~s4);
-#pragma unroll
-                    for (int m = 0; m < 5; m++) F2[m] = (F1[m + 2] & s8) | (F1[m] & ~s8);
-                    uint32_t v[4], mk[4];
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        v[k] = __builtin_amdgcn_alignbyte(F2[k + 1], F2[k], sh & 3u);
-                        mk[k] = chunk_dword_mask(q.pa[e], q.pz[e], k);
-                    }
-#pragma unroll
-                    for (int j = 0; j < 16; j++) {
-                        const bool at = row == (uint32_t)j;
-#pragma unroll
-                        for (int k = 0; k < 4; k++) {
-                            const uint32_t m = at ? mk[k] : 0u;
-                            Y.X[j][k] = (v[k] & m) | (Y.X[j][k] & ~m);
-                        }
-                    }
-                }
-                // changed chunks back to the pool (rows of the pages this set owns)
-                const uint64_t P = pool + (uint64_t)Y.pg * 4096u + 16u * i;
-                const uint32_t len = q.rhi - q.rlo;
-                const uint32_t y0 = 16u * i + 15u - q.rlo;  // chunk overlaps the piece iff y0 + 256 j < len + 15
-                store_rows<0>(Y.X, Y.valid, y0, len + 15u, P);
-                // four Horner chains per lane, interleaved
-                uint32_t s[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) s[k] = Y.X[0][k];
-#pragma unroll
-                for (int j = 1; j < 16; j++)
-#pragma unroll
-                    for (int k = 0; k < 4; k++) s[k] = apply_g_xor(tab, s[k], Y.X[j][k], c0, c1);
-                // rotate the states by rot (s'[k] = s[(k + rot) & 3]: two selects
-                // per state), then chain k' reads column 4 i + ((k' + rot) & 3)
-                uint32_t s1[4], s2[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) s1[k] = (s[(k + 1) & 3] & rot1) | (s[k] & ~rot1);
-#pragma unroll
-                for (int k = 0; k < 4; k++) s2[k] = (s1[(k + 2) & 3] & rot2) | (s1[k] & ~rot2);
-                uint32_t r = 0;
-#pragma unroll
-                for (int k = 0; k < 4; k++) r ^= apply_fin(tab, s2[k], cfq[k]);
-                r ^= __builtin_amdgcn_mov_dpp(r, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-                r ^= __builtin_amdgcn_mov_dpp(r, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-                r ^= __builtin_amdgcn_mov_dpp(r, 0x124, 0xF, 0xF, false);  // row_ror:4
-                r ^= __builtin_amdgcn_mov_dpp(r, 0x128, 0xF, 0xF, false);  // row_ror:8
-                store_x1_if(Y.valid && i == 0, r ^ a.kconst, (uint64_t)(uintptr_t)(a.page_crcs + Y.pg));
-            };
-            // both sets in flight on entry, as on the back edge (the same
-            // outstanding loads on every edge into the loop keep its waits exact)
-            // one exit (the loop test) and the same loads on every edge: the
-            // compiler's vmcnt waits stay exact (early breaks made it over-wait a
-            // whole set); a set past the batch loads page 0 again and stores nothing
-            QuadSet SA, SB;
-            issue(SA, 0);
-            issue(SB, 1);
-            for (uint32_t t = 0; t < nq; t += 2) {
-                compute(SA);
-                issue(SA, t + 2);
-                if (t + 1 < nq) compute(SB);  // no compiler-visible memory instruction inside
-                issue(SB, t + 3);
-            }
-            // pages with several pieces: one per wave
-            for (uint64_t m = multis; m; m &= m - 1) {
-                const uint32_t h = (uint32_t)__builtin_ctzll(m);
-                log_page_multi<16, false>(a, tab, __builtin_amdgcn_readlane(key, h), __builtin_amdgcn_readlane(u0, h),
-                                          __builtin_amdgcn_readlane(nxt, h), lane);
-            }
-        }
-    }
-    if (a.done) {
-        // every thread has read head_count; the last block out leaves the
-        // counters zero for the next call
-        __syncthreads();
-        if (threadIdx.x == 0 && atomicAdd(a.done, 1u) == gridDim.x - 1) {
-            atomicExch(a.head_count, 0u);
-            atomicExch(a.done, 0u);
-        }
-    }
-}
-
 // A small log (<= 64 writes of <= one page each: at most 2 pieces a write) in
 // ONE launch, for the per-request latency of the write path: no table memset,
 // no insert.  Every wave loads the log into its lanes and finds the distinct
@@ -2447,12 +2043,6 @@ hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s) {
             hipLaunchKernelGGL((log_pages_kernel<MM, false>), dim3(a.blocks), dim3(64 * log_waves(MM, false)), 0, \
                                s, a);                                                                       \
         break;
-#if CC_LOG_QUAD
-    if (a.page_bytes == 4096 && !a.delta) {
-        hipLaunchKernelGGL(log_quad_kernel, dim3(a.blocks), dim3(64 * kQuadWaves), 0, s, a);
-        return hipGetLastError();
-    }
-#endif
     switch (a.page_bytes / kWaveBytes) {
         CC_GCASE(1)
         CC_GCASE(2)
