@@ -803,6 +803,12 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(RangeLaunch
         Pos pD = pC;
         uint32_t s = 0;
         uint32_t segk = 0;  // block of the range the current segment began at
+        // split-range segments of this item (at most its first and its last):
+        // their accumulator atomics return values, and waiting on a returning
+        // atomic waits for every load issued before it -- so they run after
+        // the ring, when nothing is in flight (inside it: +1.8 % a batch)
+        uint64_t seg_r0 = 0, seg_r1 = 0;
+        uint32_t seg_v0 = 0, seg_v1 = 0, seg_n0 = 0, seg_n1 = 0, seg_nb0 = 0, seg_nb1 = 0, nseg = 0;
         auto step = [&](uint32_t (&X)[17], const Pos& px, uint32_t (&Y)[17], const Pos& py) {
             load_range_block(Y, buf, py.g, py.k, lane, xr, py.real);
             const RangeGeo& gx = px.g;
@@ -826,19 +832,20 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(RangeLaunch
                 const uint32_t bit = lane < 32u ? (raw_pad >> (31u - lane)) & 1u : 0u;
                 uint32_t v = end ? wave_xor(bit ? X[16] : 0u) : mulmod_small(pw, raw_pad);
                 if (end) v ^= gx.len >= 4 ? 0xFFFFFFFFu : ~mulmod_small(pw, 0xFFFFFFFFu);
-                if (lane == 0) {
-                    if (end && segk == 0) {
-                        out[px.r] = v;
-                    } else {  // one segment of a split range (rare: <= 2 an item)
-                        uint32_t* acc = a.acc + 2 * px.r;
-                        const uint32_t nblk = kx + 1 - segk;
-                        const uint32_t x = atomicXor(acc, v);
-                        asm volatile("" ::"v"(x) : "memory");  // the XOR is performed before the count says so
-                        if (atomicAdd(acc + 1, nblk) + nblk == gx.nb) {  // the range's last segment
-                            out[px.r] = atomicExch(acc, 0u);
-                            atomicExch(acc + 1, 0u);
-                        }
-                    }
+                if (end && segk == 0) {
+                    if (lane == 0) out[px.r] = v;
+                } else {  // a segment of a split range: the item's first and/or last, met after the ring
+                    // (selects, not an index: a dynamically indexed array lives in scratch)
+                    const bool second = nseg != 0;
+                    seg_r1 = second ? px.r : seg_r1;
+                    seg_v1 = second ? v : seg_v1;
+                    seg_n1 = second ? kx + 1 - segk : seg_n1;
+                    seg_nb1 = second ? gx.nb : seg_nb1;
+                    seg_r0 = second ? seg_r0 : px.r;
+                    seg_v0 = second ? seg_v0 : v;
+                    seg_n0 = second ? seg_n0 : kx + 1 - segk;
+                    seg_nb0 = second ? seg_nb0 : gx.nb;
+                    nseg++;
                 }
             }
         };
@@ -856,6 +863,20 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(RangeLaunch
             pC = adv(pB);
             step(Dq, pD, Cq, pC);
         }
+        // the item's split segments meet in their ranges' accumulator pairs:
+        // XOR in, then add the blocks; the add that completes the range takes
+        // the XOR, stores it and leaves the pair zero
+        auto meet = [&](uint64_t r, uint32_t v, uint32_t nblk, uint32_t nb) {
+            uint32_t* acc = a.acc + 2 * r;
+            const uint32_t x = atomicXor(acc, v);
+            asm volatile("" ::"v"(x) : "memory");  // the XOR is performed before the count says so
+            if (atomicAdd(acc + 1, nblk) + nblk == nb) {
+                out[r] = atomicExch(acc, 0u);
+                atomicExch(acc + 1, 0u);
+            }
+        };
+        if (lane == 0 && nseg > 0) meet(seg_r0, seg_v0, seg_n0, seg_nb0);
+        if (lane == 0 && nseg > 1) meet(seg_r1, seg_v1, seg_n1, seg_nb1);
     }
 }
 
