@@ -683,8 +683,9 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(RangeLaunch
     // the tail's counter: slot epoch % 2 of the block; this call zeroes the
     // other slot for the stream's next call (nobody here touches it), so no
     // wave has to count arrivals at the end to reset it
-    unsigned long long* dyn_ctr = a.tail + (a.epoch & 1u) * kDynHeadStride;
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(a.tail + ((a.epoch + 1u) & 1u) * kDynHeadStride, 0ull);
+    unsigned long long* dyn_ctr = a.tail + (a.epoch & 1u) * kDynCtrWords64;
+    if (blockIdx.x == 0 && threadIdx.x < kRangeHeads)
+        atomicExch(a.tail + ((a.epoch + 1u) & 1u) * kDynCtrWords64 + threadIdx.x * kDynHeadStride, 0ull);
     uint32_t dyn_head, dyn_tried;
     tail_cursor<kRangeHeads>(dyn_head, dyn_tried);
 
