@@ -709,6 +709,7 @@ int cc_shift_dev(const uint32_t* d_crcs, const uint64_t* d_shift_bytes, uint64_t
     return map_err(launch_shift(d_crcs, d_shift_bytes, n, d_out, static_cast<hipStream_t>(stream)));
 }
 
+extern "C++" {
 namespace {
 // The stream's range scratch: kRangeTiles tile words, the tail block, then the
 // accumulator pairs of up to `cap` ranges; zero when created (cleared on the
@@ -750,6 +751,45 @@ DevCtx::RangeWork* range_work(DevCtx* c, hipStream_t s, uint64_t n, hipError_t* 
     return t;
 }
 
+// The stream's range scratch for one launch: the tile words, the tail slots,
+// `n_acc` accumulator pairs, and the call's epoch, handed to launch(tiles,
+// tail, acc, epoch) under c->range_mu (the epoch order is the stream order).
+// Scratch of the call's own (allocated and cleared on the stream) when the
+// stream has none cached for that size.
+template <typename F>
+hipError_t with_range_scratch(DevCtx* c, hipStream_t s, uint64_t n_acc, F launch) {
+    std::lock_guard<std::mutex> lk(c->range_mu);
+    hipError_t e;
+    DevCtx::RangeWork* w = range_work(c, s, n_acc, &e);
+    if (e != hipSuccess) return e;
+    unsigned char* base = nullptr;
+    unsigned char* tmp = nullptr;
+    uint32_t epoch = 1;
+    if (w) {
+        base = w->p;
+        // 24-bit epochs; the wrap keeps the parity alternating (2^24 - 1 is odd:
+        // next 2), as the tail's counter slots need
+        w->epoch = w->epoch + 1 < (1u << 24) ? w->epoch + 1 : 2u;
+        epoch = w->epoch;
+    } else {
+        const uint64_t bytes = kRangeHeader + n_acc * 8;
+        if ((e = hipMallocAsync(reinterpret_cast<void**>(&tmp), bytes, s)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(tmp, 0, bytes, s)) != hipSuccess) {
+            (void)hipFreeAsync(tmp, s);
+            return e;
+        }
+        base = tmp;
+    }
+    e = launch(reinterpret_cast<uint64_t*>(base), reinterpret_cast<unsigned long long*>(base + kRangeTiles * 8),
+               reinterpret_cast<uint32_t*>(base + kRangeHeader), epoch);
+    if (w && e != hipSuccess) w->dirty = true;  // may have run in part: clear before the next use
+    if (tmp) {
+        const hipError_t f = hipFreeAsync(tmp, s);
+        if (e == hipSuccess) e = f;
+    }
+    return e;
+}
+
 // One range batch (the flat kernel, kernels.h launch_range_flat) on stream s.
 hipError_t range_batch(DevCtx* c, const unsigned char* buf, const RangeDesc* rd, uint64_t n, uint32_t* out,
                        hipStream_t s) {
@@ -761,40 +801,16 @@ hipError_t range_batch(DevCtx* c, const unsigned char* buf, const RangeDesc* rd,
     a.image = c->image;
     a.out = out;
     a.blocks = c->cus;
-    std::lock_guard<std::mutex> lk(c->range_mu);
-    hipError_t e;
-    DevCtx::RangeWork* w = range_work(c, s, n, &e);
-    if (e != hipSuccess) return e;
-    unsigned char* base = nullptr;
-    unsigned char* tmp = nullptr;
-    if (w) {
-        base = w->p;
-        // 24-bit epochs; the wrap keeps the parity alternating (2^24 - 1 is odd:
-        // next 2), as the tail's counter slots need
-        w->epoch = w->epoch + 1 < (1u << 24) ? w->epoch + 1 : 2u;
-        a.epoch = w->epoch;
-    } else {  // scratch of this call's own, cleared
-        const uint64_t bytes = kRangeHeader + n * 8;
-        if ((e = hipMallocAsync(reinterpret_cast<void**>(&tmp), bytes, s)) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(tmp, 0, bytes, s)) != hipSuccess) {
-            (void)hipFreeAsync(tmp, s);
-            return e;
-        }
-        base = tmp;
-        a.epoch = 1;
-    }
-    a.tiles = reinterpret_cast<uint64_t*>(base);
-    a.tail = reinterpret_cast<unsigned long long*>(base + kRangeTiles * 8);
-    a.acc = reinterpret_cast<uint32_t*>(base + kRangeHeader);
-    e = launch_range_flat(a, s);
-    if (w && e != hipSuccess) w->dirty = true;  // may have run in part: clear before the next use
-    if (tmp) {
-        const hipError_t f = hipFreeAsync(tmp, s);
-        if (e == hipSuccess) e = f;
-    }
-    return e;
+    return with_range_scratch(c, s, n, [&](uint64_t* tiles, unsigned long long* tail, uint32_t* acc, uint32_t epoch) {
+        a.tiles = tiles;
+        a.tail = tail;
+        a.acc = acc;
+        a.epoch = epoch;
+        return launch_range_flat(a, s);
+    });
 }
 }  // namespace
+}  // extern "C++"
 
 int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, uint32_t* d_out, void* stream) {
     if (n == 0) return CC_OK;
@@ -1247,11 +1263,11 @@ int cc_apply_log_delta_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_byte
                      work_bytes, stream, 1);
 }
 
+// The engine holds the schedule scratch (the stream's range scratch); d_work is
+// kept in the ABI (a caller sized it with this function) and not used.
 uint64_t cc_verify_reads_work_bytes(uint64_t n_reads) {
     if (n_reads == 0 || n_reads >= (1ull << 31)) return 0;
-    const size_t temp = scan_temp_bytes(n_reads);
-    if (!temp) return 0;
-    return 2 * align256(n_reads * 8) + align256(temp) + align256(kDynCtrBytes);  // + the dynamic-tail heads
+    return 256;
 }
 
 int cc_verify_reads_dev(const void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const cc_range* d_reads,
@@ -1267,33 +1283,30 @@ int cc_verify_reads_dev(const void* d_pool, uint64_t pool_bytes, uint32_t page_b
     int rc = get_ctx(&c);
     if (rc) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    unsigned char* w = static_cast<unsigned char*>(d_work);
     ReadVerifyLaunch a = {};
     a.pool = static_cast<const uint32_t*>(d_pool);
     a.pool_bytes = pool_bytes;
     a.page_bytes = page_bytes;
+    a.page_shift = (uint32_t)__builtin_ctz(page_bytes);  // a power of two (log_page_ok)
     a.reads = reinterpret_cast<const RangeDesc*>(d_reads);
     a.n_reads = n_reads;
-    a.counts = reinterpret_cast<uint64_t*>(w);
-    a.start = reinterpret_cast<uint64_t*>(w + align256(n_reads * 8));
-    void* temp = w + 2 * align256(n_reads * 8);
-    const size_t temp_bytes = align256(scan_temp_bytes(n_reads));
-    a.dyn_ctr = reinterpret_cast<unsigned long long*>(w + 2 * align256(n_reads * 8) + temp_bytes);
     a.page_crcs = d_page_crcs;
     a.bad_per_read = d_bad_per_read;
     a.bad_total = reinterpret_cast<unsigned long long*>(d_bad_total);
     a.image = c->image;
     a.kconst = kconst_for(page_bytes);
-    a.blocks = c->cus;  // every wave takes an equal share of the (device-computed) page slots
-    hipError_t e;
-    // batches of up to 64 reads take the one-launch path (page counts summed in
+    a.blocks = c->cus;  // every wave takes an equal share of the (device-counted) page slots
+    // batches of up to 64 reads take the one-launch small path (page counts summed in
     // 32 bits there: pools of < 2^26 pages keep 64 reads' sum exact)
     if (n_reads <= 64 && pool_bytes / page_bytes < (1ull << 26))
         return map_err(launch_read_verify_small(a, s));
-    if ((e = launch_read_counts(a, s)) != hipSuccess) return map_err(e);
-    if ((e = exclusive_scan_u64(temp, temp_bytes, a.counts, a.start, n_reads, s)) != hipSuccess)
-        return map_err(e);
-    return map_err(launch_read_verify(a, s));
+    return map_err(with_range_scratch(c.get(), s, 0,
+                                      [&](uint64_t* tiles, unsigned long long* tail, uint32_t*, uint32_t epoch) {
+                                          a.tiles = tiles;
+                                          a.tail = tail;
+                                          a.epoch = epoch;
+                                          return launch_read_verify(a, s);
+                                      }));
 }
 
 // Streaming scan.  Each staging slot holds a batch of whole chunks (data and

@@ -149,31 +149,29 @@ struct RangeDesc {
 };
 
 // Verify-on-read for a batch of reads (cc_verify_reads_dev): every page a read
-// touches is a "slot"; slots of read i start at start[i] (exclusive scan of the
-// per-read page counts); each wave rehashes the reads starting in an equal
-// share of the slots.
+// touches is a "slot"; the batch's slots are read 0's pages, then read 1's, ...;
+// ONE launch on the range kernel's schedule: the waves count kRangeTiles tiles
+// of reads themselves (epoch-tagged words in the stream's range scratch) and
+// each rehashes an equal share of the slots, the last 1/16 dynamically.
 struct ReadVerifyLaunch {
     const uint32_t* pool;
     uint64_t pool_bytes;
     uint32_t page_bytes;
+    uint32_t page_shift;        // log2(page_bytes)
     const RangeDesc* reads;
     uint64_t n_reads;
-    uint64_t* counts;           // [n_reads] pages per read
-    uint64_t* start;            // [n_reads] exclusive scan of counts
     const uint32_t* page_crcs;  // stored CRC per pool page
     uint32_t* bad_per_read;     // [n_reads] += mismatching pages; UINT32_MAX for a read beyond the pool
     unsigned long long* bad_total;
-    unsigned long long* dyn_ctr;  // dynamic-tail chunk counter (zeroed by the count kernel)
+    uint64_t* tiles;            // [kRangeTiles] epoch << 40 | pages of the tile
+    unsigned long long* tail;   // dynamic-tail counter slots (epoch % 2: this call's; the other zeroed for the next)
+    uint32_t epoch;
     const void* image;
     uint32_t kconst;
     int blocks;
 };
-hipError_t launch_read_counts(const ReadVerifyLaunch& a, hipStream_t s);
-size_t scan_temp_bytes(uint64_t n);
-hipError_t exclusive_scan_u64(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
-                              hipStream_t s);
 hipError_t launch_read_verify(const ReadVerifyLaunch& a, hipStream_t s);
-// <= 64 reads in one launch (no counts / scan; pages split over waves)
+// <= 64 reads in one launch (no tiles; pages split over waves)
 hipError_t launch_read_verify_small(const ReadVerifyLaunch& a, hipStream_t s);
 // CRC32C (butil Value) of arbitrary byte ranges of one device buffer, on the
 // flat block schedule, ONE launch: range_flat_kernel counts the

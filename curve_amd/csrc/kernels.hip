@@ -609,6 +609,68 @@ __device__ __forceinline__ uint64_t wave_scan_incl(uint64_t v, uint32_t lane) {
     return v;
 }
 
+// Every tile count of this call into tb (lane l: tiles kTpl*l .. kTpl*l + kTpl-1):
+// poll the epoch-tagged words (sc1 loads: a data-tagged granule needs no
+// fence), and count a tile whose word is still missing after kTileWaitTicks
+// with count(t) -- its workgroup is not running, and no wave waits on another
+// without a bound.
+template <int kTpl, typename Count>
+__device__ __forceinline__ void wait_tiles(uint64_t (&tb)[kTpl], const uint64_t* tiles, uint64_t tag, uint32_t lane,
+                                           Count count) {
+    constexpr uint64_t kCountMask = (1ull << kEpochShift) - 1;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t have = 0;  // bit j: tb[j] holds this call's count
+    for (;;) {
+#pragma unroll
+        for (int j = 0; j < kTpl; j++) {
+            const uint64_t v = __hip_atomic_load(tiles + kTpl * lane + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool ok = (v & ~kCountMask) == tag;
+            tb[j] = ok ? v & kCountMask : tb[j];
+            have |= ok ? 1u << j : 0u;
+        }
+        if (!__ballot(have != (1u << kTpl) - 1u)) return;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kTileWaitTicks) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+#pragma unroll
+    for (int j = 0; j < kTpl; j++) {
+        for (uint64_t m = __ballot(!((have >> j) & 1u)); m; m &= m - 1) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(m);
+            const uint64_t cnt = count(kTpl * l + j);
+            tb[j] = lane == l ? cnt : tb[j];
+        }
+    }
+}
+
+// The tile holding unit u of the stream, and the units before it: lane tl's
+// tiles (cum = inclusive prefix of the lanes' sums), then the first of them
+// whose running count passes u.
+struct TileHit {
+    uint32_t tile;
+    uint64_t before;
+};
+template <int kTpl>
+__device__ __forceinline__ TileHit tile_of(uint64_t cum, const uint64_t (&tb)[kTpl], uint64_t u, uint32_t lane) {
+    const uint32_t tl = (uint32_t)__builtin_ctzll(__ballot(cum > u));
+    TileHit h;
+    h.before = tl ? readlane64(cum, tl - 1) : 0;
+    h.tile = kTpl * tl;
+    bool found = false;
+#pragma unroll
+    for (int j = 0; j < kTpl; j++) {
+        const uint64_t v = readlane64(tb[j], tl);
+        if (!found) {
+            if (h.before + v > u) {
+                found = true;
+                h.tile = kTpl * tl + j;
+            } else {
+                h.before += v;
+            }
+        }
+    }
+    return h;
+}
+
 constexpr int kFlatWaves = 8;  // waves per CU of the flat range kernel (A/B on WAL sizes: 8 beats 12 by ~4 %, 16 by ~10 %)
 constexpr uint32_t kRangeRounds = 2;  // static pieces per wave (A/B: 2 best; 1 loses on equal sizes, 8 on random)
 constexpr uint64_t kRangeDynDiv = 32;  // 1/32 of the blocks go to the dynamic tail (A/B: 1/8 and 1/16 lose to
@@ -643,36 +705,8 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(RangeLaunch
     // every tile count of this call: lane l holds tiles kTpl*l .. kTpl*l + kTpl-1,
     // cum = inclusive prefix of the lane sums
     constexpr int kTpl = kRangeTiles / 64;
-    constexpr uint64_t kCountMask = (1ull << kEpochShift) - 1;
     uint64_t tb[kTpl];
-    {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        uint32_t have = 0;  // bit j: tb[j] holds this call's count
-        for (;;) {
-#pragma unroll
-            for (int j = 0; j < kTpl; j++) {
-                const uint64_t v =
-                    __hip_atomic_load(a.tiles + kTpl * lane + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const bool ok = (v & ~kCountMask) == tag;
-                tb[j] = ok ? v & kCountMask : tb[j];
-                have |= ok ? 1u << j : 0u;
-            }
-            if (!__ballot(have != (1u << kTpl) - 1u)) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kTileWaitTicks) {
-                // a tile's wave is not running: count the missing tiles here
-#pragma unroll
-                for (int j = 0; j < kTpl; j++) {
-                    for (uint64_t m = __ballot(!((have >> j) & 1u)); m; m &= m - 1) {
-                        const uint32_t l = (uint32_t)__builtin_ctzll(m);
-                        const uint64_t cnt = range_tile_count(a, kTpl * l + j, lane, false);
-                        tb[j] = lane == l ? cnt : tb[j];
-                    }
-                }
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
+    wait_tiles<kTpl>(tb, a.tiles, tag, lane, [&](uint32_t t) { return range_tile_count(a, t, lane, false); });
     uint64_t lsum = 0;
 #pragma unroll
     for (int j = 0; j < kTpl; j++) lsum += tb[j];
@@ -704,23 +738,9 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(RangeLaunch
             b0 = Bs + c * kRangeDynBlocks;
             b1 = b0 + kRangeDynBlocks < B ? b0 + kRangeDynBlocks : B;
         }
-        // tile holding block b0: lane tl's tiles, then the first of them whose running count passes b0
-        const uint32_t tl = (uint32_t)__builtin_ctzll(__ballot(cum > b0));
-        uint64_t before = tl ? readlane64(cum, tl - 1) : 0;
-        uint32_t tile = kTpl * tl;
-        bool found = false;
-#pragma unroll
-        for (int j = 0; j < kTpl; j++) {
-            const uint64_t v = readlane64(tb[j], tl);
-            if (!found) {
-                if (before + v > b0) {
-                    found = true;
-                    tile = kTpl * tl + j;
-                } else {
-                    before += v;
-                }
-            }
-        }
+        const TileHit th = tile_of(cum, tb, b0, lane);
+        const uint32_t tile = th.tile;
+        const uint64_t before = th.before;
         // range holding block b0: the tile's ranges 64 at a time
         uint64_t r = n * tile / kRangeTiles;
         uint64_t rel = b0 - before;
@@ -1678,34 +1698,45 @@ __global__ __launch_bounds__(64 * log_small_waves(M, Delta)) void log_small_kern
 // ---------------------------------------------------------------------------
 // Verify-on-read for a batch of datastore reads (cc_verify_reads_dev)
 // ---------------------------------------------------------------------------
-// Pages each read touches (a read past the pool touches none and is marked).
-__global__ void read_counts_kernel(ReadVerifyLaunch a) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < kDynCtrWords64) a.dyn_ctr[i] = 0;  // read_verify_kernel's dynamic-tail heads
-    if (i >= a.n_reads) return;
-    const RangeDesc r = a.reads[i];
-    uint64_t c = 0;
-    if (r.off >= a.pool_bytes || r.len > a.pool_bytes - r.off) {
-        if (r.len) a.bad_per_read[i] = 0xFFFFFFFFu;
-    } else if (r.len) {
-        c = (r.off + r.len - 1) / a.page_bytes - r.off / a.page_bytes + 1;
-    }
-    a.counts[i] = c;
+// Pages a read touches (0 for an empty read and for one past the pool).
+__device__ __forceinline__ uint64_t read_pages(const ReadVerifyLaunch& a, const RangeDesc& r) {
+    if (!r.len || r.off >= a.pool_bytes || r.len > a.pool_bytes - r.off) return 0;
+    return ((r.off + r.len - 1) >> a.page_shift) - (r.off >> a.page_shift) + 1;
 }
 
-// Every page a read touches is one slot; read i owns slots start[i] ..
-// start[i] + counts[i] - 1 (start = exclusive scan of counts).  Wave w owns
-// the slots [T*w/W, T*(w+1)/W) at page granularity (a read may be split over
-// waves; its mismatches are counted by atomics), found with two 64-ary
-// searches over start[] (lanes probe 64 entries per round trip).  It takes its reads 64 at a
-// time (lane j <- one read: first page, page count) and lays their pages out
-// as one stream with a wave prefix sum: page k of the stream belongs to the
-// first lane whose running count exceeds k (a ballot), so the stream is walked
-// with uniform scalar math only -- no loads in the per-page path -- hashed with
-// the next two pages' loads in flight (three register sets rotating).  The
-// stored CRCs come in with VECTOR loads (an opaque zero in the address) so
-// they never share lgkmcnt with the chain's LDS lookups.  A mismatch is
-// counted on its read (rare: atomics).
+// Pages of tile t (reads [n t / T, n (t+1) / T)), uniform; mark: reads past the
+// pool get bad_per_read = UINT32_MAX (the tile's counting wave marks them).
+__device__ __forceinline__ uint64_t read_tile_count(const ReadVerifyLaunch& a, uint32_t t, uint32_t lane, bool mark) {
+    const uint64_t lo = a.n_reads * t / kRangeTiles, hi = a.n_reads * (t + 1) / kRangeTiles;
+    uint64_t sum = 0;
+    for (uint64_t i = lo + lane; i < hi; i += 64) {
+        const RangeDesc r = a.reads[i];
+        sum += read_pages(a, r);
+        if (mark && r.len && (r.off >= a.pool_bytes || r.len > a.pool_bytes - r.off)) a.bad_per_read[i] = 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int d = 32; d; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    return sum;
+}
+
+// Every page a read touches is one slot; the batch's slots are read 0's pages,
+// then read 1's, ...  ONE launch, scheduled as the range kernel is (§7): the
+// waves count kRangeTiles tiles of reads themselves (epoch-tagged words, a
+// bounded wait) and hold the counts in registers; wave w owns the slots
+// [Ts w / W, Ts (w+1) / W) at PAGE granularity (a read may be split over
+// waves; its mismatches are counted by atomics), the last T / kRvDynDiv slots
+// are dynamic chunks.  A share starts at the read holding its first slot
+// (tile search in registers, then the tile's reads 64 at a time); the wave
+// takes its reads 64 at a time (lane j <- one read: first page, page count)
+// and lays their pages out as one stream with a wave prefix sum: page k of
+// the stream belongs to the first lane whose running count exceeds k (a
+// ballot), so the stream is walked with uniform scalar math only -- no loads
+// in the per-page path -- hashed with the next two pages' loads in flight
+// (three register sets rotating).  The stored CRCs come in with VECTOR loads
+// (an opaque zero in the address) so they never share lgkmcnt with the chain's
+// LDS lookups.  A mismatch is counted on its read (rare: atomics).
+// (Rounds 2-3: a count kernel and rocPRIM's two-launch exclusive scan ran
+// first, 16-24 us of a 0.67 ms call.)
 constexpr int kRvWaves = 8;  // waves per CU of the verify-on-read kernel
 constexpr uint64_t kRvDynDiv = 16;  // 1/16 of the slots form the dynamic tail (A/B: 2-3 % over none; 1/8, 1/32 less)
 constexpr uint32_t kRvHeads = 1;  // tail heads (A/B round 3: 8 per-XCD heads = one counter at 1/16)
@@ -1716,42 +1747,40 @@ template <int M>
 __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLaunch a) {
     __shared__ uint32_t tab[kLdsBytes / 4];
     const uint64_t n = a.n_reads;
-    const uint64_t T = a.start[n - 1] + a.counts[n - 1];
-    // W waves share the slots: all of the grid for a large batch, fewer for a
-    // small one, and the blocks left without a share exit before filling LDS
-    const uint64_t Wg = (uint64_t)gridDim.x * kRvWaves, Wt = (T + kRvMinSlots - 1) / kRvMinSlots;
-    const uint64_t W = Wt < Wg ? (Wt ? Wt : 1) : Wg;
-    if ((uint64_t)blockIdx.x * kRvWaves >= W) return;  // uniform per block
-    fill_lds<64 * kRvWaves>(tab, static_cast<const uint4*>(a.image));
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t Wg = (uint64_t)gridDim.x * kRvWaves;
+    const uint64_t w = (uint64_t)blockIdx.x * kRvWaves + wave;
+    const uint64_t tag = (uint64_t)a.epoch << kEpochShift;
+    // this wave's tile counts, published before the LDS fill
+    for (uint64_t t = w; t < kRangeTiles; t += Wg) {
+        const uint64_t cnt = read_tile_count(a, (uint32_t)t, lane, true);
+        if (lane == 0) __hip_atomic_store(a.tiles + t, tag | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the tail's counter: slot epoch % 2; this call zeroes the other for the next
+    unsigned long long* dyn_ctr = a.tail + (a.epoch & 1u) * kDynCtrWords64;
+    if (blockIdx.x == 0 && threadIdx.x < kRvHeads)
+        atomicExch(a.tail + ((a.epoch + 1u) & 1u) * kDynCtrWords64 + threadIdx.x * kDynHeadStride, 0ull);
+    fill_lds<64 * kRvWaves>(tab, static_cast<const uint4*>(a.image));
     const uint32_t c0 = lane << 2 & 0x7Cu;
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
     const uint32_t* pages = a.pool + lane;
-    const uint64_t w = (uint64_t)blockIdx.x * kRvWaves + wave;
     uint32_t vz = 0;
     asm volatile("" : "+v"(vz));  // opaque zero: keeps uniform-address loads on the vector path
-    // first read whose first slot is >= target (n if none): 64-ary search
-    auto lower_bound = [&](uint64_t target) -> uint64_t {
-        uint64_t lo = 0, hi = n;  // answer in [lo, hi]
-        while (lo < hi) {
-            const uint64_t step = (hi - lo + 63) / 64;
-            const uint64_t idx = lo + (uint64_t)lane * step;
-            const bool probe = idx < hi;
-            const uint64_t st = a.start[(probe ? idx : lo) + vz];
-            const uint64_t lt = __ballot(probe && st < target);  // a prefix of the probes
-            if (!lt) {
-                hi = lo;
-                break;
-            }
-            const uint32_t j = 63u - (uint32_t)__builtin_clzll(lt);
-            lo = lo + (uint64_t)j * step + 1;
-            const uint64_t nh = lo - 1 + step;
-            hi = nh < hi ? nh : hi;
-        }
-        return lo;
-    };
+
+    constexpr int kTpl = kRangeTiles / 64;
+    uint64_t tb[kTpl];
+    wait_tiles<kTpl>(tb, a.tiles, tag, lane, [&](uint32_t t) { return read_tile_count(a, t, lane, false); });
+    uint64_t lsum = 0;
+#pragma unroll
+    for (int j = 0; j < kTpl; j++) lsum += tb[j];
+    const uint64_t cum = wave_scan_incl(lsum, lane);
+    const uint64_t T = readlane64(cum, 63);
+    // W waves share the slots: all of the grid for a large batch, fewer for a small one
+    const uint64_t Wt = (T + kRvMinSlots - 1) / kRvMinSlots;
+    const uint64_t W = Wt < Wg ? (Wt ? Wt : 1) : Wg;
+    if ((uint64_t)blockIdx.x * kRvWaves >= W) return;  // uniform per block: no share, no tail
     auto stored_crc = [&](uint64_t g) { return a.page_crcs[g + vz]; };
     // static shares of the first Ts slots, then dynamic chunks of kRvDynSlots
     // slots (the page kernel's tail: the XCDs run at different rates)
@@ -1762,30 +1791,42 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
 #pragma unroll 1
     for (;;) {
         // slots [lo_slot, hi_slot) at PAGE granularity: from the read holding
-        // slot lo_slot (the last read whose first slot is <= it) through the
-        // reads starting before hi_slot, cut at both ends
-        const uint64_t rb = lo_slot < hi_slot ? lower_bound(lo_slot + 1) - 1 : 0;
-        const uint64_t re = lo_slot < hi_slot ? lower_bound(hi_slot) : 0;
-        for (uint64_t base = rb; base < re; base += 64) {
+        // slot lo_slot through the reads starting before hi_slot, cut at both ends
+        uint64_t base = n, S = 0;  // the group's first read and the slot of its page 0
+        if (lo_slot < hi_slot) {
+            const TileHit th = tile_of(cum, tb, lo_slot, lane);
+            base = n * th.tile / kRangeTiles;
+            S = th.before;
+            // the tile's reads 64 at a time, to the group whose pages pass lo_slot
+            for (;;) {
+                const uint64_t ri = base + lane;
+                const uint64_t c = wave_scan_incl(ri < n ? read_pages(a, a.reads[ri]) : 0u, lane);
+                const uint64_t tot = readlane64(c, 63);
+                if (S + tot > lo_slot || base + 64 >= n) break;
+                S += tot;
+                base += 64;
+            }
+        }
+        for (; base < n && S < hi_slot; base += 64) {
             const uint64_t ri = base + lane;
-            const bool valid = ri < re;
+            const bool valid = ri < n;
             const RangeDesc r = a.reads[(valid ? ri : base) + vz];
-            const uint32_t cnt = valid ? (uint32_t)a.counts[ri] : 0u;  // 0 also for reads past the pool
-            const uint64_t S = readlane64(a.start[base + vz], 0);      // slot of the group's page 0
-            const uint64_t p0 = r.off / a.page_bytes;
-            uint32_t cum = cnt;  // inclusive prefix sum over the lanes
+            const uint32_t cnt = valid ? (uint32_t)read_pages(a, r) : 0u;  // 0 also for reads past the pool
+            const uint64_t p0 = r.off >> a.page_shift;
+            uint32_t cum32 = cnt;  // inclusive prefix sum over the lanes
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t o = __shfl_up(cum, d, 64);
-                if (lane >= (uint32_t)d) cum += o;
+                const uint32_t o = __shfl_up(cum32, d, 64);
+                if (lane >= (uint32_t)d) cum32 += o;
             }
-            const uint32_t P = __builtin_amdgcn_readlane(cum, 63);
+            const uint32_t P = __builtin_amdgcn_readlane(cum32, 63);
             const uint32_t ks = lo_slot > S ? (uint32_t)(lo_slot - S) : 0u;
             const uint32_t ke = hi_slot - S < (uint64_t)P ? (uint32_t)(hi_slot - S) : P;
+            S += P;
             if (ks >= ke) continue;
             auto page_at = [&](uint32_t k, uint32_t& owner) -> uint64_t {
-                owner = (uint32_t)__builtin_ctzll(__ballot(cum > k));
-                const uint32_t before = owner ? (uint32_t)__builtin_amdgcn_readlane(cum, owner - 1) : 0u;
+                owner = (uint32_t)__builtin_ctzll(__ballot(cum32 > k));
+                const uint32_t before = owner ? (uint32_t)__builtin_amdgcn_readlane(cum32, owner - 1) : 0u;
                 const uint64_t first = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(p0 >> 32), owner) << 32) |
                                        (uint32_t)__builtin_amdgcn_readlane((uint32_t)p0, owner);
                 return first + (k - before);
@@ -1818,7 +1859,7 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
             }
         }
         const uint64_t n_dyn = (T - Ts + kRvDynSlots - 1) / kRvDynSlots;
-        const uint64_t c = tail_pull<kRvHeads>(a.dyn_ctr, n_dyn, dyn_head, dyn_tried, lane);
+        const uint64_t c = tail_pull<kRvHeads>(dyn_ctr, n_dyn, dyn_head, dyn_tried, lane);
         if (c >= n_dyn) break;
         lo_slot = Ts + c * kRvDynSlots;
         hi_slot = lo_slot + kRvDynSlots < T ? lo_slot + kRvDynSlots : T;
@@ -2102,11 +2143,6 @@ hipError_t launch_log_small(const LogLaunch& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_read_counts(const ReadVerifyLaunch& a, hipStream_t s) {
-    if (a.n_reads == 0) return hipSuccess;
-    hipLaunchKernelGGL(read_counts_kernel, dim3((uint32_t)((a.n_reads + 255) / 256)), dim3(256), 0, s, a);
-    return hipGetLastError();
-}
 
 hipError_t launch_read_verify_small(const ReadVerifyLaunch& a, hipStream_t s) {
     if (a.n_reads == 0 || a.n_reads > 64) return hipErrorInvalidValue;

@@ -37,11 +37,11 @@ ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 $S
 [ "${1:-}" = "--fuzz-only" ] && exit 0
 # 1 + 2: the libraries
 HF="-O1 -std=c++17 -fPIC --offload-arch=gfx950 -Xarch_host -fsanitize=address,undefined -Xarch_host -fno-sanitize-recover=undefined -Xarch_host -fno-omit-frame-pointer"
-for f in engine kernels pool read_scan; do
+for f in engine kernels pool; do
   [ $S/obj/$f.o -nt $f.hip ] && [ $S/obj/$f.o -nt kernels.h ] || $HIPCC $HF -c $f.hip -o $S/obj/$f.o
 done
 $HIPCC -shared -fPIC --offload-arch=gfx950 -fsanitize=address,undefined -shared-libsan -o $S/libcurvecrc.so \
-    $S/obj/crc32c_cpu.o $S/obj/integrity.o $S/obj/engine.o $S/obj/kernels.o $S/obj/pool.o $S/obj/read_scan.o \
+    $S/obj/crc32c_cpu.o $S/obj/integrity.o $S/obj/engine.o $S/obj/kernels.o $S/obj/pool.o \
     -L$ROCM/lib -lrccl
 $CXX -shared $SAN -shared-libsan -o $S/libcurvehost.so $S/obj/chunkserver_host.o $S/obj/integrity_service.o \
     $S/obj/integrity_capi.o -L$S -lcurvecrc -Wl,-rpath,$S -lpthread

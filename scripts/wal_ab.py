@@ -3,7 +3,8 @@
 the bench's WAL-replay shape (65,536 entries, data 1-128 KiB, 4 KiB-aligned slots
 after a 28-byte header, over a 16 GiB pool).  Each build gets its own ctypes
 handle; rounds alternate the order; every build's output is compared with the
-first build's on every round.  usage: wal_ab.py LIB.so [LIB.so ...]"""
+first build's on every round.  usage: wal_ab.py [--fixed BYTES] LIB.so [LIB.so ...]
+(--fixed: every entry that many data bytes, the balance probe of equal sizes)"""
 import ctypes
 import os
 import sys
@@ -11,12 +12,20 @@ import sys
 import numpy as np
 import torch
 
-args = [x for x in sys.argv[1:] if not x.startswith("--")]
+argv = sys.argv[1:]
+fixed = 0
+if "--fixed" in argv:
+    i = argv.index("--fixed")
+    fixed = int(argv[i + 1])
+    del argv[i:i + 2]
+args = [x for x in argv if not x.startswith("--")]
 dev = torch.device("cuda", 0)
 pool = torch.empty(16 << 30, dtype=torch.uint8, device=dev).random_(0, 256)
 rng = np.random.default_rng(0x3A1)
 n = 65536
 real = rng.integers(1024, (128 << 10) + 1, n).astype(np.uint64)
+if fixed:
+    real[:] = fixed
 slot = (28 + real + 4095) // 4096 * 4096
 offs = np.concatenate([[0], np.cumsum(slot)[:-1]]).astype(np.uint64) + 4096 + 28
 rec = np.empty((n, 2), dtype=np.uint64)
@@ -60,5 +69,5 @@ for r in range(30):
         same[p] &= bool(torch.equal(libs[p][1], libs[order[0]][1]))
 for p, v in ms.items():
     med = sorted(v)[len(v) // 2]
-    print(f"wal {os.path.basename(p)}: median {med:.4f} ms min {min(v):.4f} mean {np.mean(v):.4f} "
+    print(f"wal{' fixed %d' % fixed if fixed else ''} {os.path.basename(p)}: median {med:.4f} ms min {min(v):.4f} mean {np.mean(v):.4f} "
           f"frac {(data_bytes + 4 * n) / (med * 1e-3) / 8e12:.4f} same_as_first {same[p]}", flush=True)

@@ -1193,6 +1193,17 @@ def test_crc_ranges_scratch_left_clean_between_calls(dev, oracle):
     sample = np.unique(np.concatenate([np.arange(0, n, 211), np.arange(n - 3000, n)]))
     check(offs, lens, sample)
     check(*batches[0])
+    # verify on read shares the stream's scratch and epochs: interleaved with
+    # range batches it still flags exactly the reads over a rotten page
+    crcs = C.page_crc(d, 4096)
+    crcs[333] ^= 4
+    roff = rng.integers(0, size - (130 << 10), 20000)
+    rlen = rng.integers(1, 128 << 10, 20000)
+    want_per = (((roff // 4096) <= 333) & (333 <= (roff + rlen - 1) // 4096)).astype(np.int64)
+    for k in range(3):
+        per, tot = C.verify_reads(d, crcs, roff, rlen)
+        assert (per.cpu().numpy() == want_per).all() and int(tot.item()) == int(want_per.sum())
+        check(*batches[k])
     assert _lib.lib().cc_engine_trim() == 0
     check(*batches[2])
 
@@ -1231,12 +1242,14 @@ def test_crc_ranges_streams_and_threads(dev, oracle):
 
 
 def test_crc_ranges_without_every_workgroup_resident(dev, oracle):
-    """The launch's tile counts come from every workgroup; a wave never waits
-    for one without a bound.  With the process's queues limited to 8 CUs
-    (HSA_CU_MASK) the grid of one workgroup per CU cannot be resident at once:
-    the running waves give up on the missing tile words after their wait and
-    count those tiles themselves.  Results still == the oracle (run in a child
-    process so the mask applies to its queues only)."""
+    """cc_crc_ranges_dev and cc_verify_reads_dev count their own schedule:
+    tile counts come from every workgroup, and a wave never waits for one
+    without a bound.  With the process's queues limited to 8 CUs (HSA_CU_MASK)
+    the grid of one workgroup per CU cannot be resident at once: the running
+    waves give up on the missing tile words after their wait and count those
+    tiles themselves.  Range CRCs still == the oracle, and verify on read flags
+    exactly the reads over the two rotten pages (run in a child process so the
+    mask applies to its queues only)."""
     import subprocess
     import sys
     code = r"""
@@ -1254,8 +1267,18 @@ for _ in range(2):
     got = C.crc_ranges(d, offs, lens).cpu().numpy().view(np.uint32)
 want = np.array([O.crc32c(buf[o:o + l].tobytes()) for o, l in zip(offs, lens)], dtype=np.uint32)
 bad = np.flatnonzero(got != want)
-print("bad", bad.size)
-sys.exit(1 if bad.size else 0)
+# verify on read, the same schedule: 3,000 reads, pages 17 and 901 rotten
+crcs = C.page_crc(d, 4096)
+crcs[17] ^= 1
+crcs[901] ^= 2
+roff = rng.integers(0, size - (130 << 10), 3000)
+rlen = rng.integers(1, 128 << 10, 3000)
+per, tot = C.verify_reads(d, crcs, roff, rlen)
+per = per.cpu().numpy()
+hit = [int(((o // 4096) <= p) & (p <= (o + l - 1) // 4096)) for o, l in zip(roff, rlen) for p in (17, 901)]
+want_per = np.array(hit, dtype=np.int64).reshape(-1, 2).sum(1)
+print("bad", bad.size, "verify", int((per != want_per).sum()), int(tot.item()), int(want_per.sum()))
+sys.exit(1 if bad.size or (per != want_per).any() or int(tot.item()) != int(want_per.sum()) else 0)
 """ % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, HSA_CU_MASK="0:0-7")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
