@@ -246,3 +246,55 @@ def range_accumulate(segs, nbs, contrib, rng):
             acc[r] = (x, c + cnt)
     left = [r for r, p in acc.items() if p != (0, 0)]
     return out, left, stores
+
+
+def verify_flat_pages(counts, waves: int, tiles: int = 1024, dyn_div: int = 16, dyn_slots: int = 32,
+                      min_slots: int = 8):
+    """The page slots read_verify_kernel hashes, as (read, page-of-read) pairs in
+    the order each share visits them: its static shares [Ts w / W, Ts (w+1) / W)
+    and the dynamic chunks, each started at the tile holding its first slot (tile
+    counts of reads [n t / tiles, n (t+1) / tiles)) and walked 64 reads a group
+    from the tile's first read, the group's first slot being the running sum of
+    the groups before it -- exactly the kernel's arithmetic."""
+    n = len(counts)
+    counts = np.asarray(counts, dtype=np.int64)
+    tb = np.array([counts[n * t // tiles:n * (t + 1) // tiles].sum() for t in range(tiles)], dtype=np.int64)
+    cum_t = np.cumsum(tb)
+    T = int(cum_t[-1]) if tiles else 0
+    Wt = (T + min_slots - 1) // min_slots
+    W = min(Wt if Wt else 1, waves)
+    Ts = T - T // dyn_div
+    out = []
+
+    def share(lo, hi):
+        if lo >= hi:
+            return
+        t = int(np.searchsorted(cum_t, lo, side="right"))  # first tile whose running count passes lo
+        base = n * t // tiles
+        S = int(cum_t[t - 1]) if t else 0
+        while True:  # the tile's reads 64 at a time, to the group whose pages pass lo
+            tot = int(counts[base:base + 64].sum())
+            if S + tot > lo or base + 64 >= n:
+                break
+            S += tot
+            base += 64
+        while base < n and S < hi:
+            grp = counts[base:base + 64]
+            cum = np.cumsum(grp)
+            P = int(cum[-1])
+            ks = lo - S if lo > S else 0
+            ke = min(hi - S, P)
+            for k in range(ks, ke):
+                owner = int(np.searchsorted(cum, k, side="right"))
+                before = int(cum[owner - 1]) if owner else 0
+                out.append((base + owner, k - before))
+            S += P
+            base += 64
+
+    for w in range(W):
+        share(Ts * w // W, Ts * (w + 1) // W)
+    n_dyn = (T - Ts + dyn_slots - 1) // dyn_slots
+    for c in range(n_dyn):
+        lo = Ts + c * dyn_slots
+        share(lo, min(lo + dyn_slots, T))
+    return out

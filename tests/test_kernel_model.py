@@ -116,3 +116,25 @@ def test_range_flat_schedule_and_split_meeting(shape, waves):
         out, left, stores = km.range_accumulate(segs, nbs, contrib, rng)
         assert out == want and not left
         assert all(c == 1 for c in stores.values()) and set(stores) == {r for r in range(n) if nbs[r]}
+
+
+@pytest.mark.parametrize("shape", ["reads", "tiny", "empties", "few"])
+@pytest.mark.parametrize("waves", [2048, 256, 5])
+def test_verify_flat_schedule_covers_every_page_once(shape, waves):
+    """read_verify_kernel's self-counted schedule (tile counts, static shares at
+    page granularity, dynamic chunks, 64-read groups walked from the tile start)
+    visits every page of every read exactly once, with the right owner read."""
+    rng = np.random.default_rng(len(shape) * 77 + waves)
+    if shape == "reads":
+        counts = rng.integers(1, 33, 20000)  # 4-128 KiB reads at 4 KiB pages
+    elif shape == "tiny":
+        counts = rng.integers(1, 3, 30000)
+    elif shape == "empties":
+        counts = rng.integers(0, 5, 9000)
+        counts[::7] = 0  # empty reads and reads past the pool: no pages
+        counts[:200] = 0
+    else:
+        counts = np.array([0, 4097, 1, 0, 33])
+    got = km.verify_flat_pages(counts, waves)
+    want = [(r, p) for r in range(len(counts)) for p in range(int(counts[r]))]
+    assert len(got) == len(want) and sorted(got) == want
