@@ -207,6 +207,34 @@ def _stream_expected(dn, mn, n, pool_n, lay, lo):
     return mc, sl, fc, dig
 
 
+def cpu_digest_check(pool, lay, lo, n, digest, dist_, dev, sample=(0, 37)):
+    """Copysets `sample` of the pool's digests, recomputed on the host: every
+    rank hashes its own chunk files of those copysets with libcurvecrc's CPU
+    primitive (file CRC = combine(metapage CRC, data CRC, 16 MiB), shifted by
+    the bytes after the file in its copyset's sorted-name chain) and the partials
+    are XOR-reduced over the ranks.  Returns {"copysets", "ok"} (same on every rank)."""
+    from curve_amd import crc as C
+    from curve_amd.pool import reduce_digests
+    part = np.zeros(lay.n_groups, dtype=np.uint32)
+    files = 0
+    for i in range(n):
+        gi = lo + i
+        if lay.group[gi] not in sample:
+            continue
+        m = pool.meta[i].cpu().numpy()
+        d = pool.data[i].cpu().numpy()
+        fc = C.combine(C.CRC32(m), C.CRC32(d), C.CHUNK_SIZE)
+        part[lay.group[gi]] ^= C.shift(fc, lay.after_bytes[gi])
+        files += 1
+    t = torch.from_numpy(part.view(np.int32)).to(dev)
+    full = reduce_digests(t, dist_) if dist_ is not None else t
+    got = digest.cpu().numpy().view(np.uint32)
+    want = full.cpu().numpy().view(np.uint32)
+    ok = bool(all(got[g] == want[g] for g in sample))
+    return {"copysets": list(sample), "files_hashed_on_this_rank": files, "ok": ok,
+            "by": "libcurvecrc CPU primitive over the chunk files' bytes, partials XOR-reduced over the ranks"}
+
+
 def stream_leg(args):
     """BASELINE config 4: scan-service stream of `--stream-chunks` x 16 MiB chunk
     files from pinned host memory (as pread into pinned buffers would leave
@@ -759,6 +787,13 @@ def main():
         local = torch.zeros_like(digest)
         pool_scan(pool, after_mult, group, local, comm=None, stream=stream)
         digest_check = bool(torch.equal(native, reduce_digests(local, dist)))
+    # untimed, every N: the exchanged digests of two copysets == the sorted-name
+    # chain of those copysets' files over the WHOLE pool, from the bytes by
+    # libcurvecrc's CPU primitive (each rank hashes its own files on the host;
+    # partials XOR-reduced over torch.distributed): the exchange checked against
+    # an independent computation, not only against another transport
+    final_digest = full_digest[0] if (world > 1 and comm is None) else digest
+    cpu_digest = cpu_digest_check(pool, lay, lo, n, final_digest, dist if world > 1 else None, dev)
     kern_each = [a.elapsed_time(b) for a, b in ev]
     kern_ms = float(np.mean(kern_each))
     # every rank's mean page-kernel time: the aggregate roofline is set by the slowest
@@ -869,8 +904,10 @@ def main():
                      "frac_of_load_only_probe": round(achieved / load_only_gbs, 4)},
         "verify": {"GiBps": round(n * chunk / GiB / (verify_ms * 1e-3), 2), "bad_pages": bad},
     }
+    out["digest_check_cpu"] = cpu_digest
     if world > 1:
-        out["digest_exchange"] = {"path": comm_note, "matches_torch_distributed": digest_check}
+        out["digest_exchange"] = {"path": comm_note, "matches_torch_distributed": digest_check,
+                                  "matches_cpu_chain": cpu_digest["ok"]}
         # aggregate roofline over the node: every rank's algorithmic bytes over the
         # slowest rank's page-kernel time, against N x the per-GPU peak
         agg = world * launch_pages * ALG_BYTES_PER_PAGE / (max(rank_kern) * 1e-3) / 1e9
