@@ -3,9 +3,10 @@
 # tracked sources of curve_amd/csrc + include to /tmp/var_NAME, edits the COPY of
 # kernels.hip, and builds build/variants/libcurvecrc_NAME.so from it.
 # usage: scripts/make_variant.sh NAME sed 'SED-EXPR'     (e.g. a constant)
-#        scripts/make_variant.sh NAME py  scripts/patches/X.py   (a patch script: X.py KERNELS_HIP)
+#        scripts/make_variant.sh NAME py  scripts/patches/X.py [ARGS...]   (X.py KERNELS_HIP ARGS...)
 set -e
 N=$1; KIND=$2; ARG=$3
+shift 3
 R=$(cd "$(dirname "$0")/.." && pwd)
 D=/tmp/var_$N
 rm -rf "$D" && mkdir -p "$D"
@@ -13,7 +14,7 @@ rm -rf "$D" && mkdir -p "$D"
 cp "$R/curve_amd/csrc/kernels.hip" "$D/curve_amd/csrc/kernels.hip"  # the working tree's kernels
 case $KIND in
   sed) sed -i "$ARG" "$D/curve_amd/csrc/kernels.hip" ;;
-  py) python3 "$R/$ARG" "$D/curve_amd/csrc/kernels.hip" ;;
+  py) python3 "$R/$ARG" "$D/curve_amd/csrc/kernels.hip" "$@" ;;
   *) echo "kind: sed | py"; exit 2 ;;
 esac
 if cmp -s "$R/curve_amd/csrc/kernels.hip" "$D/curve_amd/csrc/kernels.hip"; then echo "edit changed nothing"; exit 1; fi
