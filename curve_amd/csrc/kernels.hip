@@ -672,7 +672,7 @@ __device__ __forceinline__ TileHit tile_of(uint64_t cum, const uint64_t (&tb)[kT
 }
 
 constexpr int kFlatWaves = 8;  // waves per CU of the flat range kernel (A/B on WAL sizes: 8 beats 12 by ~4 %, 16 by ~10 %)
-constexpr uint32_t kRangeRounds = 2;  // static pieces per wave (A/B: 2 best; 1 loses on equal sizes, 8 on random)
+constexpr uint32_t kRangeRounds = 1;  // static pieces per wave (round 4, one launch: 1 beats 2 by 0.7 % on random and on equal sizes; 4 +4.7 %, 8 +10.6 %)
 constexpr uint64_t kRangeDynDiv = 32;  // 1/32 of the blocks go to the dynamic tail (A/B: 1/8 and 1/16 lose to
                                        // the one counter's atomics, 1/64 leaves tail)
 constexpr uint32_t kRangeHeads = 1;    // tail heads (A/B round 3: 8 per-XCD heads = one counter at 1/32)
