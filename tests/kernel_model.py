@@ -192,7 +192,7 @@ def range_crc_model(buf: np.ndarray, off: int, length: int, img: np.ndarray) -> 
     return mulmod(xinv_bytes(t), raw_pad) ^ C.zeros(length)
 
 
-def range_flat_items(B: int, waves: int, rounds: int = 2, dyn_div: int = 32, dyn_blocks: int = 16):
+def range_flat_items(B: int, waves: int, rounds: int = 1, dyn_div: int = 32, dyn_blocks: int = 16):
     """Work items of range_flat_kernel over a stream of B blocks: `rounds`
     static pieces per wave ([Bs c / RW, Bs (c+1) / RW), c < rounds * waves,
     empty ones skipped), then the dynamic tail's chunks of dyn_blocks blocks."""

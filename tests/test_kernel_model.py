@@ -99,22 +99,23 @@ def test_range_flat_schedule_and_split_meeting(shape, waves):
         nbs = rng.integers(0, 3, n)
     else:
         nbs = np.array([4097, 0, 1])
-    segs = km.range_flat_segments(nbs, waves)
-    cover = {}
-    for r, kb, cnt in segs:
-        assert cnt >= 1 and kb + cnt <= nbs[r]
-        cover.setdefault(r, []).append((kb, cnt))
-    for r in range(n):
-        parts = sorted(cover.get(r, []))
-        assert sum(c for _, c in parts) == nbs[r]
-        assert all(a + c == b for (a, c), (b, _) in zip(parts, parts[1:]))  # contiguous, disjoint
-    contrib = rng.integers(0, 2**32, len(segs)).tolist()
-    want = {}
-    for (r, _, _), v in zip(segs, contrib):
-        want[r] = want.get(r, 0) ^ v
-    for _ in range(3):
-        out, left, stores = km.range_accumulate(segs, nbs, contrib, rng)
-        assert out == want and not left
+    for rounds in (1, 2):  # the shipped schedule (one static piece a wave) and round 3's
+        segs = km.range_flat_segments(nbs, waves, rounds=rounds)
+        cover = {}
+        for r, kb, cnt in segs:
+            assert cnt >= 1 and kb + cnt <= nbs[r]
+            cover.setdefault(r, []).append((kb, cnt))
+        for r in range(n):
+            parts = sorted(cover.get(r, []))
+            assert sum(c for _, c in parts) == nbs[r]
+            assert all(a + c == b for (a, c), (b, _) in zip(parts, parts[1:]))  # contiguous, disjoint
+        contrib = rng.integers(0, 2**32, len(segs)).tolist()
+        want = {}
+        for (r, _, _), v in zip(segs, contrib):
+            want[r] = want.get(r, 0) ^ v
+        for _ in range(3):
+            out, left, stores = km.range_accumulate(segs, nbs, contrib, rng)
+            assert out == want and not left
         assert all(c == 1 for c in stores.values()) and set(stores) == {r for r in range(n) if nbs[r]}
 
 
