@@ -1128,7 +1128,7 @@ bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork
     w->table_entries = te;
     w->next_off = 0;
     w->heads_off = align256(w->n_pieces * 4);
-    w->bytes = w->heads_off + align256(w->n_pieces * 4);
+    w->bytes = w->heads_off + align256(w->n_pieces * 8);  // head records {table slot, claiming piece}
     return true;
 }
 

@@ -127,7 +127,7 @@ struct LogLaunch {
     uint64_t* table;            // [table_mask + 1] {page + 1, piece + 1} of the page's list head (0 = empty)
     uint32_t table_mask;
     uint32_t* next;             // [n_pieces] next piece of the same page (kNoPiece = end)
-    uint32_t* heads;            // [n_pieces] table slots of the touched pages (unordered)
+    uint32_t* heads;            // [n_pieces] head records {table slot, claiming piece} of the touched pages (uint2, unordered)
     uint32_t* head_count;       // number of them
     // non-null: the table and head_count are the engine's per-stream table, to be
     // left zero -- the page kernel clears each slot it consumes, and the last

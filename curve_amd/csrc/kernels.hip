@@ -1110,7 +1110,10 @@ __device__ __forceinline__ void insert_piece(const LogLaunch& a, uint64_t t, uin
     __syncthreads();
     uint32_t base = wcount[nw];
     for (uint32_t w = 0; w < wv; w++) base += wcount[w];
-    if (fresh) a.heads[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = slot;
+    // the head record: the page's table slot and the claiming piece (the list's
+    // tail: a page whose entry still names it has no other piece)
+    if (fresh) reinterpret_cast<uint2*>(a.heads)[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] =
+        make_uint2(slot, (uint32_t)t);
 }
 
 __global__ __launch_bounds__(kInsertThreads) void log_insert_kernel(LogLaunch a) {
@@ -1417,21 +1420,25 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         // lane k <- head base + k*W (clamped loads: no branches around them)
         const uint64_t ih = (uint64_t)base + (uint64_t)lane * W;
         const bool hv = ih < H;
-        const uint32_t hslot = a.heads[hv ? ih : base];
+        // the head record gives the table slot AND the claiming piece, so the
+        // claimer's descriptor loads beside the table entry: two dependent
+        // round trips to a page's geometry instead of three (the list link is
+        // needed by pages with several pieces only, far behind)
+        const uint2 hrec = reinterpret_cast<const uint2*>(a.heads)[hv ? ih : base];
+        const uint32_t hslot = hrec.x, claimer = hrec.y;
         const unsigned long long ent = reinterpret_cast<const unsigned long long*>(a.table)[hslot];
+        const UpdateDesc d = a.upd[claimer / a.slots];
         if (a.done && hv) a.table[hslot] = 0ull;  // the slot is this lane's alone (one head per page)
         const uint32_t key = (uint32_t)(ent >> 32) - 1u;  // the page
-        const uint32_t pfirst = (uint32_t)ent - 1u;       // one of its pieces (the list head)
-        const uint32_t nxt = a.next[pfirst];
+        const uint32_t pfirst = (uint32_t)ent - 1u;       // the list head (the latest piece)
+        const uint32_t nxt = a.next[pfirst];              // consumed by the several-piece path only
         const uint32_t u0 = pfirst / a.slots;  // the head piece's update
-        const UpdateDesc d = a.upd[u0];
-        // the head piece's geometry in its page, packed: rlo | rhi << 16 and the
-        // source pointer (3 VGPRs instead of the 5 of its descriptor)
+        // the claimer's geometry in its page (the only piece when single), packed:
+        // rlo | rhi << 16 and the source pointer (3 VGPRs instead of the 5 of its descriptor)
         const Piece hp0 = piece_in_page((uint64_t)key * pb, pb, d.dst, d.src, d.len, a.src);
         const uint32_t hrr = hp0.rlo | hp0.rhi << 16;
         const uint64_t hsp = (uint64_t)(uintptr_t)hp0.sp;
-        const bool single = nxt == kNoPiece;  // the page's only piece
-        const uint32_t u1 = single ? 0u : nxt / a.slots;  // several pieces: the second one's update
+        const bool single = pfirst == claimer;  // nobody pushed onto the claimer: the page's only piece
         const uint64_t singles = __ballot(single);
         const uint32_t cnt = (uint32_t)__popcll(__ballot(hv));  // valid lanes are 0 .. cnt-1
         // two pages in flight: k (being merged + hashed) and k+1.  (A third
@@ -1504,7 +1511,8 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
                 // together, so a two-piece page (nearly every page with several)
                 // pays one round trip for its list instead of four.  (Loading these
                 // with the previous step's edge loads instead measured equal.)
-                const uint32_t u0h = __builtin_amdgcn_readlane(u0, hh), u1h = __builtin_amdgcn_readlane(u1, hh);
+                const uint32_t u0h = __builtin_amdgcn_readlane(u0, hh);
+                const uint32_t u1h = (uint32_t)__builtin_amdgcn_readlane(nxt, hh) / a.slots;  // the second piece's update
                 uint32_t cnt = 2, mu = lane == 0 ? u0h : (lane == 1 ? u1h : 0xFFFFFFFFu);  // update of lane's piece
                 const UpdateDesc dq = a.upd[lane < 2 ? mu : u0h];
                 uint32_t q = a.next[__builtin_amdgcn_readlane(nxt, hh)];

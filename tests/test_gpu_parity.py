@@ -412,9 +412,9 @@ def test_pool_scan_fused_metapages_and_tail_reuse(dev, oracle, meta_sz):
     launch's tail as chunks of its own -- 300 metapages = 4 full 64-page chunks
     and a partial one; an 8 KiB metapage gets a launch of its own.  Every page,
     metapage and slice CRC and every digest equals the oracle's, and stays so
-    over back-to-back scans on one stream and on two streams in turn: the
-    stream's tail counters reset themselves at the end of each launch
-    (kernels.hip tail_reset), so no call zeroes them."""
+    over back-to-back scans on one stream and on two streams in turn: each
+    launch zeroes the tail-counter slot set its stream's next launch pulls from
+    (kernels.hip tail_clear_next), so no call clears them."""
     from curve_amd import crc as C
     from curve_amd.pool import copyset_layout, pool_scan
     from curve_amd.scan import DevicePool, chunk_file_name
@@ -443,10 +443,10 @@ def test_pool_scan_fused_metapages_and_tail_reuse(dev, oracle, meta_sz):
     streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
     for rep, st in enumerate([0, 0, 1, 0, 1, 1]):
         s = streams[st]
-        s.wait_stream(torch.cuda.current_stream())
         pool.page_crcs.fill_(0)
         pool.meta_crcs.fill_(0)
         digest = torch.full((lay.n_groups,), rep, dtype=torch.int32, device=dev)
+        s.wait_stream(torch.cuda.current_stream())  # after the fills: the scan must not race them
         with torch.cuda.stream(s):
             pool_scan(pool, after_mult, group, digest, stream=s)
         s.synchronize()
