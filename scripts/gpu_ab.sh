@@ -8,7 +8,7 @@ set -u
 P=$1; shift
 mkdir -p gpurun_out
 case $P in
-  log) K="write_log or partial" ;;
+  log) K="write_log or partial or resident" ;;
   page|pool) K="page or pool or scan or golden" ;;
   reads) K="verify or read" ;;
   wal) K="range or wal or bufs or chunk_hash" ;;

@@ -4,7 +4,7 @@ delta variant with --delta) across libcurvecrc builds, in the bench's
 partial-write shape: 65,536 random 512 B-4 KiB writes over a 16 GiB pool.
 Each build gets its own ctypes handle and work buffer; every build is then
 checked once: after one more batch, the stored CRCs equal a fresh rehash.
-usage: log_ab.py [--delta] LIB.so [LIB.so ...]"""
+usage: log_ab.py [--delta] [--n WRITES] LIB.so [LIB.so ...]   (--n: writes per log, default 65,536)"""
 import ctypes
 import os
 import sys
@@ -15,11 +15,17 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from curve_amd import crc as C  # noqa: E402
 
-args = [x for x in sys.argv[1:] if not x.startswith("--")]
+argv = sys.argv[1:]
+n_arg = None
+if "--n" in argv:
+    i = argv.index("--n")
+    n_arg = int(argv[i + 1])
+    del argv[i:i + 2]
+args = [x for x in argv if not x.startswith("--")]
 delta = "--delta" in sys.argv
 fn = "cc_apply_log_delta_dev" if delta else "cc_apply_log_dev"
 dev = torch.device("cuda", 0)
-pb, U = 4096, 65536
+pb, U = 4096, n_arg or 65536
 pool = torch.empty(16 << 30, dtype=torch.uint8, device=dev).random_(0, 256)
 crcs = C.page_crc(pool, pb)
 src = torch.empty(U * pb, dtype=torch.uint8, device=dev).random_(0, 256)
@@ -74,5 +80,5 @@ for p in libs:
     ok[p] = bool(torch.equal(crcs, C.page_crc(pool, pb)))
 for p, v in ms.items():
     med = sorted(v)[len(v) // 2]
-    print(f"{'delta' if delta else 'full'} {os.path.basename(p)}: median {med:.4f} ms min {min(v):.4f} "
+    print(f"{'delta' if delta else 'full'} n={U} {os.path.basename(p)}: median {med:.4f} ms min {min(v):.4f} "
           f"crcs_consistent {ok[p]}", flush=True)

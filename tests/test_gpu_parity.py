@@ -1247,9 +1247,11 @@ def test_crc_ranges_without_every_workgroup_resident(dev, oracle):
     without a bound.  With the process's queues limited to 8 CUs (HSA_CU_MASK)
     the grid of one workgroup per CU cannot be resident at once: the running
     waves give up on the missing tile words after their wait and count those
-    tiles themselves.  Range CRCs still == the oracle, and verify on read flags
-    exactly the reads over the two rotten pages (run in a child process so the
-    mask applies to its queues only)."""
+    tiles themselves.  Range CRCs still == the oracle, verify on read flags
+    exactly the reads over the two rotten pages, and the write log (whose
+    kernels never wait on another workgroup) still lands as in-order
+    application (run in a child process so the mask applies to its queues
+    only)."""
     import subprocess
     import sys
     code = r"""
@@ -1277,8 +1279,26 @@ per, tot = C.verify_reads(d, crcs, roff, rlen)
 per = per.cpu().numpy()
 hit = [int(((o // 4096) <= p) & (p <= (o + l - 1) // 4096)) for o, l in zip(roff, rlen) for p in (17, 901)]
 want_per = np.array(hit, dtype=np.int64).reshape(-1, 2).sum(1)
-print("bad", bad.size, "verify", int((per != want_per).sum()), int(tot.item()), int(want_per.sum()))
-sys.exit(1 if bad.size or (per != want_per).any() or int(tot.item()) != int(want_per.sum()) else 0)
+# the write log on the 8 CUs: 30,000 writes, both modes, twice each (the
+# stream's table reused)
+ok_log = True
+for delta in (False, True):
+    for rnd in range(2):
+        host = d.cpu().numpy()
+        crcs = C.page_crc(d, 4096)
+        n = 30000
+        lens = rng.integers(1, 4097, n)
+        dst = rng.integers(0, size - 4096, n)
+        src = rng.integers(0, 256, int(lens.sum()) + 8, dtype=np.uint8)
+        soff = np.concatenate([[0], np.cumsum(lens)[:-1]])
+        C.apply_updates(d, crcs, torch.from_numpy(src).to("cuda:0"), dst, soff, lens, 4096, delta=delta)
+        want_b = host.copy()
+        for i in range(n):
+            want_b[dst[i]:dst[i] + lens[i]] = src[soff[i]:soff[i] + lens[i]]
+        ok_log &= bool((d.cpu().numpy() == want_b).all())
+        ok_log &= bool((crcs.cpu().numpy().view(np.uint32) == O.page_crcs(want_b, 4096)).all())
+print("bad", bad.size, "verify", int((per != want_per).sum()), int(tot.item()), int(want_per.sum()), "log", ok_log)
+sys.exit(1 if bad.size or (per != want_per).any() or int(tot.item()) != int(want_per.sum()) or not ok_log else 0)
 """ % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, HSA_CU_MASK="0:0-7")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
