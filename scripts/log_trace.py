@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
-"""Per-wave phase times of one write-log launch (the log_trace variant:
+"""Per-wave times of the write-log page kernel (the log_trace variant:
 scripts/make_variant.sh ltrace py scripts/patches/log_trace.py) in the bench's
 partial-write shape: 65,536 random 512 B-4 KiB writes over a 16 GiB pool.
-Prints, over the grid's waves, when each phase ends (us after the first wave
-started): insert tiles, LDS fill, wait for every tile, end.
+Prints, over the grid's waves, when they end (us after the first wave's LDS
+fill), by XCD and by age group, the pages each rehashed and the tails taken.
 usage: log_trace.py LIB.so [--delta] [--out FILE.json]"""
 import ctypes
 import json
@@ -55,7 +55,7 @@ for k in range(70):
         t0 = t[:, 0].min()
         us = lambda c: (t[:, c].astype(np.int64) - int(t0)) / 100.0  # noqa: E731
         row = {}
-        for name, c in (("start", 0), ("inserted", 1), ("filled", 2), ("waited", 3), ("end", 4)):
+        for name, c in (("filled", 0), ("end", 4)):
             v = us(c)
             row[name] = [round(float(np.percentile(v, q)), 2) for q in (0, 50, 90, 100)]
         res.append(row)
@@ -81,8 +81,10 @@ pages = last[:, 6].astype(np.int64)
 rate = {int(x): round(float(np.median(((end - (last[:, 3].astype(np.int64) - t0) / 100.0) / np.maximum(pages, 1))[xcc == x])), 3)
         for x in np.unique(xcc)}
 print("end median by XCD:", by_xcd, "by age group:", by_age, flush=True)
+steals = last[:, 7].astype(np.int64)
 print("us per page by XCD (page phase / pages):", rate, "pages per wave min/median/max", int(pages.min()),
-      int(np.median(pages)), int(pages.max()), flush=True)
+      int(np.median(pages)), int(pages.max()), "tails taken:", int(steals.sum()), "by", int((steals > 0).sum()),
+      "waves", flush=True)
 print(f"workgroup end (last wave): min {wg_end.min():.1f} median {np.median(wg_end):.1f} max {wg_end.max():.1f}; "
       f"median spread inside a workgroup {spread_in_wg:.1f} us", flush=True)
 print("median over", len(res), "launches:", json.dumps(med), flush=True)
