@@ -298,3 +298,115 @@ def verify_flat_pages(counts, waves: int, tiles: int = 1024, dyn_div: int = 16, 
         lo = Ts + c * dyn_slots
         share(lo, min(lo + dyn_slots, T))
     return out
+
+
+# ---------------------------------------------------------------------------
+# Write-log page kernel: age-weighted static shares + tail stealing
+# (kernels.hip log_pages_body, round 4).  An event simulation over per-wave
+# speeds: every wave rehashes its share [first, H); the last 1/tail_div of it
+# (the tail, from ts) is claimed by one atomic max -- the owner as it starts the
+# page before the tail (read when that page is done), a finished wave after a scan of 64
+# candidates (the 4 youngest waves of the next 16 workgroups).  The table slot
+# of a head is cleared by the wave that won it, after that wave read it.
+# ---------------------------------------------------------------------------
+SKEW = (33, 27, 22, 18)
+
+
+def log_share(Hall: int, grid: int, wv: int, b: int, w: int):
+    pre = lambda t: sum(SKEW[(u // 4) & 3] for u in range(t))  # noqa: E731
+    h0, h1 = Hall * b // grid, Hall * (b + 1) // grid
+    Hb, ws = h1 - h0, pre(wv)
+    return h0 + Hb * pre(w) // ws, h0 + Hb * pre(w + 1) // ws
+
+
+def log_steal_schedule(Hall: int, grid: int, wv: int, speed, tail_div: int = 4, max_steals: int = 4, start=None):
+    """-> (owner[h]: the wave that rehashed head h, cleared_by[h], read_ok,
+    end[w]: when each wave finished).  speed[w]: time per page of wave w;
+    start[w]: when it starts (a workgroup not yet resident starts late)."""
+    import heapq
+    W = grid * wv
+    start = start if start is not None else [0.0] * W
+    claim = [None] * W  # who won wave w's tail
+    owner = [-1] * Hall
+    cleared = [False] * Hall
+    read_ok = True
+    end = [0.0] * W
+    shares = [log_share(Hall, grid, wv, w // wv, w % wv) for w in range(W)]
+    tails = [(h - (h - f) // tail_div, h) for f, h in shares]
+    # a wave's life as a generator of (time, action) steps; actions run in time order
+    def life(w):
+        nonlocal read_ok
+        t = start[w]
+        f, H = shares[w]
+        ts, _ = tails[w]
+        segs = [(f, H, True)]
+        steals = 0
+        while segs:
+            s0, s1, own = segs.pop()
+            if own and ts < H:
+                # own part; the claim goes out as the page before the tail starts
+                issue = max(ts - 1, s0)
+                for h in range(s0, s1):
+                    if h == issue:
+                        yield t, ("claim", w, w)
+                    if h == ts:
+                        if claim[w] != w:
+                            break
+                        for k in range(ts, s1):
+                            if cleared[k]:
+                                read_ok = False
+                            cleared[k] = True  # cleared once won (read at load time, before)
+                    if h < ts:
+                        if cleared[h]:
+                            read_ok = False
+                        cleared[h] = True
+                    t += speed[w]
+                    yield t, ("page", w, h)
+            else:
+                for h in range(s0, s1):
+                    if own or True:
+                        if cleared[h]:
+                            read_ok = False
+                        cleared[h] = True
+                for h in range(s0, s1):
+                    t += speed[w]
+                    yield t, ("page", w, h)
+            if steals >= max_steals:
+                break
+            # scan: the 4 youngest waves of the next 16 workgroups
+            b = w // wv
+            got = None
+            for l in range(64):
+                vb, vw = (b + 1 + l // 4) % grid, wv - 1 - l % 4
+                v = vb * wv + vw
+                if v != w and tails[v][0] < tails[v][1] and claim[v] is None:
+                    yield t, ("claim", w, v)
+                    if claim[v] == w:
+                        got = v
+                        break
+            if got is None:
+                break
+            steals += 1
+            segs.append((tails[got][0], tails[got][1], False))
+        end[w] = t
+    gens = {w: life(w) for w in range(W)}
+    heap = []
+    for w, g in gens.items():
+        try:
+            tt, act = next(g)
+            heapq.heappush(heap, (tt, w, act))
+        except StopIteration:
+            end[w] = start[w]
+    while heap:
+        tt, w, act = heapq.heappop(heap)
+        kind, who, v = act
+        if kind == "claim" and claim[v] is None:
+            claim[v] = who
+        elif kind == "page":
+            owner[v] = who if owner[v] == -1 else -2  # -2: rehashed twice
+        try:
+            tt, act = next(gens[w])
+            heapq.heappush(heap, (tt, w, act))
+        except StopIteration:
+            pass
+    return owner, cleared, read_ok, end

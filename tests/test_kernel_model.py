@@ -139,3 +139,22 @@ def test_verify_flat_schedule_covers_every_page_once(shape, waves):
     got = km.verify_flat_pages(counts, waves)
     want = [(r, p) for r in range(len(counts)) for p in range(int(counts[r]))]
     assert len(got) == len(want) and sorted(got) == want
+
+
+@pytest.mark.parametrize("Hall,grid,wv", [(101161, 256, 16), (5000, 40, 16), (37, 4, 16), (900, 17, 12)])
+def test_write_log_tail_stealing_rehashes_every_page_once(Hall, grid, wv):
+    """The write-log page kernel's tail stealing (log_pages_body): whatever the
+    wave speeds (three XCDs ~6 % slow, young waves slower, a late workgroup that
+    is not resident at first), every touched page is rehashed by exactly one
+    wave, every table slot is cleared once, after the wave that won it read it,
+    and with uneven speeds the last wave ends earlier than without stealing."""
+    rng = np.random.default_rng(Hall)
+    W = grid * wv
+    speed = [1.0 + (0.06 if (w // wv) % 8 in (3, 4, 5) else 0.0) + 0.02 * ((w % wv) // 4) + rng.uniform(0, 0.02)
+             for w in range(W)]
+    start = [0.0] * W
+    start[(grid // 2) * wv:(grid // 2 + 1) * wv] = [40.0] * wv
+    owner, cleared, ok, end = km.log_steal_schedule(Hall, grid, wv, speed, start=start)
+    assert min(owner) >= 0 and all(cleared) and ok
+    _, _, _, end0 = km.log_steal_schedule(Hall, grid, wv, speed, max_steals=0, start=start)
+    assert max(end) <= max(end0)
