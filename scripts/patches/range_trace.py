@@ -17,11 +17,10 @@ def rep(old, new):
     s = s.replace(old, new, 1)
 
 
-rep("""    tail_cursor<kRangeHeads>(dyn_head, dyn_tried);
-
+rep("""
     // work items: static pieces item < rounds, then dynamic chunks until the counter runs out
 #pragma unroll 1
-    for (uint32_t item = 0;; item++) {""", """    tail_cursor<kRangeHeads>(dyn_head, dyn_tried);
+    for (uint32_t item = 0;; item++) {""", """
     const uint64_t tr_t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t tr_ts = 0, tr_blocks = 0, tr_dyn = 0;
 
