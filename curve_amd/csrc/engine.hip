@@ -179,21 +179,22 @@ int map_err(hipError_t e) {
 
 void staging_free(Staging& st) {
     for (int i = 0; i < 2; i++) {
-        if (st.stream[i]) hipStreamSynchronize(st.stream[i]);
-        if (st.host[i]) hipHostFree(st.host[i]);
-        if (st.dev[i]) hipFree(st.dev[i]);
-        if (st.dcrc[i]) hipFree(st.dcrc[i]);
-        if (st.hcrc[i]) hipHostFree(st.hcrc[i]);
-        if (st.stream[i]) hipStreamDestroy(st.stream[i]);
-        if (st.done[i]) hipEventDestroy(st.done[i]);
+        // teardown: nothing to do about a failure here but go on freeing the rest
+        if (st.stream[i]) (void)hipStreamSynchronize(st.stream[i]);
+        if (st.host[i]) (void)hipHostFree(st.host[i]);
+        if (st.dev[i]) (void)hipFree(st.dev[i]);
+        if (st.dcrc[i]) (void)hipFree(st.dcrc[i]);
+        if (st.hcrc[i]) (void)hipHostFree(st.hcrc[i]);
+        if (st.stream[i]) (void)hipStreamDestroy(st.stream[i]);
+        if (st.done[i]) (void)hipEventDestroy(st.done[i]);
         st.host[i] = st.dev[i] = nullptr;
         st.dcrc[i] = st.hcrc[i] = nullptr;
         st.stream[i] = nullptr;
         st.done[i] = nullptr;
         st.sig[i].fired = true;
     }
-    if (st.aux) hipFree(st.aux);
-    if (st.aux_ready) hipEventDestroy(st.aux_ready);
+    if (st.aux) (void)hipFree(st.aux);
+    if (st.aux_ready) (void)hipEventDestroy(st.aux_ready);
     st.aux = nullptr;
     st.aux_ready = nullptr;
     st.aux_bytes = 0;
@@ -210,10 +211,10 @@ DevCtx::~DevCtx() {
     if (device >= 0 && hipSetDevice(device) == hipSuccess) {
         (void)hipDeviceSynchronize();  // kernels enqueued by *_dev calls may still read the image / tables
         staging_free(st);
-        if (image) hipFree(image);
+        if (image) (void)hipFree(image);
         for (int i = 0; i < kEpiSlots; i++)
-            if (void* p = epi_ptr[i].load()) hipFree(p);
-        for (auto& t : tails) hipFree(t.p);
+            if (void* p = epi_ptr[i].load()) (void)hipFree(p);
+        for (auto& t : tails) (void)hipFree(t.p);
         for (auto& t : log_tabs) (void)hipFreeAsync(t.p, nullptr);
         for (auto& t : range_works) (void)hipFreeAsync(t.p, nullptr);
         (void)hipDeviceSynchronize();
@@ -966,7 +967,7 @@ bool epilogue_geometry(DevCtx* c, uint32_t pages_per_chunk, uint32_t page_bytes,
     void* dev = nullptr;
     if (hipMalloc(&dev, h.size() * 4) != hipSuccess) return false;
     if (hipMemcpy(dev, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
-        hipFree(dev);  // never publish a half-initialised table
+        (void)hipFree(dev);  // never publish a half-initialised table
         return false;
     }
     c->epi_ptr[free_slot].store(dev, std::memory_order_relaxed);
