@@ -745,32 +745,33 @@ __global__ __launch_bounds__(64 * kFlatWaves) void range_flat_kernel(RangeLaunch
         uint64_t r = n * tile / kRangeTiles;
         uint64_t rel = b0 - before;
         uint32_t k0 = 0;
+        // window of 64 descriptors (ranges wb + lane), refilled when passed; the
+        // search's last 64 descriptors are the first window (no second load)
+        uint64_t wb;
+        RangeDesc wd;
+        uint64_t wbits;  // lanes of the window holding a range with blocks
         for (;;) {
             const uint64_t ri = r + lane;
-            const RangeDesc d = ranges[ri < n ? ri : n - 1];
-            const uint64_t nbl = (ri < n && d.len) ? range_geo(d.off, d.len).nb : 0u;
+            wd = ranges[ri < n ? ri : n - 1];
+            const uint64_t nbl = (ri < n && wd.len) ? range_geo(wd.off, wd.len).nb : 0u;
             const uint64_t c = wave_scan_incl(nbl, lane);
             const uint64_t tot = readlane64(c, 63);
             if (rel < tot) {
                 const uint32_t h = (uint32_t)__builtin_ctzll(__ballot(c > rel));
                 k0 = (uint32_t)(rel - (h ? readlane64(c, h - 1) : 0));
+                wb = r;
+                wbits = __ballot(ri < n && wd.len != 0);
                 r += h;
                 break;
             }
             rel -= tot;
             r += 64;
         }
-
-        // window of 64 descriptors (ranges wb + lane), refilled when passed
-        uint64_t wb = r;
-        RangeDesc wd;
-        uint64_t wbits;  // lanes of the window holding a range with blocks
         auto load_window = [&]() {
             const uint64_t ri = wb + lane;
             wd = ranges[ri < n ? ri : n - 1];
             wbits = __ballot(ri < n && wd.len != 0);
         };
-        load_window();
         uint64_t left = b1 - b0;  // blocks not yet issued
         struct Pos {
             RangeGeo g;
