@@ -1802,6 +1802,8 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
         // slots [lo_slot, hi_slot) at PAGE granularity: from the read holding
         // slot lo_slot through the reads starting before hi_slot, cut at both ends
         uint64_t base = n, S = 0;  // the group's first read and the slot of its page 0
+        RangeDesc rs;              // the search's last 64 descriptors: the first group's (no second load)
+        bool have_rs = false;
         if (lo_slot < hi_slot) {
             const TileHit th = tile_of(cum, tb, lo_slot, lane);
             base = n * th.tile / kRangeTiles;
@@ -1809,17 +1811,20 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
             // the tile's reads 64 at a time, to the group whose pages pass lo_slot
             for (;;) {
                 const uint64_t ri = base + lane;
-                const uint64_t c = wave_scan_incl(ri < n ? read_pages(a, a.reads[ri]) : 0u, lane);
+                rs = a.reads[(ri < n ? ri : base) + vz];
+                const uint64_t c = wave_scan_incl(ri < n ? read_pages(a, rs) : 0u, lane);
                 const uint64_t tot = readlane64(c, 63);
                 if (S + tot > lo_slot || base + 64 >= n) break;
                 S += tot;
                 base += 64;
             }
+            have_rs = true;
         }
         for (; base < n && S < hi_slot; base += 64) {
             const uint64_t ri = base + lane;
             const bool valid = ri < n;
-            const RangeDesc r = a.reads[(valid ? ri : base) + vz];
+            const RangeDesc r = have_rs ? rs : a.reads[(valid ? ri : base) + vz];
+            have_rs = false;
             const uint32_t cnt = valid ? (uint32_t)read_pages(a, r) : 0u;  // 0 also for reads past the pool
             const uint64_t p0 = r.off >> a.page_shift;
             uint32_t cum32 = cnt;  // inclusive prefix sum over the lanes
