@@ -1108,12 +1108,13 @@ inline uint32_t log_slots(uint32_t max_len, uint32_t page_bytes) { return (max_l
 }  // namespace
 
 namespace {
-// The caller's work buffer of the write log: next links | head slots (neither
-// needs clearing).  The page table lives in the engine (LogTable): header of
-// 256 bytes (head count at 0, the page kernel's block-arrival count at 64), then
-// the open-addressing table.
+// The caller's work buffer of the write log: next links | head segments (one
+// per insert block) | segment counts (none needs clearing).  The page table
+// lives in the engine (LogTable): a 256-byte header (unused), then the
+// open-addressing table.
 struct LogWork {
-    uint64_t n_pieces, table_entries, next_off, heads_off, bytes;
+    uint64_t n_pieces, table_entries, next_off, heads_off, counts_off, bytes;
+    uint32_t n_segs, seg_cap;
 };
 constexpr uint64_t kLogTableHeader = 256;
 bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork* w) {
@@ -1127,9 +1128,17 @@ bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork
     while (te < 8 * w->n_pieces && te < (1ull << 32)) te <<= 1;
     if (te < 4 * w->n_pieces) return false;
     w->table_entries = te;
+    // insert blocks: one per 1,024-piece chunk up to kInsertBlocks (then
+    // grid-stride); block b's head segment holds the records of its chunks
+    const uint64_t chunks = (w->n_pieces + kInsertThreads - 1) / kInsertThreads;
+    w->n_segs = (uint32_t)(chunks < kInsertBlocks ? chunks : kInsertBlocks);
+    const uint64_t cap = (chunks + w->n_segs - 1) / w->n_segs * kInsertThreads;
+    if (cap >= (1ull << 32)) return false;
+    w->seg_cap = (uint32_t)cap;
     w->next_off = 0;
     w->heads_off = align256(w->n_pieces * 4);
-    w->bytes = w->heads_off + align256(w->n_pieces * 8);  // head records {table slot, claiming piece}
+    w->counts_off = w->heads_off + align256((uint64_t)w->n_segs * cap * 8);  // head records {table slot, claiming piece}
+    w->bytes = w->counts_off + align256(kInsertBlocks * 4);
     return true;
 }
 
@@ -1207,6 +1216,9 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
     a.n_pieces = lw.n_pieces;
     a.next = reinterpret_cast<uint32_t*>(w + lw.next_off);
     a.heads = reinterpret_cast<uint32_t*>(w + lw.heads_off);
+    a.seg_count = reinterpret_cast<uint32_t*>(w + lw.counts_off);
+    a.n_segs = lw.n_segs;
+    a.seg_cap = lw.seg_cap;
     a.image = c->image;
     a.kconst = kconst_for(page_bytes);
     a.page_crcs = d_page_crcs;
@@ -1224,8 +1236,7 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
     if (e != hipSuccess) return map_err(e);
     unsigned char* tmp = nullptr;  // no table free for this stream: a cleared one for this call
     if (t) {
-        a.head_count = reinterpret_cast<uint32_t*>(t->p);
-        a.done = reinterpret_cast<uint32_t*>(t->p + 64);
+        a.clear_table = 1;
         a.table = reinterpret_cast<uint64_t*>(t->p + kLogTableHeader);
         a.table_mask = (uint32_t)(t->entries - 1);
     } else {
@@ -1235,7 +1246,6 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
             (void)hipFreeAsync(tmp, s);
             return map_err(e);
         }
-        a.head_count = reinterpret_cast<uint32_t*>(tmp);
         a.table = reinterpret_cast<uint64_t*>(tmp + kLogTableHeader);
         a.table_mask = (uint32_t)(lw.table_entries - 1);
     }

@@ -107,6 +107,8 @@ struct UpdateDesc {
 // pieces in log order in registers, stores the changed rows and rehashes it.
 // A page with more than 64 pieces is finished by its wave replaying the log.
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
+constexpr uint32_t kInsertThreads = 1024;  // pieces per insert chunk (one per thread)
+constexpr uint32_t kInsertBlocks = 256;    // insert blocks at most (grid-stride over chunks): head segments
 constexpr int kLogWaves = 12;  // waves per CU of the write-log page kernel at 8 KiB pages (A/B at 4 KiB, round 1: 12 beats 8 by ~6 %)
 constexpr int kLogWavesFull = 16;   // full mode, pages <= 4 KiB: 103 VGPRs since the row offsets went into the offset field
 constexpr int kLogWavesDelta = 16;  // delta mode, pages <= 4 KiB: 120 VGPRs at 16 waves (was 12 waves: 129 would spill)
@@ -127,12 +129,14 @@ struct LogLaunch {
     uint64_t* table;            // [table_mask + 1] {page + 1, piece + 1} of the page's list head (0 = empty)
     uint32_t table_mask;
     uint32_t* next;             // [n_pieces] next piece of the same page (kNoPiece = end)
-    uint32_t* heads;            // [n_pieces] head records {table slot, claiming piece} of the touched pages (uint2, unordered)
-    uint32_t* head_count;       // number of them
-    // non-null: the table and head_count are the engine's per-stream table, to be
-    // left zero -- the page kernel clears each slot it consumes, and the last
-    // block out (counted here) zeroes head_count and this word
-    uint32_t* done;
+    // head records {table slot, claiming piece} of the touched pages (uint2), in
+    // one segment of seg_cap records per insert block: block b's at b * seg_cap,
+    // seg_count[b] of them (written by the insert, no clearing needed)
+    uint32_t* heads;
+    uint32_t* seg_count;        // [n_segs]
+    uint32_t seg_cap;
+    uint32_t n_segs;            // insert blocks (<= kInsertBlocks)
+    int clear_table;            // the table is the engine's per-stream one: the page kernel leaves it zero
     const void* image;
     uint32_t kconst;
     uint32_t* page_crcs;        // out; in delta mode also in (the CRCs before the batch)

@@ -1060,12 +1060,13 @@ __device__ __forceinline__ uint32_t page_hash(uint32_t page, uint32_t mask) {
     return (page * 2654435761u) & mask;  // Fibonacci hashing; sequential pages spread
 }
 
-constexpr uint32_t kInsertThreads = 1024;  // one head-list atomic per 1024 pieces (a per-wave atomic on the one
-                                          // counter serialised 2048 waves: 26 of the kernel's 31 us)
-// Piece t of the log (t >= n_pieces: none) into the table.  Every thread of
-// the block calls it; `wcount` = LDS scratch of blockDim/64 + 1 words, free
-// again after the block's next __syncthreads.
-__device__ __forceinline__ void insert_piece(const LogLaunch& a, uint64_t t, uint32_t* wcount) {
+// Piece t of the log (t >= n_pieces: none) into the table; its head record,
+// if it claims a page, goes to the block's own segment (no global counter: a
+// per-wave atomic on one counter serialised 2,048 waves, 26 of the kernel's 31
+// us, and even one per block was a returning atomic on the critical path).
+// Every thread of the block calls it; `wcount` = LDS scratch of blockDim/64 + 1
+// words; `used` = the segment's records so far (uniform), advanced here.
+__device__ __forceinline__ void insert_piece(const LogLaunch& a, uint64_t t, uint32_t* wcount, uint32_t& used) {
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
     bool fresh = false;
     uint32_t slot = 0;
@@ -1103,23 +1104,29 @@ __device__ __forceinline__ void insert_piece(const LogLaunch& a, uint64_t t, uin
     const uint64_t m = __ballot(fresh);
     if (lane == 0) wcount[wv] = (uint32_t)__popcll(m);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t tot = 0;
-        for (uint32_t w = 0; w < nw; w++) tot += wcount[w];
-        wcount[nw] = tot ? atomicAdd(a.head_count, tot) : 0u;
+    uint32_t base = used, tot = 0;
+    for (uint32_t w = 0; w < nw; w++) {
+        base += w < wv ? wcount[w] : 0u;
+        tot += wcount[w];
     }
-    __syncthreads();
-    uint32_t base = wcount[nw];
-    for (uint32_t w = 0; w < wv; w++) base += wcount[w];
+    used += tot;
     // the head record: the page's table slot and the claiming piece (the list's
     // tail: a page whose entry still names it has no other piece)
-    if (fresh) reinterpret_cast<uint2*>(a.heads)[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] =
-        make_uint2(slot, (uint32_t)t);
+    if (fresh)
+        reinterpret_cast<uint2*>(a.heads)[(uint64_t)blockIdx.x * a.seg_cap + base +
+                                          (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = make_uint2(slot, (uint32_t)t);
+    __syncthreads();  // wcount reused by the next chunk
 }
 
+// Block b inserts chunks b, b + grid, ... of kInsertThreads pieces into its
+// head segment and leaves its record count in seg_count[b].
 __global__ __launch_bounds__(kInsertThreads) void log_insert_kernel(LogLaunch a) {
     __shared__ uint32_t wcount[kInsertThreads / 64 + 1];
-    insert_piece(a, (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, wcount);
+    uint32_t used = 0;
+    const uint64_t chunks = (a.n_pieces + kInsertThreads - 1) / kInsertThreads;
+    for (uint64_t c = blockIdx.x; c < chunks; c += gridDim.x)
+        insert_piece(a, c * kInsertThreads + threadIdx.x, wcount, used);
+    if (threadIdx.x == 0) a.seg_count[blockIdx.x] = used;
 }
 
 // The bytes of one update that fall inside one page, page-relative: page bytes
@@ -1382,14 +1389,32 @@ __device__ __forceinline__ void load_rows(uint32_t (&w)[M], const unsigned char*
 template <int M, bool Delta>
 __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab) {
     constexpr int WV = log_waves(M, Delta);
+    // the insert blocks' segment counts: lane l holds segments 4l .. 4l+3,
+    // scum = inclusive prefix of the lanes' sums; head h (in segment order) is
+    // record h - (heads before its segment) of its segment
+    constexpr int kSpl = kInsertBlocks / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t sc[kSpl];  // (32-bit: these stay live over the page loop)
+    uint32_t ssum = 0;
+#pragma unroll
+    for (int j = 0; j < kSpl; j++) {
+        const uint32_t sg = kSpl * lane + j;
+        sc[j] = sg < a.n_segs ? a.seg_count[sg] : 0u;
+        ssum += sc[j];
+    }
+    uint32_t scum = ssum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(scum, d, 64);
+        if (lane >= (uint32_t)d) scum += o;
+    }
     // an equal share of the heads per workgroup: [hb0, hb1); a workgroup without
     // one (a small log) leaves before filling its 160 KiB of LDS
-    const uint32_t Hall = *a.head_count;
+    const uint32_t Hall = __builtin_amdgcn_readlane(scum, 63);
     const uint32_t hb0 = (uint32_t)((uint64_t)Hall * blockIdx.x / gridDim.x);
     const uint32_t hb1 = (uint32_t)((uint64_t)Hall * (blockIdx.x + 1) / gridDim.x);
     if (hb0 >= hb1) return;
     fill_lds<64 * WV>(tab, static_cast<const uint4*>(a.image));
-    const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t c0 = lane << 2 & 0x7Cu;
     const uint32_t c1 = c0 | 0x10000u;
@@ -1421,15 +1446,51 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         // lane k <- head base + k*W (clamped loads: no branches around them)
         const uint64_t ih = (uint64_t)base + (uint64_t)lane * W;
         const bool hv = ih < H;
+        // the lane's head in its segment: from the segment holding head `base`,
+        // walk the (few) segments the batch spans
+        const uint32_t hi = hv ? (uint32_t)ih : base;
+        // the segment holding head `base`: lane tl's segments, then the first of them past it
+        uint32_t seg, sbefore;
+        {
+            const uint32_t tl = (uint32_t)__builtin_ctzll(__ballot(scum > base));
+            uint32_t st = tl ? __builtin_amdgcn_readlane(scum, tl - 1) : 0u, s = kSpl * tl;
+            bool found = false;
+#pragma unroll
+            for (int j = 0; j < kSpl; j++) {
+                const uint32_t v = __builtin_amdgcn_readlane(sc[j], tl);
+                if (!found) {
+                    if (st + v > base) {
+                        found = true;
+                        s = kSpl * tl + j;
+                    } else {
+                        st += v;
+                    }
+                }
+            }
+            seg = s;
+            sbefore = st;
+            const uint32_t last = base + 63u < H - 1u ? base + 63u : H - 1u;
+            for (;;) {
+                uint32_t v = sc[0];
+#pragma unroll
+                for (int j = 1; j < kSpl; j++) v = (s % kSpl) == (uint32_t)j ? sc[j] : v;
+                const uint32_t cnt = __builtin_amdgcn_readlane(v, s / kSpl);
+                if (st + cnt > last || s + 1 >= a.n_segs) break;
+                st += cnt;
+                s++;
+                seg = hi >= st ? s : seg;
+                sbefore = hi >= st ? st : sbefore;
+            }
+        }
         // the head record gives the table slot AND the claiming piece, so the
         // claimer's descriptor loads beside the table entry: two dependent
         // round trips to a page's geometry instead of three (the list link is
         // needed by pages with several pieces only, far behind)
-        const uint2 hrec = reinterpret_cast<const uint2*>(a.heads)[hv ? ih : base];
+        const uint2 hrec = reinterpret_cast<const uint2*>(a.heads)[(uint64_t)seg * a.seg_cap + (hi - sbefore)];
         const uint32_t hslot = hrec.x, claimer = hrec.y;
         const unsigned long long ent = reinterpret_cast<const unsigned long long*>(a.table)[hslot];
         const UpdateDesc d = a.upd[claimer / a.slots];
-        if (a.done && hv) a.table[hslot] = 0ull;  // the slot is this lane's alone (one head per page)
+        if (a.clear_table && hv) a.table[hslot] = 0ull;  // the slot is this lane's alone (one head per page)
         const uint32_t key = (uint32_t)(ent >> 32) - 1u;  // the page
         const uint32_t pfirst = (uint32_t)ent - 1u;       // the list head (the latest piece)
         const uint32_t nxt = a.next[pfirst];              // consumed by the several-piece path only
@@ -1613,15 +1674,6 @@ template <int M, bool Delta>
 __global__ __launch_bounds__(64 * log_waves(M, Delta)) void log_pages_kernel(LogLaunch a) {
     __shared__ uint32_t tab[kLdsBytes / 4];
     log_pages_body<M, Delta>(a, tab);
-    if (a.done) {
-        // every thread of the block has read head_count (the early exit is per
-        // block); the last block out leaves the counters zero for the next call
-        __syncthreads();
-        if (threadIdx.x == 0 && atomicAdd(a.done, 1u) == gridDim.x - 1) {
-            atomicExch(a.head_count, 0u);
-            atomicExch(a.done, 0u);
-        }
-    }
 }
 
 // A small log (<= 64 writes of <= one page each: at most 2 pieces a write) in
@@ -2104,8 +2156,8 @@ hipError_t launch_shift(const uint32_t* crcs, const uint64_t* shift_bytes, uint6
 
 hipError_t launch_log_insert(const LogLaunch& a, hipStream_t s) {
     if (a.n_pieces == 0) return hipSuccess;
-    hipLaunchKernelGGL(log_insert_kernel, dim3((uint32_t)((a.n_pieces + kInsertThreads - 1) / kInsertThreads)),
-                       dim3(kInsertThreads), 0, s, a);
+    if (a.n_segs == 0 || a.n_segs > kInsertBlocks) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(log_insert_kernel, dim3(a.n_segs), dim3(kInsertThreads), 0, s, a);
     return hipGetLastError();
 }
 

@@ -410,3 +410,39 @@ def log_steal_schedule(Hall: int, grid: int, wv: int, speed, tail_div: int = 4, 
         except StopIteration:
             pass
     return owner, cleared, read_ok, end
+
+
+def log_head_segments(counts, base: int, H: int, kspl: int = 4):
+    """The write-log page kernel's head addressing (round 4): insert block b
+    leaves counts[b] head records in its own segment; a batch of heads
+    [base, min(base + 64, H)) in segment order finds, per lane, (segment,
+    record) -- the segment holding `base` by a register search, then a walk
+    over the segments the batch spans.  Returns [(segment, record)] per head."""
+    counts = list(counts) + [0] * (64 * kspl - len(counts))
+    n_segs = len(counts)
+    # lane l holds segments kspl*l .. kspl*l + kspl-1; scum = inclusive prefix of the lane sums
+    lane_sum = [sum(counts[kspl * l:kspl * l + kspl]) for l in range(64)]
+    scum = np.cumsum(lane_sum)
+    tl = int(np.argmax(scum > base))
+    st = int(scum[tl - 1]) if tl else 0
+    s = kspl * tl
+    for j in range(kspl):
+        v = counts[kspl * tl + j]
+        if st + v > base:
+            s = kspl * tl + j
+            break
+        st += v
+    seg = [s] * 64
+    sbefore = [st] * 64
+    his = [base + l if base + l < H else base for l in range(64)]
+    last = min(base + 63, H - 1)
+    while True:
+        cnt = counts[s]
+        if st + cnt > last or s + 1 >= n_segs:
+            break
+        st += cnt
+        s += 1
+        for l in range(64):
+            if his[l] >= st:
+                seg[l], sbefore[l] = s, st
+    return [(seg[l], his[l] - sbefore[l]) for l in range(64) if base + l < H]

@@ -158,3 +158,26 @@ def test_write_log_tail_stealing_rehashes_every_page_once(Hall, grid, wv):
     assert min(owner) >= 0 and all(cleared) and ok
     _, _, _, end0 = km.log_steal_schedule(Hall, grid, wv, speed, max_steals=0, start=start)
     assert max(end) <= max(end0)
+
+
+@pytest.mark.parametrize("n_segs", [1, 3, 128, 256])
+def test_write_log_head_segments_map_every_head_once(n_segs):
+    """The write-log page kernel finds head h in the insert blocks' segments
+    (per-block head lists, no global counter): every batch of 64 heads maps each
+    head to the right (segment, record), across empty segments and segment ends."""
+    rng = np.random.default_rng(n_segs)
+    for trial in range(30):
+        counts = rng.integers(0, 900, n_segs)
+        if trial % 3 == 0:
+            counts[rng.random(n_segs) < 0.5] = 0  # many empty segments
+        if trial % 5 == 0:
+            counts[:] = rng.integers(0, 3, n_segs)  # tiny segments: a batch spans dozens
+        total = int(counts.sum())
+        if total == 0:
+            continue
+        want = [(s, k) for s in range(n_segs) for k in range(int(counts[s]))]
+        for _ in range(20):
+            H = int(rng.integers(1, total + 1))
+            base = int(rng.integers(0, H))
+            got = km.log_head_segments(counts, base, H)
+            assert got == want[base:min(base + 64, H)]
