@@ -107,7 +107,7 @@ struct UpdateDesc {
 // pieces in log order in registers, stores the changed rows and rehashes it.
 // A page with more than 64 pieces is finished by its wave replaying the log.
 constexpr uint32_t kNoPiece = 0xFFFFFFFFu;
-constexpr uint32_t kInsertThreads = 512;   // pieces per insert chunk (one per thread; 512 vs 1024: every CU busy, A/B below)
+constexpr uint32_t kInsertThreads = 512;   // pieces per insert chunk, one a thread (512: every CU busy; profiles/write_log_insert_threads_ab_r04.txt)
 constexpr uint32_t kInsertBlocks = 256;    // insert blocks at most (grid-stride over chunks): head segments
 constexpr int kLogWaves = 12;  // waves per CU of the write-log page kernel at 8 KiB pages (A/B at 4 KiB, round 1: 12 beats 8 by ~6 %)
 constexpr int kLogWavesFull = 16;   // full mode, pages <= 4 KiB: 103 VGPRs since the row offsets went into the offset field
