@@ -970,6 +970,40 @@ def test_write_log_random_configs(dev, oracle, seed):
     assert (u32(crcs) == oracle.page_crcs(want, pb)).all(), (pb, n, max_len, delta)
 
 
+@pytest.mark.parametrize("delta", [False, True])
+def test_write_log_many_segments_and_batches(dev, oracle, delta):
+    """A log big enough for every layer of the write log's bookkeeping:
+    200,000 writes of 1 B .. 3 pages (4 pieces a write: 800,000 pieces, 1,563
+    insert chunks, so each of the 256 insert blocks fills its head segment from
+    6-7 chunks) over a 1 GiB pool (~260,000 touched pages: waves with more than
+    64 heads run several batches, each batch finding its heads across segment
+    ends).  Bytes == in-order host application, every page CRC == the oracle."""
+    from curve_amd import crc as C
+    rng = np.random.default_rng(4242 + delta)
+    pb, n = 4096, 200000
+    pool_bytes = 1 << 30
+    host = rng.integers(0, 256, pool_bytes, dtype=np.uint8)
+    d_pool = to_dev(host, dev)
+    crcs = C.page_crc(d_pool, pb)
+    max_len = 3 * pb
+    lens = rng.integers(1, 2 * pb, n).astype(np.uint32)
+    long = rng.random(n) < 0.3  # 3-page writes: 4 pieces
+    lens[long] = rng.integers(2 * pb, max_len + 1, int(long.sum()))
+    dst = rng.integers(0, pool_bytes - max_len, n).astype(np.uint64)
+    src_data = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    src_off = rng.integers(0, (1 << 20) - max_len, n).astype(np.uint64)
+    rec = C.log_records(dst, src_off, lens)
+    d_log = torch.from_numpy(rec.view(np.uint8)).to(dev)
+    C.apply_log(d_pool, crcs, to_dev(src_data, dev), d_log, n, max_len, pb, delta=delta)
+    want = host
+    for i in range(n):
+        want[dst[i]:dst[i] + lens[i]] = src_data[src_off[i]:src_off[i] + lens[i]]
+    assert (d_pool.cpu().numpy() == want).all()
+    assert (u32(crcs) == oracle.page_crcs(want, pb, threads=8)).all()
+    del d_pool, crcs
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("seed", range(16))
 def test_verify_reads_random_configs(dev, oracle, seed):
     """Randomised read batches (1..2000 reads: the one-launch and the count +
