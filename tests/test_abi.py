@@ -90,7 +90,7 @@ def test_argument_checks_need_no_gpu():
 
 def test_write_log_work_sizing_limits():
     """cc_apply_log_work_bytes (host arithmetic only): the caller's buffer holds
-    a list link and a touched-page slot per piece (the hash table is the
+    a list link per piece and the insert blocks' head segments (the hash table is the
     engine's: >= 8 entries per piece in a power of two up to 2^32 slots, never
     fewer than 4 per piece), and a log whose table would need more than 2^32
     slots at 4 per piece (32-bit slot indices) is refused with 0, not truncated."""
@@ -102,3 +102,14 @@ def test_write_log_work_sizing_limits():
     assert L.cc_apply_log_work_bytes((1 << 29) + 1, 4096, 4096) == 0   # would need 2^33 slots
     assert L.cc_apply_log_work_bytes(0, 4096, 4096) == 0
     assert L.cc_apply_log_work_bytes(10, 0, 4096) == 0
+    # the buffer holds a 4-byte link per piece, the head segments (one per insert
+    # block, each as long as the pieces of the 512-piece chunks that block takes:
+    # at most 256 blocks, grid-stride beyond) and 256 segment counts
+    for n, max_len in ((1, 1), (65536, 4096), (200000, 3 * 4096), (1 << 20, 4096)):
+        pieces = n * ((max_len - 1) // 4096 + 2)
+        chunks = -(-pieces // 512)
+        segs = min(chunks, 256)
+        cap = -(-chunks // segs) * 512
+        need = L.cc_apply_log_work_bytes(n, max_len, 4096)
+        assert need >= pieces * 4 + segs * cap * 8 + 256 * 4, (n, max_len, need)
+        assert need <= pieces * 4 + segs * cap * 8 + 256 * 4 + 3 * 256, (n, max_len, need)
