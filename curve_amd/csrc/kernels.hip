@@ -1446,10 +1446,10 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         // lane k <- head base + k*W (clamped loads: no branches around them)
         const uint64_t ih = (uint64_t)base + (uint64_t)lane * W;
         const bool hv = ih < H;
-        // the lane's head in its segment: from the segment holding head `base`,
-        // walk the (few) segments the batch spans
+        // the lane's head in its segment: the segment holding head `base` (lane
+        // tl's segments, then the first of them past it), then a walk over the
+        // (few) segments the batch spans
         const uint32_t hi = hv ? (uint32_t)ih : base;
-        // the segment holding head `base`: lane tl's segments, then the first of them past it
         uint32_t seg, sbefore;
         {
             const uint32_t tl = (uint32_t)__builtin_ctzll(__ballot(scum > base));
