@@ -936,8 +936,8 @@ __global__ __launch_bounds__(256) void fold_kernel_wave(const uint32_t* __restri
 // Fused scan epilogue (one launch per batch instead of fold + fold + combine +
 // digest): block b = chunk b, 256 threads.  Thread t loads its q page CRCs
 // (coalesced), folds them by Horner through an LDS product table of
-// x^(8*page_bytes), then a combine tree over threads (shuffles inside a wave
-// with LDS product tables, LDS across the 4 waves): after slice_shift levels thread (k << slice_shift)
+// x^(8*page_bytes), then a combine tree over threads (shuffles inside a wave,
+// LDS across the 4 waves): after slice_shift levels thread (k << slice_shift)
 // holds slice k's CRC (ScanMap.crc), after 8 levels thread 0 holds the chunk
 // data CRC -> file CRC = combine(metapage CRC, data CRC, chunk_bytes) -> digest
 // contribution atomicXor'ed into its copyset.
@@ -950,26 +950,16 @@ __device__ __forceinline__ uint32_t mul_tab(const uint32_t* __restrict__ t, uint
 }
 
 __global__ __launch_bounds__(256) void epilogue_kernel(EpilogueLaunch a) {
-    // the Horner table and the in-wave combine levels 0..5, copied once per block
-    // (levels from global memory: 4.4 us more per scan step, profiles/epilogue_lds_ab_r04.txt)
-    __shared__ uint32_t mt[7 * 1024];
+    __shared__ uint32_t mt[1024];  // x^(8 page_bytes) product table (Horner), copied once per block
     __shared__ uint32_t part[4];
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    for (uint32_t i = t; i < 7 * 1024; i += 256) mt[i] = a.mtab[i];
+    for (uint32_t i = t; i < 1024; i += 256) mt[i] = a.mtab[i];
     __syncthreads();
     const uint32_t slices = 256u >> a.slice_shift;
     const uint32_t* lvl = a.mtab + 1024;           // level k table at lvl + 1024 k
     const uint32_t* chk = a.mtab + 9 * 1024;
     for (uint64_t c = blockIdx.x; c < a.n_chunks; c += gridDim.x) {
         const uint32_t* p = a.page_crcs + c * a.pages_per_chunk + (uint64_t)t * a.q;
-        uint32_t meta = 0, grp = 0, aft = 0;
-        if (t == 0) {
-            meta = a.meta_crcs[c];
-            if (a.digest) {
-                grp = a.group[c];
-                aft = a.after_mult[c];
-            }
-        }
         auto horner = [&](uint32_t s, uint32_t w) {
             const uint32_t u = __builtin_amdgcn_bitop3_b32(mt[s & 255u], mt[256 + ((s >> 8) & 255u)],
                                                            mt[512 + ((s >> 16) & 255u)], 0x96);
@@ -1001,7 +991,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(EpilogueLaunch a) {
 #pragma unroll
         for (uint32_t k = 0; k < 6; k++) {
             const uint32_t other = __shfl_down(s, 1u << k, 64);
-            if ((lane & ((2u << k) - 1u)) == 0) s = mul_tab(mt + 1024 * (k + 1), s) ^ other;
+            if ((lane & ((2u << k) - 1u)) == 0) s = mul_tab(lvl + 1024 * k, s) ^ other;
             if (k + 1 == a.slice_shift && (t & ((2u << k) - 1u)) == 0) a.slice_crcs[c * slices + (t >> a.slice_shift)] = s;
         }
         // levels 6..7 across the 4 waves
@@ -1016,9 +1006,9 @@ __global__ __launch_bounds__(256) void epilogue_kernel(EpilogueLaunch a) {
             }
             const uint32_t data = mul_tab(lvl + 7 * 1024, w0) ^ w1;
             if (a.slice_shift == 8) a.slice_crcs[c] = data;
-            const uint32_t file = mul_tab(chk, meta) ^ data;
+            const uint32_t file = mul_tab(chk, a.meta_crcs[c]) ^ data;
             if (a.file_crcs) a.file_crcs[c] = file;
-            if (a.digest) atomicXor(a.digest + grp, mulmod_dev(aft, file));
+            if (a.digest) atomicXor(a.digest + a.group[c], mulmod_dev(a.after_mult[c], file));
         }
         __syncthreads();
     }
