@@ -54,6 +54,7 @@ def parse():
     p.add_argument("--stream-chunks", type=int, default=10000, help="config-4 stream leg (0 = skip)")
     p.add_argument("--stream-chunks-per-rank", type=int, default=2000, help="N>1: streamed chunks per rank")
     p.add_argument("--file-chunks", type=int, default=128, help="datastore read-path leg (0 = skip)")
+    p.add_argument("--file-passes", type=int, default=5, help="datastore read-path leg: passes per io-thread count")
     p.add_argument("--wal-entries", type=int, default=65536, help="WAL replay leg: entries per batch (0 = skip)")
     p.add_argument("--comm-timeout-ms", type=int, default=60000, help="N>1: bound on the native RCCL init")
     p.add_argument("--exchange-timeout-ms", type=int, default=120000,
@@ -272,7 +273,8 @@ def stream_all_ranks_leg(args, rank, world, dev):
     CPU primitive over every rank's chunks."""
     from curve_amd import crc as C
     from curve_amd.pool import copyset_layout, reduce_digests
-    n, pool_n, per = args.stream_chunks_per_rank, 64, 100
+    n, per = args.stream_chunks_per_rank, 100
+    pool_n = min(64, n)  # distinct pinned 16 MiB chunks per rank (1 GiB at most)
     total = n * world
     lay = copyset_layout(list(range(total)), [i // per for i in range(total)],
                          [C.CHUNK_SIZE + C.META_PAGE_SIZE] * total)
@@ -322,12 +324,25 @@ def files_leg(args):
             paths.append(p)
         out = {"files": n, "file_bytes": C.CHUNK_SIZE + C.META_PAGE_SIZE, "source": "tmp dir, page-cache resident"}
         C.scan_files(paths[:4])  # warm
-        for t in (4, 8, 16):
-            t0 = time.perf_counter()
-            st, _, _, _ = C.scan_files(paths, io_threads=t)
-            el = time.perf_counter() - t0
-            assert (st == 0).all()
-            out[f"GiBps_io{t}"] = round(n * (C.CHUNK_SIZE + C.META_PAGE_SIZE) / GiB / el, 2)
+        fb = n * (C.CHUNK_SIZE + C.META_PAGE_SIZE) / GiB
+        # median of --file-passes passes per io-thread count, the counts
+        # interleaved pass by pass (a slow stretch of the box hits every count);
+        # io_threads=0 is the engine's default (from the affinity and cgroup quota)
+        counts = (0, 4, 8, 16)
+        runs = {t: [] for t in counts}
+        for _ in range(args.file_passes):
+            for t in counts:
+                t0 = time.perf_counter()
+                st, _, _, _ = C.scan_files(paths, io_threads=t)
+                el = time.perf_counter() - t0
+                assert (st == 0).all()
+                runs[t].append(fb / el)
+        for t in counts:
+            key = "GiBps_default" if t == 0 else f"GiBps_io{t}"
+            out[key] = round(float(np.median(runs[t])), 2)
+            out[key + "_each"] = [round(x, 2) for x in runs[t]]
+        out["default_io_threads"] = C.default_io_threads()
+        out["passes"] = args.file_passes
         return out
     finally:
         shutil.rmtree(d, ignore_errors=True)
@@ -760,11 +775,16 @@ def main():
         torch.cuda.synchronize()
 
     def fail(e):
-        # one JSON error line (every rank: the driver reads rank 0's), then leave
-        # at once -- no barrier, no teardown that could wait for the lost peer
-        print(json.dumps({"error": f"rank {rank}: digest exchange failed: {e}", "n_gpus": world,
-                          "metric": "GiB/s CRC32C over 4KiB pages (device-resident) + % HBM roofline, 1/2/4/8 GPU",
-                          "value": None}), flush=True)
+        # one JSON error line -- rank 0's on stdout (the line the driver reads),
+        # every other rank's on stderr (ranks share the launcher's stdout: two
+        # lines written at once could interleave into one unparsable line) --
+        # then leave at once: no barrier, no teardown that could wait for the
+        # lost peer
+        line = json.dumps({"error": f"rank {rank}: digest exchange failed: {e}", "n_gpus": world,
+                           "metric": "GiB/s CRC32C over 4KiB pages (device-resident) + % HBM roofline, 1/2/4/8 GPU",
+                           "value": None})
+        print(line, file=sys.stdout if rank == 0 else sys.stderr, flush=True)
+        sys.stdout.flush()
         sys.stderr.flush()
         os._exit(3)
 
@@ -787,13 +807,7 @@ def main():
         local = torch.zeros_like(digest)
         pool_scan(pool, after_mult, group, local, comm=None, stream=stream)
         digest_check = bool(torch.equal(native, reduce_digests(local, dist)))
-    # untimed, every N: the exchanged digests of two copysets == the sorted-name
-    # chain of those copysets' files over the WHOLE pool, from the bytes by
-    # libcurvecrc's CPU primitive (each rank hashes its own files on the host;
-    # partials XOR-reduced over torch.distributed): the exchange checked against
-    # an independent computation, not only against another transport
     final_digest = full_digest[0] if (world > 1 and comm is None) else digest
-    cpu_digest = cpu_digest_check(pool, lay, lo, n, final_digest, dist if world > 1 else None, dev)
     kern_each = [a.elapsed_time(b) for a, b in ev]
     kern_ms = float(np.mean(kern_each))
     # every rank's mean page-kernel time: the aggregate roofline is set by the slowest
@@ -804,18 +818,21 @@ def main():
         dist.all_gather_into_tensor(ga, kt)
         rank_kern = [float(x) for x in ga.cpu().tolist()]
 
-    # verify pass (after the timed region): every page must match
-    # (4 back-to-back calls, the first untimed: one call right after a host sync
-    # would time the clock ramp, not the kernel)
+    # verify pass (after the timed region, before any host-side work that idles
+    # the GPU): every page must match.  The clock floor first (the gather above
+    # and the host sync leave the GPU idle; round 4 timed the verify pass right
+    # after a host CRC check and read the clock ramp: 5,104 vs ~6,400 GiB/s),
+    # then 5 calls back to back, each between its own event pair.
     cnt = torch.tensor([0, -1], dtype=torch.int64, device=dev)
-    C.page_verify(pool.data, pool.page_crcs, pb, counters=cnt)
-    ve0, ve1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ve0.record(stream)
-    for _ in range(3):
+    warm_clock(lambda: C.page_verify(pool.data, pool.page_crcs, pb, counters=cnt), min(args.clock_warm_ms, 500.0))
+    vev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+    for ve0, ve1 in vev:
+        ve0.record(stream)
         C.page_verify(pool.data, pool.page_crcs, pb, counters=cnt)
-    ve1.record(stream)
+        ve1.record(stream)
     torch.cuda.synchronize()
-    verify_ms = ve0.elapsed_time(ve1) / 3
+    verify_each = [a.elapsed_time(b) for a, b in vev]
+    verify_ms = float(np.mean(verify_each))
     bad = int(cnt[0].item())
 
     # measured read ceiling of THIS device: pure nt read of the same 16 GiB, same stream
@@ -844,6 +861,20 @@ def main():
             lo_ms.append(pe0.elapsed_time(pe1))
     del lo_out
     load_only_gbs = pool.data.numel() // 4096 * ALG_BYTES_PER_PAGE / (float(np.mean(lo_ms)) * 1e-3) / 1e9
+
+    # untimed, every N, after the device timings above (it idles the GPU for tens
+    # of ms): the exchanged digests of two copysets == the sorted-name chain of
+    # those copysets' files over the WHOLE pool, from the bytes by libcurvecrc's
+    # CPU primitive (each rank hashes its own files on the host; partials
+    # XOR-reduced over torch.distributed): the exchange checked against an
+    # independent computation, not only against another transport
+    cpu_digest = cpu_digest_check(pool, lay, lo, n, final_digest, dist if world > 1 else None, dev)
+    shard_ranges = [[lo, hi]]
+    if world > 1:
+        st = torch.tensor([lo, hi], dtype=torch.int64, device="cpu" if backend == "gloo" else dev)
+        sg = torch.empty(2 * world, dtype=torch.int64, device=st.device)
+        dist.all_gather_into_tensor(sg, st)
+        shard_ranges = sg.view(world, 2).cpu().tolist()
 
     n_pages = n * chunk // pb
     # the timed launch: with a metapage the size of a page and a batch big enough
@@ -902,7 +933,14 @@ def main():
                      "frac_of_read_probe": round(achieved / probe_gbs, 4),
                      "load_only_probe_GBps": round(load_only_gbs, 1),
                      "frac_of_load_only_probe": round(achieved / load_only_gbs, 4)},
-        "verify": {"GiBps": round(n * chunk / GiB / (verify_ms * 1e-3), 2), "bad_pages": bad},
+        "verify": {"GiBps": round(n * chunk / GiB / (verify_ms * 1e-3), 2), "bad_pages": bad,
+                   "ms_avg": round(verify_ms, 4), "ms_each": [round(x, 4) for x in verify_each],
+                   "spread_pct": round((max(verify_each) - min(verify_each)) / min(verify_each) * 100, 2),
+                   "alg_frac_of_hbm_peak": round(n_pages * (pb + 4) / (verify_ms * 1e-3) / 1e9
+                                                 / HBM_PEAK_GBS, 4),
+                   "note": "cc_page_verify_dev over the pool after a clock floor; alg bytes = 4096 read + "
+                           "4 expected CRC read per page"},
+        "shard_ranges": shard_ranges,
     }
     out["digest_check_cpu"] = cpu_digest
     if world > 1:

@@ -116,6 +116,7 @@ SIGNATURES = {
     "cc_lds_image": (_int, [_vp, _sz]),
     "cc_scan_files": (_int, [ctypes.POINTER(ctypes.c_char_p), _u64, _u32, _u32, _u32, _u32, _u32, _vp,
                               ctypes.POINTER(CcFileResult)]),
+    "cc_default_io_threads": (_u32, []),
     "cc_scan_host": (_int, [ctypes.POINTER(CcChunkSrc), _u64, _u32, _u32, _u32, _u32, _vp, _vp, _vp]),
     "cc_apply_log_work_bytes": (_u64, [_u64, _u32, _u32]),
     "cc_apply_log_dev": (_int, [_vp, _u64, _u32, _vp, _vp, _u64, _u32, _vp, _vp, _u64, _vp]),

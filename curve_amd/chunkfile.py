@@ -116,7 +116,7 @@ def read_into(path: str, dst) -> int:
 
 
 def copyset_hash_dir(data_dir: str, chunk_size: int = C.CHUNK_SIZE, meta_size: int = C.META_PAGE_SIZE,
-                     io_threads: int = 8, page_bytes: int = C.PAGE_SIZE) -> str:
+                     io_threads: int = 0, page_bytes: int = C.PAGE_SIZE) -> str:
     """CopysetNode::GetHash over a real data directory: list, std::sort the
     names, chain CRC32 over whole files.  Chunk files (meta || data of the
     configured geometry: chunkserver.conf's chunk_size / meta_page_size, and

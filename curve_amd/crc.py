@@ -570,7 +570,7 @@ def verify_reads(pool, page_crcs, offsets, lengths, page_bytes: int = PAGE_SIZE,
 
 
 def scan_files(paths, chunk_bytes: int = CHUNK_SIZE, meta_bytes: int = META_PAGE_SIZE,
-               page_bytes: int = PAGE_SIZE, slice_bytes: int = SCAN_SIZE, io_threads: int = 8):
+               page_bytes: int = PAGE_SIZE, slice_bytes: int = SCAN_SIZE, io_threads: int = 0):
     """cc_scan_files: native pread + scan of chunk files.
     Returns (status[n] int32, meta_crcs[n], slice_crcs[n, S], file_crcs[n]) numpy."""
     import numpy as np
@@ -585,6 +585,11 @@ def scan_files(paths, chunk_bytes: int = CHUNK_SIZE, meta_bytes: int = META_PAGE
     mc = np.array([res[i].meta_crc for i in range(n)], dtype=np.uint32)
     fc = np.array([res[i].file_crc for i in range(n)], dtype=np.uint32)
     return st, mc, sc, fc
+
+
+def default_io_threads() -> int:
+    """cc_default_io_threads: the reader count scan_files(io_threads=0) uses."""
+    return int(lib().cc_default_io_threads())
 
 
 def as_u32(t) -> "list[int]":

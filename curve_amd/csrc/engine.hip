@@ -15,12 +15,15 @@
 
 #include <errno.h>
 #include <fcntl.h>
+#include <sched.h>
+#include <stdio.h>
 #include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
 
 #include <atomic>
 #include <condition_variable>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -89,12 +92,17 @@ struct Staging {
 // insert takes the context's table mutex).
 constexpr int kEpiSlots = 16;
 
-// Per-stream state (the page kernel's tail counters, the write log's table) is
-// keyed by stream.  hipStreamPerThread, hipStreamLegacy and the null stream are
-// pseudo-handles: one value standing for a different real stream in each
-// thread (per-thread default streams), so kernels of two threads could run
-// concurrently on one block or table.  Their key is the handle AND the calling
-// thread; a real stream's key is its handle.
+// Per-stream state (the page kernel's tail counters, the write log's table,
+// the range scratch) is keyed by stream.  The null stream and hipStreamLegacy
+// name ONE real stream of the device (the legacy default stream: this library
+// is built without per-thread default streams), so their key is the handle,
+// like a created stream's; the per-state mutex orders enqueues on it.
+// hipStreamPerThread names a different real stream in each thread: its key is
+// the handle AND the calling thread, and a thread's entries are dropped when
+// the thread exits (ThreadEntries below), so a later thread that reuses the
+// id (glibc reuses pthread_t) never inherits scratch whose kernels may still
+// run on the old thread's stream, and short-lived threads do not use up the
+// kMaxTailBlocks entries.
 struct StreamKey {
     hipStream_t s = nullptr;
     std::thread::id tid;
@@ -103,11 +111,80 @@ struct StreamKey {
 inline StreamKey stream_key(hipStream_t s) {
     StreamKey k;
     k.s = s;
-    if (s == nullptr || s == hipStreamLegacy || s == hipStreamPerThread) k.tid = std::this_thread::get_id();
+    if (s == hipStreamPerThread) k.tid = std::this_thread::get_id();
     return k;
 }
 
-struct DevCtx {
+// Persistent reader threads of cc_scan_files, one pool per device context:
+// created on first use (grown to the largest io_threads asked), parked on a
+// condition variable between batches, joined when the context is freed.  A
+// batch runs `fn(0)` on the caller and `fn(1..n-1)` on pool threads, and
+// returns when all have returned (round 4 spawned and joined a std::thread
+// set per 7-file batch: the spawns alone cost more as io_threads grew).
+class ReaderPool {
+   public:
+    ~ReaderPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        go_.notify_all();
+        for (auto& t : threads_) t.join();
+    }
+    // run fn(k) for k in [0, n): k = 0 on the calling thread
+    template <class F>
+    void run(uint32_t n, F&& fn) {
+        std::lock_guard<std::mutex> one(run_mu_);  // one batch at a time per pool
+        if (n > 1) grow(n - 1);
+        std::function<void(uint32_t)> job = fn;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &job;
+            want_ = n - 1;
+            taken_ = 0;
+            left_ = n - 1;
+            gen_++;
+        }
+        if (n > 1) go_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return left_ == 0; });
+        job_ = nullptr;
+    }
+
+   private:
+    void grow(uint32_t n) {
+        while (threads_.size() < n) threads_.emplace_back([this] { loop(); });
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            go_.wait(lk, [&] { return stop_ || (gen_ != seen && taken_ < want_); });
+            if (stop_) return;
+            if (taken_ >= want_) {  // this generation is fully staffed
+                seen = gen_;
+                continue;
+            }
+            const uint32_t k = 1 + taken_++;
+            seen = gen_;
+            std::function<void(uint32_t)>* job = job_;
+            lk.unlock();
+            (*job)(k);
+            lk.lock();
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    std::mutex run_mu_, mu_;
+    std::condition_variable go_, done_;
+    std::vector<std::thread> threads_;
+    std::function<void(uint32_t)>* job_ = nullptr;
+    uint64_t gen_ = 0;
+    uint32_t want_ = 0, taken_ = 0, left_ = 0;
+    bool stop_ = false;
+};
+
+struct DevCtx : std::enable_shared_from_this<DevCtx> {
     int device = -1;
     bool ready = false;
     int cus = 256;
@@ -152,6 +229,7 @@ struct DevCtx {
     };
     std::mutex range_mu;
     std::vector<RangeWork> range_works;
+    ReaderPool readers;  // cc_scan_files' io threads
     DevCtx() {
         for (int i = 0; i < kEpiSlots; i++) {
             epi_key[i].store(0);
@@ -162,6 +240,56 @@ struct DevCtx {
 };
 
 using CtxRef = std::shared_ptr<DevCtx>;
+
+// A thread's hipStreamPerThread entries, dropped when the thread exits: taken
+// out of the context's lists under their mutexes (no call can reach them after
+// that), then freed once the exiting thread's own per-thread stream -- the
+// only stream that used them -- has drained.  No lock is held while waiting.
+void drop_thread_entries(DevCtx* c, std::thread::id tid) {
+    StreamKey key;
+    key.s = hipStreamPerThread;
+    key.tid = tid;
+    std::vector<void*> dead;
+    auto take = [&](auto& vec, std::mutex& mu) {
+        std::lock_guard<std::mutex> lk(mu);
+        for (size_t i = 0; i < vec.size();) {
+            if (vec[i].s == key) {
+                if (vec[i].p) dead.push_back(vec[i].p);
+                vec.erase(vec.begin() + i);
+            } else {
+                i++;
+            }
+        }
+    };
+    take(c->tails, c->tail_mu);
+    take(c->log_tabs, c->log_mu);
+    take(c->range_works, c->range_mu);
+    if (dead.empty()) return;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (hipSetDevice(c->device) == hipSuccess) {
+        (void)hipStreamSynchronize(hipStreamPerThread);
+        for (void* p : dead) (void)hipFree(p);
+    }
+    if (cur >= 0) (void)hipSetDevice(cur);
+}
+
+struct ThreadEntries {
+    std::vector<std::weak_ptr<DevCtx>> ctxs;  // contexts holding entries of this thread
+    ~ThreadEntries() {
+        const std::thread::id tid = std::this_thread::get_id();
+        for (auto& w : ctxs)
+            if (std::shared_ptr<DevCtx> c = w.lock()) drop_thread_entries(c.get(), tid);
+    }
+};
+thread_local ThreadEntries t_entries;
+
+// Called when an entry keyed by hipStreamPerThread is created for the calling thread.
+void note_thread_entry(DevCtx* c) {
+    for (auto& w : t_entries.ctxs)
+        if (w.lock().get() == c) return;
+    t_entries.ctxs.push_back(c->weak_from_this());
+}
 
 constexpr int kMaxDevices = 64;
 std::mutex g_mu;                 // context creation / teardown only
@@ -329,6 +457,7 @@ DevCtx::TailBlock* tail_block(DevCtx* c, hipStream_t s) {
         return nullptr;
     }
     c->tails.push_back({key, static_cast<unsigned long long*>(p), 0u, false});
+    if (s == hipStreamPerThread) note_thread_entry(c);
     return &c->tails.back();
 }
 
@@ -568,16 +697,27 @@ int cc_engine_trim(void) {
     CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
-    std::lock_guard<std::mutex> lk(c->log_mu);  // no write-log call enqueues meanwhile
-    std::lock_guard<std::mutex> lr(c->range_mu);  // nor a range call
-    const hipError_t e = hipDeviceSynchronize();  // kernels of earlier calls may still use a table
-    if (e != hipSuccess) return map_err(e);
-    for (auto& t : c->log_tabs)
-        if (t.p) (void)hipFree(t.p);
-    c->log_tabs.clear();
-    for (auto& t : c->range_works)
-        if (t.p) (void)hipFree(t.p);
-    c->range_works.clear();
+    // take the cached tables and scratch out of the context under their
+    // mutexes (a call after this point creates fresh ones), then wait for the
+    // device WITHOUT the mutexes: a stream stuck in a collective whose peer is
+    // gone (what cc_comm_wait bounds) then blocks only this call, never the
+    // write-log / range / verify calls of other threads
+    std::vector<void*> dead;
+    {
+        std::lock_guard<std::mutex> lk(c->log_mu);
+        for (auto& t : c->log_tabs)
+            if (t.p) dead.push_back(t.p);
+        c->log_tabs.clear();
+    }
+    {
+        std::lock_guard<std::mutex> lk(c->range_mu);
+        for (auto& t : c->range_works)
+            if (t.p) dead.push_back(t.p);
+        c->range_works.clear();
+    }
+    const hipError_t e = hipDeviceSynchronize();  // kernels of earlier calls may still use them
+    if (e != hipSuccess) return map_err(e);  // (not freed: a faulted device keeps them)
+    for (void* p : dead) (void)hipFree(p);
     return CC_OK;
 }
 
@@ -734,6 +874,7 @@ DevCtx::RangeWork* range_work(DevCtx* c, hipStream_t s, uint64_t n, hipError_t* 
     if (!t) {
         if (c->range_works.size() >= kMaxTailBlocks) return nullptr;
         c->range_works.push_back({key, nullptr, 0, 0, false});
+        if (s == hipStreamPerThread) note_thread_entry(c);
         t = &c->range_works.back();
     }
     if (!t->p) {
@@ -1165,6 +1306,7 @@ DevCtx::LogTable* log_table(DevCtx* c, hipStream_t s, uint64_t entries, hipError
     if (!t) {
         if (c->log_tabs.size() >= kMaxTailBlocks) return nullptr;
         c->log_tabs.push_back({key, nullptr, 0, false});
+        if (s == hipStreamPerThread) note_thread_entry(c);
         t = &c->log_tabs.back();
     }
     if (!t->p) {
@@ -1543,6 +1685,41 @@ int cc_scan_host(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t chunk_b
 namespace {
 constexpr uint64_t kReadPiece = 2ull << 20;  // io work item
 
+// CPUs this process may run on: the affinity mask, capped by the cgroup v2
+// CPU quota (cpu.max) when there is one -- a GPU box hands each GPU a share of
+// a larger host, and readers beyond the quota only get throttled.
+uint32_t usable_cpus() {
+    cpu_set_t set;
+    uint32_t n = 0;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = (uint32_t)CPU_COUNT(&set);
+    if (n == 0) {
+        const long v = sysconf(_SC_NPROCESSORS_ONLN);
+        n = v > 0 ? (uint32_t)v : 1u;
+    }
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        unsigned long long per = 0;
+        if (fscanf(f, "%31s %llu", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0) {
+            const unsigned long long quota = strtoull(q, nullptr, 10);
+            const uint32_t cap = (uint32_t)(quota / per);  // whole CPUs of quota
+            if (cap >= 1 && cap < n) n = cap;
+        }
+        fclose(f);
+    }
+    return n;
+}
+
+// Default reader count: half the usable CPUs (the HIP runtime's threads and the
+// caller need the rest), at least 2, at most kMaxDefaultReaders.
+constexpr uint32_t kMaxDefaultReaders = 8;
+uint32_t default_io_threads() {
+    static const uint32_t n = [] {
+        const uint32_t h = usable_cpus() / 2;
+        return h < 2 ? 2u : (h > kMaxDefaultReaders ? kMaxDefaultReaders : h);
+    }();
+    return n;
+}
+
 int read_full(int fd, void* dst, size_t n, off_t off) {
     char* p = static_cast<char*>(dst);
     size_t got = 0;
@@ -1558,6 +1735,8 @@ int read_full(int fd, void* dst, size_t n, off_t off) {
     return 0;
 }
 }  // namespace
+
+uint32_t cc_default_io_threads(void) { return default_io_threads(); }
 
 int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_bytes, uint32_t meta_bytes,
                   uint32_t page_bytes, uint32_t slice_bytes, uint32_t io_threads, uint32_t* h_slice_crcs,
@@ -1590,7 +1769,7 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
     f2.m_unit = xpow((uint64_t)slice_bytes << 3);
     for (int t = 0; t < 6; t++) f2.m_tree[t] = xpow(((uint64_t)slice_bytes * (slices / 64) << t) << 3);
     const uint32_t m_chunk = xpow((uint64_t)chunk_bytes << 3);
-    const uint32_t threads = io_threads ? (io_threads > 64 ? 64 : io_threads) : 8;
+    const uint32_t threads = io_threads ? (io_threads > 64 ? 64 : io_threads) : default_io_threads();
 
     auto take = [&](int s) {
         return [&, s](uint64_t f, uint64_t nb) {
@@ -1621,7 +1800,7 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
             if (fd < 0) status = p ? -errno : CC_EINVAL;
             struct stat sb;
             if (!status && fstat(fd, &sb) != 0) status = -errno;
-            if (!status && (uint64_t)sb.st_size != per_file) status = CC_EINVAL;
+            if (!status && (uint64_t)sb.st_size != per_file) status = CC_EFORMAT;  // CSChunkFile::Open's FileFormatError
             fds[i] = fd;
             fst[i].store(status);
         }
@@ -1646,13 +1825,7 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
                 }
             }
         };
-        {
-            std::vector<std::thread> pool;
-            const uint32_t nt = (uint32_t)(items < threads ? items : threads);
-            for (uint32_t t = 1; t < nt; t++) pool.emplace_back(reader);
-            reader();
-            for (auto& th : pool) th.join();
-        }
+        c->readers.run((uint32_t)(items < threads ? items : threads), [&](uint32_t) { reader(); });
         for (uint64_t i = 0; i < nb; i++) {
             if (fds[i] >= 0) close(fds[i]);
             cc_file_result& fr = h_results[first + i];

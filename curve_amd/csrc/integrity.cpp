@@ -129,11 +129,15 @@ struct ChunkId {
     uint64_t size = 0;
 };
 
-int chunk_identity(const char* path, uint32_t meta_bytes, ChunkId* id) {
+// file_bytes != 0: the chunk geometry's file size; any other size is
+// CC_EFORMAT before the metapage is read, as CSChunkFile::Open checks the size
+// first (chunkserver_chunkfile.cpp:233-238, FileFormatError)
+int chunk_identity(const char* path, uint32_t meta_bytes, ChunkId* id, uint64_t file_bytes = 0) {
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) return -errno;
     struct stat sb;
     int rc = fstat(fd, &sb) == 0 ? 0 : -errno;
+    if (!rc && file_bytes && (uint64_t)sb.st_size != file_bytes) rc = CC_EFORMAT;
     std::vector<unsigned char> mp(meta_bytes);
     if (!rc) rc = read_full(fd, mp.data(), meta_bytes, 0);
     close(fd);
@@ -284,7 +288,7 @@ int store_table(const char* chunk_path, uint32_t meta_bytes, const char* table_p
     ChunkId id;
     int rc = chunk_identity(chunk_path, meta_bytes, &id);
     if (rc) return rc;
-    if (id.size != (uint64_t)meta_bytes + (uint64_t)n_pages * page_bytes) return CC_EINVAL;
+    if (id.size != (uint64_t)meta_bytes + (uint64_t)n_pages * page_bytes) return CC_EFORMAT;  // FileFormatError
     if (expect && (id.sn != expect->sn || id.mtime != expect->mtime || id.size != expect->size)) return CC_ESTALE;
     cc_pcrc_header h = {page_bytes, n_pages, id.sn, id.mtime, id.size, stamp ? stamp : now_ns()};
     std::vector<unsigned char> buf(cc_pcrc_encoded_bytes(n_pages));
@@ -346,7 +350,8 @@ int cc_integrity_check(const char* const* chunk_paths, const char* const* table_
             res[i].status = CC_EINVAL;
             continue;
         }
-        res[i].status = chunk_identity(chunk_paths[i], o->meta_bytes, &before[i]);
+        res[i].status = chunk_identity(chunk_paths[i], o->meta_bytes, &before[i],
+                                       (uint64_t)o->meta_bytes + o->chunk_bytes);
     }
     // 2. page CRCs of every chunk's data on the device (slice = page: the
     //    per-slice CRCs of cc_scan_files ARE the page CRCs)

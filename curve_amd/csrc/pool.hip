@@ -35,8 +35,10 @@ struct cc_comm {
     uint32_t* gather = nullptr;  // nranks x cap words of all-gather scratch on `device`
     uint64_t cap = 0;
     hipEvent_t done = nullptr;   // cc_comm_wait's completion marker
+    uint32_t stall_ms = 0;       // failpoint only: $CC_INJECT_EXCHANGE_STALL_MS, read once at init
     uint32_t* stall_abort = nullptr;  // failpoint only: host-mapped word the stall kernel polls
-    std::mutex mu;               // guards the scratch (re)allocation, the event and the failpoint word
+    uint32_t* stall_word = nullptr;   // its device address
+    std::mutex mu;               // guards the scratch (re)allocation and the event
 };
 
 static_assert(CC_COMM_ID_BYTES == sizeof(ncclUniqueId), "RCCL unique id size");
@@ -97,10 +99,11 @@ uint32_t wait_timeout_ms(uint32_t asked) {
 }
 
 // Failure injection (tests only; the reference's libfiu failpoints play this
-// role, test/failpoint/): $CC_INJECT_EXCHANGE_STALL_MS > 0 makes every digest
-// exchange first spin one wave on the stream for that long (at most 30 s), as
-// a collective whose peer stopped participating after init would sit in its
-// kernel.  cc_comm_wait must then give up at its deadline.  Like RCCL's own
+// role, test/failpoint/): $CC_INJECT_EXCHANGE_STALL_MS > 0 when a communicator
+// is created makes every digest exchange on it first spin one wave on the
+// stream for that long (at most 30 s), as a collective whose peer stopped
+// participating after init would sit in its kernel.  The variable is read once,
+// in cc_comm_init: the exchange path itself never consults the environment.  cc_comm_wait must then give up at its deadline.  Like RCCL's own
 // kernels, which poll the communicator's abort flag, the stall also ends as
 // soon as cc_comm_wait raises the comm's host-mapped abort word (an abort
 // cannot preempt a kernel: without the word it would wait out the stall).
@@ -123,6 +126,9 @@ __global__ void stall_kernel(uint64_t ticks, const uint32_t* abort_word) {
 }  // namespace
 
 extern "C" {
+
+static int comm_release(cc_comm* comm, bool abort);
+static int comm_release_abort(cc_comm* comm) { return comm_release(comm, true); }
 
 int cc_comm_unique_id(void* id, size_t bytes) {
     if (!id || bytes < sizeof(ncclUniqueId)) return CC_EINVAL;
@@ -156,6 +162,21 @@ int cc_comm_init_timeout(cc_comm** comm, int nranks, int rank, const void* id, s
     c->nranks = nranks;
     c->rank = rank;
     c->device = dev;
+    if ((c->stall_ms = injected_stall_ms())) {  // failpoint armed: its abort word, mapped for the stall kernel
+        void* p = nullptr;
+        void* d = nullptr;
+        hipError_t e = hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) {
+            c->stall_abort = static_cast<uint32_t*>(p);
+            *c->stall_abort = 0u;
+            e = hipHostGetDevicePointer(&d, p, 0);
+        }
+        if (e != hipSuccess) {
+            (void)comm_release_abort(c);
+            return map_hip(e);
+        }
+        c->stall_word = static_cast<uint32_t*>(d);
+    }
     *comm = c;
     return CC_OK;
 }
@@ -225,10 +246,7 @@ int cc_comm_wait(cc_comm* comm, void* stream, uint32_t timeout_ms) {
         if (failed || late) {
             // leave without the peers: the abort also releases the collective's
             // kernels still waiting for them, so the stream drains
-            {
-                std::lock_guard<std::mutex> lk(comm->mu);
-                if (comm->stall_abort) __atomic_store_n(comm->stall_abort, 1u, __ATOMIC_RELEASE);
-            }
+            if (comm->stall_abort) __atomic_store_n(comm->stall_abort, 1u, __ATOMIC_RELEASE);
             (void)ncclCommAbort(comm->nc);
             comm->nc = nullptr;
             return back(failed ? CC_ECOMM : CC_ETIMEDOUT);
@@ -257,24 +275,9 @@ int cc_digest_allreduce_dev(cc_comm* comm, uint32_t* d_digest, uint64_t n, void*
             comm->cap = n;
         }
     }
-    if (const uint32_t ms = injected_stall_ms()) {
-        uint32_t* word = nullptr;
-        {
-            std::lock_guard<std::mutex> lk(comm->mu);
-            if (!comm->stall_abort) {
-                void* p = nullptr;
-                const hipError_t e = hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent);
-                if (e != hipSuccess) return map_hip(e);
-                comm->stall_abort = static_cast<uint32_t*>(p);
-                *comm->stall_abort = 0u;
-            }
-            void* d = nullptr;
-            const hipError_t e = hipHostGetDevicePointer(&d, comm->stall_abort, 0);
-            if (e != hipSuccess) return map_hip(e);
-            word = static_cast<uint32_t*>(d);
-        }
-        hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, s, (uint64_t)ms * 100000ull,
-                           static_cast<const uint32_t*>(word));
+    if (comm->stall_ms) {  // failpoint (armed at init)
+        hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, s, (uint64_t)comm->stall_ms * 100000ull,
+                           static_cast<const uint32_t*>(comm->stall_word));
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return map_hip(e);
     }

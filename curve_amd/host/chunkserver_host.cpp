@@ -195,11 +195,11 @@ int GetCopysetHash(const std::string& dataDir, uint32_t chunkSize, uint32_t meta
     if (!chunkPaths.empty()) {
         std::vector<cc_file_result> res(chunkPaths.size());
         const uint32_t slice = std::min<uint32_t>(4u << 20, chunkSize);
-        if (cc_scan_files(chunkPaths.data(), chunkPaths.size(), chunkSize, metaPageSize, 4096, slice, 8, nullptr,
+        if (cc_scan_files(chunkPaths.data(), chunkPaths.size(), chunkSize, metaPageSize, 4096, slice, 0, nullptr,
                           res.data()) != CC_OK)
             return -1;
         for (size_t k = 0; k < chunkIdx.size(); k++) {
-            if (res[k].status < 0 && res[k].status != CC_EINVAL) return -1;  // open/read failed
+            if (res[k].status < 0 && res[k].status != CC_EFORMAT) return -1;  // open/read failed
             if (res[k].status == 0) {
                 fileCrc[chunkIdx[k]] = res[k].file_crc;
                 done[chunkIdx[k]] = true;
@@ -259,7 +259,7 @@ int ScanCopyset(const DataStoreOptions& opt, uint32_t logicalPoolId, uint32_t co
     const uint32_t slices = opt.chunkSize / scanSize;
     std::vector<cc_file_result> res(ids.size());
     std::vector<uint32_t> sc((size_t)ids.size() * slices);
-    if (!ids.empty() && cc_scan_files(cpaths.data(), ids.size(), opt.chunkSize, opt.metaPageSize, 4096, scanSize, 8,
+    if (!ids.empty() && cc_scan_files(cpaths.data(), ids.size(), opt.chunkSize, opt.metaPageSize, 4096, scanSize, 0,
                                       sc.data(), res.data()) != CC_OK)
         return -1;
     uint64_t index = firstIndex;

@@ -446,7 +446,7 @@ void IntegrityTableAndService() {  // CPU: codec, metapage sn, atomic store / lo
            CC_OK);
     EXPECT(cc_pcrc_load(TablePath(tdir, "chunk_1").c_str(), &g, got.data(), 256) == CC_OK && got == pc && g.chunk_sn == 42);
     EXPECT(cc_pcrc_store((dd + "/chunk_1").c_str(), 4096, TablePath(tdir, "x").c_str(), pc.data(), 255, 4096) ==
-           CC_EINVAL);  // geometry of the file
+           CC_EFORMAT);  // the file is not metapage + 255 pages (FileFormatError)
     EXPECT(cc_pcrc_load(TablePath(tdir, "none").c_str(), &g, nullptr, 0) == -ENOENT);
     // the service state machine (proto/integrity.proto) on a directory with no chunk of the geometry
     IntegrityOptions o;

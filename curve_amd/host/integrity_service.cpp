@@ -258,7 +258,7 @@ void IntegrityService::DoJob(IntegrityJob* job) {
         }
         // a file's own failure (metapage header CRC -> CC_ECORRUPT, unreadable,
         // -ENOENT: deleted between the listing and the check, or a size that
-        // changed since the listing -> CC_EINVAL) is that file's result, never
+        // changed since the listing -> CC_EFORMAT) is that file's result, never
         // the job's: the rest of the copyset is still checked
         for (size_t k = 0; k < nc; k++) {
             IntegrityFileResult& r = out[at[k]];

@@ -70,7 +70,7 @@ struct IntegrityOptions {
     uint32_t metaPageSize = 4096;
     uint32_t pageSize = 4096;
     uint32_t batch = 16;          // chunk files per cc_integrity_check call
-    uint32_t ioThreads = 8;
+    uint32_t ioThreads = 0;  // readers of cc_scan_files (0 = cc_default_io_threads())
     bool createMissing = true;    // write a table for a chunk without one
     bool refreshStale = true;     // rewrite stale / corrupt tables from the current bytes
 };

@@ -128,7 +128,7 @@ class FileResult:
 
 def check_files(paths: List[str], table_paths: List[str], chunk_size: int = C.CHUNK_SIZE,
                 meta_size: int = C.META_PAGE_SIZE, page_bytes: int = C.PAGE_SIZE, create_missing: bool = True,
-                refresh_stale: bool = True, io_threads: int = 8, bad_cap: int = 4096) -> List[FileResult]:
+                refresh_stale: bool = True, io_threads: int = 0, bad_cap: int = 4096) -> List[FileResult]:
     """cc_integrity_check over one batch of chunk files."""
     n = len(paths)
     if n == 0:
@@ -170,7 +170,7 @@ class IntegrityService:
 
     def __init__(self, chunk_size: int = C.CHUNK_SIZE, meta_size: int = C.META_PAGE_SIZE,
                  page_bytes: int = C.PAGE_SIZE, batch: int = 16, create_missing: bool = True,
-                 refresh_stale: bool = True, io_threads: int = 8):
+                 refresh_stale: bool = True, io_threads: int = 0):
         self._H = _lib.host_lib()
         o = _lib.CcIsvcOpts(chunk_size, meta_size, page_bytes, batch, io_threads, int(create_missing),
                             int(refresh_stale))

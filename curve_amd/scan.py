@@ -206,7 +206,7 @@ class DevicePool:
 
 def scan_copyset_dir(data_dir: str, logical_pool_id: int, copyset_id: int, first_index: int = 0,
                      chunk_size: int = CHUNK_SIZE, meta_size: int = META_PAGE_SIZE, scan_size: int = SCAN_SIZE,
-                     io_threads: int = 8, page_bytes: int = PAGE_SIZE) -> List[ScanMap]:
+                     io_threads: int = 0, page_bytes: int = PAGE_SIZE) -> List[ScanMap]:
     """ScanManager::ScanJobProcess over a copyset's chunk files on disk
     (scan_manager.cpp:210-296): for every chunk (`chunk_<id>`, the ChunkMap;
     snapshots are not scanned) with a V2 metapage, the metapage op then the

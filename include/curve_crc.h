@@ -90,9 +90,13 @@ typedef struct cc_opts {
 
 int cc_engine_init(const cc_opts* opts);  /* NULL = defaults */
 int cc_engine_fini(void);
-/* Free the device memory the engine caches per stream for the write log
- * (cc_apply_log_dev's hash tables) on the calling thread's device; the next
- * call re-creates what it needs.  Waits for the device to be idle first. */
+/* Free the device memory the engine caches per stream on the calling thread's
+ * device: the write log's hash tables (cc_apply_log_dev) and the range /
+ * verify-on-read scratch (cc_crc_ranges_dev, cc_verify_reads_dev); the next
+ * call re-creates what it needs.  The entries are detached under the engine's
+ * locks, then the call waits for the device to be idle WITHOUT holding them
+ * (other threads' calls proceed meanwhile) and frees them.  Entries of
+ * hipStreamPerThread are also dropped when their thread exits. */
 int cc_engine_trim(void);
 int cc_device_count(void);
 const char* cc_strerror(int code);
@@ -146,7 +150,15 @@ typedef struct cc_range {
  * batch is one stream of 4 KiB blocks split evenly over the device whatever
  * the range sizes (a range cut between waves is hashed in segments and
  * recombined), the last 1/32 handed out dynamically: ranges of any size mix
- * freely.  Two launches (a tile count, then the blocks). */
+ * freely.  ONE launch: the waves count the batch's tiles themselves.  The
+ * engine keeps scratch per stream for it (tile words, tail counters and the
+ * split ranges' accumulator pairs: 8 B x the next power of two >= n, at least
+ * 64 Ki pairs, plus ~9 KiB; at most 32 MiB + 9 KiB a stream -- a batch of more
+ * than 4 Mi ranges takes scratch of its own for the call -- for at most 256
+ * streams; shared with cc_verify_reads_dev; cc_engine_trim releases it).  The
+ * scratch is left zero by every launch that completes; after a device fault
+ * the context is unusable anyway (HIP errors are sticky) -- call
+ * cc_engine_fini, or cc_engine_trim, before using the engine again. */
 int cc_crc_ranges_dev(const void* d_buf, const cc_range* d_ranges, uint64_t n, uint32_t* d_out,
                       void* stream);
 
@@ -274,8 +286,11 @@ int cc_apply_log_delta_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_byte
  * mismatching pages of read i (caller zeroes it; UINT32_MAX marks a read that
  * runs past the pool); *d_bad_total += all mismatches.  Every touched page is
  * one work slot and the slots are split evenly over the device, so reads of
- * any size mix freely.  page_bytes = 256 * 2^k (k = 0..5).
- * d_work >= cc_verify_reads_work_bytes(n_reads) bytes of device scratch. */
+ * any size mix freely.  page_bytes = 256 * 2^k (k = 0..5).  ONE launch on the
+ * range kernel's schedule, using the stream's range scratch the engine keeps
+ * (see cc_crc_ranges_dev).  d_work / work_bytes are kept for ABI stability
+ * only: cc_verify_reads_work_bytes returns a constant 256 and d_work must be
+ * non-NULL, but the engine does not touch it. */
 uint64_t cc_verify_reads_work_bytes(uint64_t n_reads);
 int cc_verify_reads_dev(const void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const cc_range* d_reads,
                         uint64_t n_reads, const uint32_t* d_page_crcs, uint32_t* d_bad_per_read,
@@ -327,7 +342,8 @@ int cc_scan_host_digest(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t 
 
 /* Per-file outcome of cc_scan_files. */
 typedef struct cc_file_result {
-    int32_t status;    /* 0 ok; -errno from open/fstat/pread; CC_EINVAL: size != meta+chunk */
+    int32_t status;    /* 0 ok; -errno from open/fstat/pread; CC_EFORMAT: size != meta+chunk
+                          (CSChunkFile::Open's FileFormatError, chunkserver_chunkfile.cpp:233-238) */
     uint32_t meta_crc; /* CRC32(metapage) */
     uint32_t file_crc; /* CRC32(metapage || data) == CopysetNode::GetHash's per-file chain step */
     uint32_t reserved;
@@ -336,14 +352,19 @@ typedef struct cc_file_result {
 /* Native datastore read path + scan: open/fstat/pread every chunk FILE (the
  * whole-file read of CopysetNode::GetHash, copyset_node.cpp:942-962, and the
  * metapage + data reads of the scan ops, chunkserver_chunkfile.cpp:497-548)
- * with `io_threads` reader threads into pinned staging, overlapping the reads
- * of batch i+1 with the H2D copy + kernels of batch i.  Outputs as
- * cc_scan_host (slice CRCs may be NULL); a file whose size is not
- * meta_bytes + chunk_bytes, or that cannot be read, gets a non-zero status and
- * no CRCs (the caller chains such files on the CPU).  Blocking, thread-safe. */
+ * with `io_threads` reader threads (0 = cc_default_io_threads(); the caller is
+ * one of them) into pinned staging, overlapping the reads of batch i+1 with the
+ * H2D copy + kernels of batch i.  The readers are persistent: created once per
+ * device on first use, parked between batches.  Outputs as cc_scan_host (slice
+ * CRCs may be NULL); a file whose size is not meta_bytes + chunk_bytes gets
+ * CC_EFORMAT, one that cannot be read -errno, and neither gets CRCs (the caller
+ * chains such files on the CPU).  Blocking, thread-safe. */
 int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_bytes, uint32_t meta_bytes,
                   uint32_t page_bytes, uint32_t slice_bytes, uint32_t io_threads, uint32_t* h_slice_crcs,
                   cc_file_result* h_results);
+/* The reader count io_threads = 0 selects: half the CPUs this process may use
+ * (its affinity mask, capped by the cgroup v2 cpu.max quota), in [2, 8]. */
+uint32_t cc_default_io_threads(void);
 
 /* ------------------------------------------------------------------------
  * Full-pool integrity scan sharded over the GPUs of a node (BASELINE config 5,
@@ -492,7 +513,8 @@ int cc_chunk_meta_sn(const void* metapage, uint32_t bytes, uint64_t* sn);
  * recording the chunk's current sn, mtime and size.  Call it after the data
  * write it describes (the write path's CSChunkFile::Write, chunkserver_chunkfile.cpp:287-427),
  * under the chunk's write lock (CSChunkFile::rwLock_) so no other write lands
- * between the two. */
+ * between the two.  CC_EFORMAT when the file's size is not meta_bytes +
+ * n_pages x page_bytes (FileFormatError). */
 int cc_pcrc_store(const char* chunk_path, uint32_t meta_bytes, const char* table_path, const uint32_t* page_crcs,
                   uint32_t n_pages, uint32_t page_bytes);
 /* The same, but only if the chunk's identity is still `expect` (its sn,
@@ -524,13 +546,14 @@ typedef struct cc_integrity_opts {
     uint32_t chunk_bytes;    /* 16 MiB */
     uint32_t meta_bytes;     /* 4 KiB */
     uint32_t page_bytes;     /* 4 KiB */
-    uint32_t io_threads;     /* readers of cc_scan_files (0 = 8) */
+    uint32_t io_threads;     /* readers of cc_scan_files (0 = cc_default_io_threads()) */
     uint32_t create_missing; /* write a table for a chunk that has none */
     uint32_t refresh_stale;  /* rewrite stale / corrupt tables from the current bytes */
 } cc_integrity_opts;
 
 typedef struct cc_integrity_result {
-    int32_t status;       /* 0; -errno; CC_EINVAL (not chunk geometry); CC_ECORRUPT (metapage header) */
+    int32_t status;       /* 0; -errno; CC_EFORMAT (file size != metapage + chunk, checked first as
+                             CSChunkFile::Open does); CC_ECORRUPT (metapage header) */
     uint32_t table_state; /* CC_TABLE_* */
     uint32_t n_pages;
     uint32_t bad_pages;   /* pages whose bytes no longer match the (valid, current) table */

@@ -1457,7 +1457,9 @@ def test_scan_copyset_dir(dev, oracle, tmp_path):
 def test_scan_files(dev, oracle, tmp_path):
     """cc_scan_files: the engine opens/preads real chunk files itself (3 staging
     batches of 1 MiB chunks), metapage / slice / file CRCs == oracle; a missing
-    file and a wrong-size file get a status and leave the others intact."""
+    file and short, truncated and extended files get a status and leave the
+    others intact."""
+    from curve_amd import _lib
     from curve_amd import crc as C
     chunk, meta_b, sl = 1 << 20, 4096, 256 << 10
     rng = np.random.default_rng(77)
@@ -1469,12 +1471,15 @@ def test_scan_files(dev, oracle, tmp_path):
         paths.append(str(p))
         raws.append(raw)
     (tmp_path / "short").write_bytes(b"y" * 1000)
-    paths.insert(5, str(tmp_path / "missing"))
-    raws.insert(5, None)
-    paths.insert(140, str(tmp_path / "short"))
-    raws.insert(140, None)
+    (tmp_path / "truncated").write_bytes(raws[0][:meta_b + chunk - 4096])
+    (tmp_path / "extended").write_bytes(raws[1] + b"x" * 4096)
+    for at, name in ((5, "missing"), (140, "short"), (141, "truncated"), (200, "extended")):
+        paths.insert(at, str(tmp_path / name))
+        raws.insert(at, None)
     st, mc, sc, fc = C.scan_files(paths, chunk, meta_b, 4096, sl, io_threads=4)
-    assert st[5] == -2 and st[140] == -22  # -ENOENT, CC_EINVAL (size)
+    # -ENOENT; a size != metapage + chunk is CSChunkFile::Open's FileFormatError
+    # (chunkserver_chunkfile.cpp:233-238): CC_EFORMAT, whether short, truncated or extended
+    assert st[5] == -2 and [int(st[i]) for i in (140, 141, 200)] == [_lib.CC_EFORMAT] * 3
     for i, raw in enumerate(raws):
         if raw is None:
             continue

@@ -147,7 +147,9 @@ def test_comm_wait_bounds_an_exchange_stuck_after_init(dev, monkeypatch):
     long first, as such a collective would.  The wait returns CC_ETIMEDOUT at
     its deadline (not the stall's end), the communicator is aborted -- later
     exchanges answer CC_ECOMM, nothing is enqueued -- and the stream still
-    drains.  Without the stall the same wait returns CC_OK."""
+    drains.  Without the stall the same wait returns CC_OK.  The failpoint is
+    read once, when a communicator is created: one made before the variable
+    was set never stalls (the exchange path does not consult the environment)."""
     import time
     from curve_amd import _lib
     from curve_amd.pool import Comm
@@ -157,6 +159,10 @@ def test_comm_wait_bounds_an_exchange_stuck_after_init(dev, monkeypatch):
     comm.wait(timeout_ms=5000)
     assert torch.equal(x, torch.arange(64, dtype=torch.int32, device=dev))
     monkeypatch.setenv("CC_INJECT_EXCHANGE_STALL_MS", "4000")
+    comm.allreduce_digest(x)  # created before the failpoint was armed: no stall
+    comm.wait(timeout_ms=2000)
+    comm.close()
+    comm = Comm(1, 0, Comm.unique_id())  # armed at its init
     try:
         comm.allreduce_digest(x)
         t0 = time.perf_counter()
