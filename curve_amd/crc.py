@@ -511,6 +511,57 @@ def apply_updates(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int 
     return n
 
 
+def log_probe_descs(dst_off, src_off, lens, page_bytes: int = PAGE_SIZE):
+    """Descriptors of cc_apply_log_probe_dev (the write log's page traffic
+    alone) for one write log, built on the host: one per touched page, in the
+    order of the first write touching it (the page pass's head order).  A page
+    with ONE piece reads the rows that piece covers whole from the source (as
+    cc_apply_log_dev does) and the rest from the page; every page stores back
+    the rows its pieces touch.  Diagnostic: not part of the write path."""
+    import numpy as np
+    if page_bytes != 4096:
+        raise CurveCrcError(_lib.CC_EINVAL, "the probe is built for 4 KiB pages")
+    dst = np.asarray(dst_off, dtype=np.uint64)
+    src = np.asarray(src_off, dtype=np.uint64)
+    ln = np.asarray(lens, dtype=np.uint64)
+    pb = np.uint64(page_bytes)
+    p0, p1 = dst // pb, (dst + ln - np.uint64(1)) // pb
+    span = int((p1 - p0).max()) + 1 if dst.size else 0
+    pg, upd = [], []
+    for k in range(span):  # piece k of every write that reaches its k-th page
+        m = p0 + np.uint64(k) <= p1
+        pg.append(p0[m] + np.uint64(k))
+        upd.append(np.nonzero(m)[0])
+    pg, upd = np.concatenate(pg), np.concatenate(upd)
+    pbase = pg * pb
+    rlo = (np.maximum(dst[upd], pbase) - pbase).astype(np.int64)
+    rhi = (np.minimum(dst[upd] + ln[upd], pbase + pb) - pbase).astype(np.int64)
+    r0, r1 = rlo >> 8, (rhi - 1) >> 8
+    dirty = ((np.int64(2) << r1) - 1) & ~((np.int64(1) << r0) - 1)
+    f0, f1 = (rlo + 255) >> 8, rhi >> 8
+    cov = np.where(f1 > f0, ((np.int64(1) << f1) - 1) & ~((np.int64(1) << f0) - 1), 0)
+    soff = src[upd] - dst[upd] + pbase  # modular, as cc_apply_log_dev's per-piece source pointer
+    order = np.lexsort((upd, pg))  # pieces grouped by page, log order inside
+    pg, upd, dirty, cov, soff = pg[order], upd[order], dirty[order], cov[order], soff[order]
+    starts = np.flatnonzero(np.r_[True, pg[1:] != pg[:-1]])
+    counts = np.diff(np.r_[starts, pg.size])
+    out = np.zeros(starts.size, dtype=[("page", "<u8"), ("src_off", "<u8"), ("covered", "<u4"), ("dirty", "<u4")])
+    out["page"] = pg[starts]
+    out["dirty"] = np.bitwise_or.reduceat(dirty, starts).astype(np.uint32)
+    single = counts == 1
+    out["covered"] = np.where(single, cov[starts], 0).astype(np.uint32)
+    out["src_off"] = np.where(single, soff[starts], 0)
+    return out[np.argsort(upd[starts], kind="stable")]  # head order: by the first write touching the page
+
+
+def log_probe(pool, src, d_desc, n: int, out, stream=None):
+    """cc_apply_log_probe_dev over `n` descriptors resident on the device."""
+    with _torch().cuda.device(pool.device):
+        check(lib().cc_apply_log_probe_dev(_dev_ptr(pool, "pool"), _nbytes(pool), _dev_ptr(src, "src"),
+                                           _dev_ptr(d_desc, "desc"), n, _dev_ptr(out, "out"),
+                                           _stream_handle(stream)), "cc_apply_log_probe_dev")
+
+
 _reads_work = {}
 
 

@@ -376,12 +376,18 @@ int get_ctx(CtxRef* out) {
     build_lds_image(img.data());
     // device image: the LDS image, then for t < kXinvEntries the 32 products
     // x^(-8t) * x^i, i = 0..31 (range kernel: a lane-parallel multiply by x^(-8t))
-    img.resize(kLdsBytes / 4 + kXinvEntries * 32);
+    img.resize(kLdsBytes / 4 + kXinvEntries * 32 + kRowShiftEntries * 32);
     uint32_t r = xinv_bytes(0);
     for (uint32_t t = 0; t < kXinvEntries; t++, r = div_x8(r)) {  // r = x^(-8t)
         uint32_t b = r;
         for (uint32_t i = 0; i < 32; i++, b = (b >> 1) ^ (kPoly & (0u - (b & 1u))))  // b *= x
             img[kLdsBytes / 4 + t * 32 + i] = b;
+    }
+    // x^(2048 t) * x^i (row shifts of the write log's delta mode)
+    for (uint32_t t = 0; t < kRowShiftEntries; t++) {
+        uint32_t b = xpow(2048ull * t);
+        for (uint32_t i = 0; i < 32; i++, b = (b >> 1) ^ (kPoly & (0u - (b & 1u))))
+            img[kRowShiftByteOff / 4 + t * 32 + i] = b;
     }
     if ((e = hipMalloc(&c->image, img.size() * 4)) != hipSuccess) return map_err(e);
     if ((e = hipMemcpy(c->image, img.data(), img.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return map_err(e);
@@ -719,6 +725,27 @@ int cc_engine_trim(void) {
     if (e != hipSuccess) return map_err(e);  // (not freed: a faulted device keeps them)
     for (void* p : dead) (void)hipFree(p);
     return CC_OK;
+}
+
+uint64_t cc_engine_stream_entries(void) {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 0;
+    CtxRef c = std::atomic_load(&g_ctx[dev]);
+    if (!c) return 0;
+    uint64_t n = 0;
+    {
+        std::lock_guard<std::mutex> lk(c->tail_mu);
+        n += c->tails.size();
+    }
+    {
+        std::lock_guard<std::mutex> lk(c->log_mu);
+        n += c->log_tabs.size();
+    }
+    {
+        std::lock_guard<std::mutex> lk(c->range_mu);
+        n += c->range_works.size();
+    }
+    return n;
 }
 
 int cc_page_crc_dev(const void* d_pages, uint64_t n_pages, uint32_t page_bytes, uint32_t* d_out, void* stream) {
@@ -1414,6 +1441,28 @@ int cc_apply_log_delta_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_byte
                            void* d_work, uint64_t work_bytes, void* stream) {
     return apply_log(d_pool, pool_bytes, page_bytes, d_src, d_log, n_updates, max_len, d_page_crcs, d_work,
                      work_bytes, stream, 1);
+}
+
+int cc_apply_log_probe_dev(void* d_pool, uint64_t pool_bytes, const void* d_src, const cc_log_probe_desc* d_desc,
+                           uint64_t n, uint32_t* d_out, void* stream) {
+    static_assert(sizeof(cc_log_probe_desc) == sizeof(LogProbeDesc), "probe descriptor layout");
+    if (n == 0) return CC_OK;
+    if (!d_pool || !d_src || !d_desc || !d_out || pool_bytes % 4096 || ((uintptr_t)d_pool & 3u) ||
+        ((uintptr_t)d_desc & 7u))
+        return CC_EINVAL;
+    CtxRef c;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    LogProbeLaunch a = {};
+    a.pool = static_cast<unsigned char*>(d_pool);
+    a.src = static_cast<const unsigned char*>(d_src);
+    a.desc = reinterpret_cast<const LogProbeDesc*>(d_desc);
+    a.n = n;
+    a.out = d_out;
+    // the write log's page pass grid: a workgroup per CU, fewer for a short list
+    const uint64_t blocks = (n + kLogWavesFull - 1) / kLogWavesFull;
+    a.blocks = (int)(blocks < (uint64_t)c->cus ? blocks : (uint64_t)c->cus);
+    return map_err(launch_log_probe(a, static_cast<hipStream_t>(stream)));
 }
 
 // The engine holds the schedule scratch (the stream's range scratch); d_work is

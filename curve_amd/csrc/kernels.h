@@ -147,6 +147,22 @@ hipError_t launch_log_insert(const LogLaunch& a, hipStream_t s);
 hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s);
 // <= 64 writes of <= 2 pieces each in one launch (no table, no insert)
 hipError_t launch_log_small(const LogLaunch& a, hipStream_t s);
+// diagnostic: the write log's page traffic alone (4 KiB pages; kernels.hip log_probe_kernel)
+struct LogProbeDesc {
+    uint64_t page;      // touched page
+    uint64_t src_off;   // source byte of page byte 0 (mod 2^64) when covered != 0
+    uint32_t covered;   // rows read from the source (the page's only piece covers them whole)
+    uint32_t dirty;     // rows stored back
+};
+struct LogProbeLaunch {
+    unsigned char* pool;
+    const unsigned char* src;
+    const LogProbeDesc* desc;
+    uint64_t n;
+    uint32_t* out;  // [n]
+    int blocks;
+};
+hipError_t launch_log_probe(const LogProbeLaunch& a, hipStream_t s);
 
 struct RangeDesc {
     uint64_t off, len;
@@ -202,6 +218,11 @@ struct RangeLaunch {
 hipError_t launch_range_flat(const RangeLaunch& a, hipStream_t s);
 // x^(-8t) mod P for t = 0..kXinvEntries-1 (undoing the zero pad after a range in its last 4 KiB block)
 constexpr uint32_t kXinvEntries = 4100;  // x^(-8t), t < 4096 + 4: the zero pad after a range in its last 4 KiB block
+// then, for t = 0..kRowShiftEntries-1, the 32 products x^(2048 t) * x^i: a
+// lane-parallel multiply by the shift over t zero 256-byte rows (the write
+// log's delta mode hashes only a piece's rows and shifts over the rows after it)
+constexpr uint32_t kRowShiftEntries = 32;
+constexpr uint32_t kRowShiftByteOff = kLdsBytes + kXinvEntries * 32 * 4;  // byte offset in the device image
 
 // Fused scan epilogue: one 256-thread block per chunk.
 struct EpilogueLaunch {

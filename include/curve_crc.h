@@ -98,6 +98,9 @@ int cc_engine_fini(void);
  * (other threads' calls proceed meanwhile) and frees them.  Entries of
  * hipStreamPerThread are also dropped when their thread exits. */
 int cc_engine_trim(void);
+/* Diagnostic: the per-stream entries (tail blocks, write-log tables, range
+ * scratch) the engine holds on the calling thread's device right now. */
+uint64_t cc_engine_stream_entries(void);
 int cc_device_count(void);
 const char* cc_strerror(int code);
 const char* cc_version(void);
@@ -591,6 +594,24 @@ int cc_hbm_read_probe_dev(const void* d_buf, uint64_t bytes, uint32_t* d_sink, v
  * d_out, so its time is the ceiling cc_page_crc_dev is held to on this device.
  * d_out receives meaningless words.  Enqueue only. */
 int cc_page_load_probe_dev(const void* d_pages, uint64_t n_pages, uint32_t* d_out, void* stream);
+
+/* Diagnostic (no reference counterpart): the write log's page traffic alone,
+ * the ceiling cc_apply_log_dev is held to on its access pattern.  One
+ * descriptor per touched 4 KiB page of a log (host-built, e.g.
+ * curve_amd.crc.log_probe_descs): the rows read from the source (covered by the
+ * page's only piece; src_off = the source byte of page byte 0, mod 2^64) -- the
+ * others from the page -- and the rows stored back.  Same grid and occupancy
+ * as the write log's page pass, no table, no CRC.  It stores back the bytes it
+ * loaded: run right after the log it describes was applied, it changes no
+ * byte.  d_out[i] = an XOR of page i's words.  Enqueue only. */
+typedef struct cc_log_probe_desc {
+    uint64_t page;
+    uint64_t src_off;
+    uint32_t covered_rows;
+    uint32_t dirty_rows;
+} cc_log_probe_desc;
+int cc_apply_log_probe_dev(void* d_pool, uint64_t pool_bytes, const void* d_src, const cc_log_probe_desc* d_desc,
+                           uint64_t n, uint32_t* d_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -869,13 +869,15 @@ def test_write_log_small_logs(dev, oracle, n, page_bytes, delta):
 
 
 def test_write_log_pseudo_streams_per_thread_and_trim(dev, oracle):
-    """the engine keys its per-stream state (the write log's hash
-    table, the page kernel's tail counters) by stream; the null stream and
-    hipStreamPerThread are ONE handle standing for a different real stream in
-    each thread, so they are keyed per calling thread.  Four threads apply
-    their own logs at the same time through those two handles (two threads
-    each); every page lands as in-order application with the oracle's CRC.
-    Then cc_engine_trim frees the cached tables and the next call rebuilds."""
+    """The engine keys its per-stream state (the write log's hash table, the
+    page kernel's tail counters) by stream.  The null stream is ONE real stream
+    (the legacy default stream: one key, enqueues ordered by the engine's
+    mutex); hipStreamPerThread is one handle standing for a different real
+    stream in each thread, so it is keyed per calling thread.  Four threads
+    apply their own logs at the same time through those two handles (two
+    threads each); every page lands as in-order application with the oracle's
+    CRC.  Then cc_engine_trim frees the cached tables and the next call
+    rebuilds."""
     import ctypes
     import threading
     from curve_amd import crc as C
@@ -1603,3 +1605,50 @@ def test_scan_epilogue_geometries(dev, oracle, ppc, pps):
     assert [int(x) for x in u32(sl)] == want_sl
     assert [int(x) for x in u32(fc)] == want_fc
     assert [int(x) for x in u32(dig)] == want_dig
+
+
+def test_per_thread_stream_entries_dropped_at_thread_exit(dev, oracle):
+    """hipStreamPerThread scratch is keyed by (handle, thread) and a
+    thread's entries are dropped when the thread exits (after its per-thread
+    stream drained).  300 short-lived threads in turn -- glibc reuses their
+    thread ids -- each run a range batch (cc_crc_ranges_dev: the stream's range
+    scratch) on hipStreamPerThread and check it against the oracle; the engine
+    holds no more entries afterwards than before (round 4 kept every exited
+    thread's scratch, up to 256 entries, then fell back to per-call
+    allocations for good, and a new thread could inherit an exited one's)."""
+    import ctypes
+    import threading
+    from curve_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(77)
+    buf = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    d_buf = to_dev(buf, dev)
+    n = 64
+    off = rng.integers(0, (1 << 20) - 8192, n)
+    ln = rng.integers(0, 8192, n)
+    want = [oracle.crc32c(buf[o:o + k].tobytes()) for o, k in zip(off, ln)]
+    rec = np.stack([off, ln], axis=1).astype(np.uint64)
+    d_rec = to_dev(rec.view(np.uint8).reshape(-1), dev)
+    torch.cuda.synchronize()
+    base = int(L.cc_engine_stream_entries())
+    errs = []
+
+    def run():
+        torch.cuda.set_device(dev)
+        out = torch.zeros(n, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        rc = L.cc_crc_ranges_dev(d_buf.data_ptr(), d_rec.data_ptr(), n, out.data_ptr(), ctypes.c_void_p(2))
+        if rc:
+            errs.append(rc)
+            return
+        L.cc_engine_stream_entries()  # (no sync here: the exit path waits for the stream)
+        torch.cuda.synchronize()
+        if [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()] != want:
+            errs.append("mismatch")
+
+    for _ in range(300):
+        t = threading.Thread(target=run)
+        t.start()
+        t.join()
+    assert not errs, errs[:5]
+    assert int(L.cc_engine_stream_entries()) <= base

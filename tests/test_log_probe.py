@@ -1,0 +1,93 @@
+"""The write-log traffic probe's descriptors (curve_amd.crc.log_probe_descs,
+host logic of the diagnostic cc_apply_log_probe_dev) against a per-page loop
+written from the write path's piece geometry (CSChunkFile::Write applies the
+writes of a batch in log order, chunkserver_chunkfile.cpp:287-427), and the
+probe on the device: idempotent right after its log is applied."""
+import numpy as np
+import pytest
+
+
+def _naive(dst, src, lens, pb=4096):
+    pages = {}
+    order = []
+    for i, (d, s, n) in enumerate(zip(dst.tolist(), src.tolist(), lens.tolist())):
+        for p in range(d // pb, (d + n - 1) // pb + 1):
+            base = p * pb
+            rlo, rhi = max(d, base) - base, min(d + n, base + pb) - base
+            dirty = 0
+            for r in range(rlo >> 8, ((rhi - 1) >> 8) + 1):
+                dirty |= 1 << r
+            cov = 0
+            for r in range((rlo + 255) >> 8, rhi >> 8):
+                cov |= 1 << r
+            if p not in pages:
+                pages[p] = []
+                order.append(p)
+            pages[p].append((dirty, cov, (s - d + base) % (1 << 64)))
+    out = []
+    for p in order:
+        pcs = pages[p]
+        dirty = 0
+        for x in pcs:
+            dirty |= x[0]
+        single = len(pcs) == 1
+        out.append((p, pcs[0][2] if single else 0, pcs[0][1] if single else 0, dirty))
+    return out
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_descs_match_per_page_loop(seed):
+    from curve_amd import crc as C
+    rng = np.random.default_rng(seed)
+    n = 3000
+    lens = rng.integers(1, 4097, n)
+    dst = rng.integers(0, 64 * 4096 - 4096, n)  # a small pool: many pages with several pieces
+    src = rng.integers(0, n * 4096, n)
+    got = C.log_probe_descs(dst, src, lens)
+    want = _naive(dst, src, lens)
+    assert [(int(g["page"]), int(g["src_off"]), int(g["covered"]), int(g["dirty"])) for g in got] == want
+
+
+def test_descs_edge_cases():
+    from curve_amd import crc as C
+    # a whole aligned page, one byte, a write on row boundaries, and a
+    # straddler from page 2's last row into page 3 (page 2: two pieces)
+    dst = np.array([0, 4096 + 5, 8192 + 256, 3 * 4096 - 10])
+    lens = np.array([4096, 1, 512, 20])
+    src = np.array([100, 7, 9000, 50])
+    got = {int(g["page"]): (int(g["covered"]), int(g["dirty"])) for g in C.log_probe_descs(dst, src, lens)}
+    assert got[0] == (0xFFFF, 0xFFFF)
+    assert got[1] == (0, 1)
+    assert got[2] == (0, 0b110 | 1 << 15)  # two pieces: nothing read from a source, both pieces' rows dirty
+    assert got[3] == (0, 1)  # the straddler's second piece: 10 bytes into page 3
+    one = C.log_probe_descs(dst[2:3], src[2:3], lens[2:3])
+    assert (int(one["covered"][0]), int(one["dirty"][0])) == (0b110, 0b110)
+    assert C.log_probe_descs(dst[:1], src[:1], lens[:1])["src_off"][0] == 100
+
+
+@pytest.mark.gpu
+def test_probe_is_idempotent_after_its_log():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from curve_amd import crc as C
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5)
+    pool = torch.from_numpy(rng.integers(0, 256, 4096 * 4096, dtype=np.uint8)).to(dev)
+    crcs = C.page_crc(pool, 4096)
+    U = 5000
+    src = torch.from_numpy(rng.integers(0, 256, U * 4096, dtype=np.uint8)).to(dev)
+    dst, so, ln = rng.integers(0, pool.numel() - 4096, U), rng.integers(0, U * 4096 - 4096, U), rng.integers(512, 4097, U)
+    C.apply_updates(pool, crcs, src, dst, so, ln)
+    before = pool.clone()
+    d = C.log_probe_descs(dst, so, ln)
+    out = torch.zeros(d.size, dtype=torch.int32, device=dev)
+    C.log_probe(pool, src, torch.from_numpy(d.view(np.uint8)).to(dev), d.size, out)
+    torch.cuda.synchronize()
+    assert torch.equal(pool, before)  # stores wrote back what the apply left
+    words = pool.view(torch.int32).view(-1, 1024)[torch.from_numpy(d["page"].astype(np.int64)).to(dev)]
+    want = words[:, 0].clone()
+    for j in range(1, 1024):
+        want ^= words[:, j]
+    assert torch.equal(out, want)
+    assert int(C.page_verify(pool, crcs, 4096)[0]) == 0
