@@ -445,7 +445,7 @@ def partial_write_leg(pool, args):
     probe_ms = float(np.mean(probe_each))
     # bytes the probe moves: 4 KiB read a page (rows from the page or the
     # source) + its dirty rows written
-    probe_moved = float(np.mean([d.size * 4096 + 256 * int(np.unpackbits(d["dirty"].view(np.uint8)).sum())
+    probe_moved = float(np.mean([d.size * 4096 + 256 * int(np.unpackbits(np.ascontiguousarray(d["dirty"]).view(np.uint8)).sum())
                                  for d in descs]))
     cnt = C.page_verify(flat, pool.page_crcs, 4096)
     torch.cuda.synchronize()

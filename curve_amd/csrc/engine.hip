@@ -22,6 +22,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -68,7 +69,15 @@ struct SlotSignal {
     std::mutex m;
     std::condition_variable cv;
     bool fired = true;
+#ifdef CC_SCAN_TRACE
+    double fired_us = 0;  // diagnostic build only: when the host function ran
+#endif
 };
+#ifdef CC_SCAN_TRACE
+inline double trace_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+#endif
 
 struct Staging {
     bool ready = false;
@@ -80,6 +89,13 @@ struct Staging {
     hipStream_t stream[2] = {nullptr, nullptr};
     hipEvent_t done[2] = {nullptr, nullptr};
     SlotSignal sig[2];
+    // cc_scan_files' host->device copies, both slots', in FIFO order on ONE
+    // stream: copies of the two slots on their own streams run side by side at
+    // half the link each, so every batch completes late and the reads of the
+    // batch after next (gated on it) start late (a host trace: pairs of batches
+    // completing together, 37.8 GiB/s against 53 GiB/s of H2D)
+    hipStream_t copy = nullptr;
+    hipEvent_t copied[2] = {nullptr, nullptr};
     // per-call device inputs of the streamed digest (after bytes, multipliers,
     // copyset index per chunk, digest accumulator): grown on demand
     void* aux = nullptr;
@@ -315,11 +331,18 @@ void staging_free(Staging& st) {
         if (st.hcrc[i]) (void)hipHostFree(st.hcrc[i]);
         if (st.stream[i]) (void)hipStreamDestroy(st.stream[i]);
         if (st.done[i]) (void)hipEventDestroy(st.done[i]);
+        if (st.copied[i]) (void)hipEventDestroy(st.copied[i]);
+        st.copied[i] = nullptr;
         st.host[i] = st.dev[i] = nullptr;
         st.dcrc[i] = st.hcrc[i] = nullptr;
         st.stream[i] = nullptr;
         st.done[i] = nullptr;
         st.sig[i].fired = true;
+    }
+    if (st.copy) {
+        (void)hipStreamSynchronize(st.copy);
+        (void)hipStreamDestroy(st.copy);
+        st.copy = nullptr;
     }
     if (st.aux) (void)hipFree(st.aux);
     if (st.aux_ready) (void)hipEventDestroy(st.aux_ready);
@@ -515,7 +538,9 @@ int staging_init(DevCtx* c) {
         if ((e = hipHostMalloc(&st.hcrc[i], per / 256 * 4, hipHostMallocDefault)) != hipSuccess) return map_err(e);
         if ((e = hipStreamCreateWithFlags(&st.stream[i], hipStreamNonBlocking)) != hipSuccess) return map_err(e);
         if ((e = hipEventCreateWithFlags(&st.done[i], hipEventDisableTiming)) != hipSuccess) return map_err(e);
+        if ((e = hipEventCreateWithFlags(&st.copied[i], hipEventDisableTiming)) != hipSuccess) return map_err(e);
     }
+    if (hipError_t e = hipStreamCreateWithFlags(&st.copy, hipStreamNonBlocking); e != hipSuccess) return map_err(e);
     hipError_t e = hipEventCreateWithFlags(&st.aux_ready, hipEventDisableTiming);
     if (e != hipSuccess) return map_err(e);
     st.ready = true;
@@ -534,6 +559,9 @@ void fire_slot(void* p) {
     {
         std::lock_guard<std::mutex> lk(sg->m);
         sg->fired = true;
+#ifdef CC_SCAN_TRACE
+        sg->fired_us = trace_us();
+#endif
     }
     sg->cv.notify_all();
 }
@@ -604,6 +632,7 @@ struct SlotRing {
         // enqueued: make sure the streams are idle either way
         for (int s = 0; s < 2; s++)
             if (st.stream[s]) (void)hipStreamSynchronize(st.stream[s]);
+        if (st.copy) (void)hipStreamSynchronize(st.copy);
         return rc;
     }
 };
@@ -1242,8 +1271,10 @@ int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
             memcpy(st.host[slot], hsrc, n * page_bytes);
             hsrc = st.host[slot];
         }
-        if ((e = hipMemcpyAsync(st.dev[slot], hsrc, n * page_bytes, hipMemcpyHostToDevice, st.stream[slot])) !=
-            hipSuccess)
+        // H2D on the FIFO copy stream (Staging::copy), the slot's stream waits for it
+        if ((e = hipMemcpyAsync(st.dev[slot], hsrc, n * page_bytes, hipMemcpyHostToDevice, st.copy)) != hipSuccess ||
+            (e = hipEventRecord(st.copied[slot], st.copy)) != hipSuccess ||
+            (e = hipStreamWaitEvent(st.stream[slot], st.copied[slot], 0)) != hipSuccess)
             return ring.fail(map_err(e));
         PageLaunch a = {};
         a.pages = static_cast<const uint32_t*>(st.dev[slot]);
@@ -1646,6 +1677,9 @@ int cc_scan_host_digest(const cc_chunk_src* chunks, uint64_t n_chunks, uint32_t 
             }
         }
         if ((e = flush_meta_run()) != hipSuccess) return ring.fail(map_err(e));
+        // (the copies stay on the slot's stream here: no read gates a batch, and
+        // the FIFO copy stream measured 48.7 vs 51.6 GiB/s on the stream leg's
+        // per-chunk pinned copies, round 5)
         uint32_t* res = st.dcrc[slot];
         uint32_t* d_pages = res + nb * (3 + (uint64_t)slices);
         uint32_t* d_meta = res;
@@ -1834,9 +1868,19 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
     };
     int slot = 0;
     hipError_t e;
+#ifdef CC_SCAN_TRACE
+    std::vector<double> tr;
+#endif
     for (uint64_t first = 0; first < n_files; first += batch) {
         const uint64_t nb = (n_files - first < batch) ? n_files - first : batch;
+#ifdef CC_SCAN_TRACE
+        tr.push_back(trace_us());
+#endif
         if ((rc = ring.drain(slot, take(slot)))) return rc;  // slot's previous batch done: its staging is free
+#ifdef CC_SCAN_TRACE
+        tr.push_back(trace_us());
+        tr.push_back(st.sig[slot].fired_us);
+#endif
         unsigned char* hstage = static_cast<unsigned char*>(st.host[slot]);
         // open + size check serially (cheap), then the reads as ~2 MiB pieces
         // pulled by the io threads (a batch holds only a few 16 MiB files)
@@ -1855,26 +1899,62 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
         }
         const uint64_t pieces = (chunk_bytes + kReadPiece - 1) / kReadPiece;
         const uint64_t items = nb * (1 + pieces);
+        hipStream_t s = st.stream[slot];
+        hipStream_t cs = st.copy;  // every H2D of the call, FIFO
+        unsigned char* ddata = static_cast<unsigned char*>(st.dev[slot]);
+        unsigned char* dmeta = ddata + nb * (uint64_t)chunk_bytes;
+        // a file's data goes to the device as soon as its last piece is read
+        // (the reader that finishes it enqueues the copy on the FIFO copy
+        // stream; the slot's kernels wait for the batch's copies by event), so
+        // the DMA starts a file into the batch.  8 native readers alone move
+        // 74 GiB/s beside a saturated H2D (scripts/file_read_probe.cpp,
+        // profiles/file_read_probe_r05.jsonl): the reads are not the limit, the
+        // copy schedule was (scripts/trace_files.py host timelines,
+        // profiles/scan_files_trace_r05.txt: whole-batch copies on the two slot
+        // streams 37.8 GiB/s; FIFO copy stream 48.0; per-file copies from the
+        // readers on it 49.4)
+        std::vector<std::atomic<uint32_t>> left(nb);
+        for (uint64_t i = 0; i < nb; i++) left[i].store((uint32_t)(1 + pieces));
+        std::atomic<int> herr{(int)hipSuccess};
         std::atomic<uint64_t> next{0};
         auto reader = [&]() {
             for (uint64_t it; (it = next.fetch_add(1)) < items;) {
                 const uint64_t i = it / (1 + pieces), k = it % (1 + pieces);
-                if (fst[i].load(std::memory_order_relaxed)) continue;
-                int r;
-                if (k == 0) {
-                    r = read_full(fds[i], hstage + nb * (uint64_t)chunk_bytes + i * (uint64_t)meta_bytes, meta_bytes, 0);
-                } else {
-                    const uint64_t off = (k - 1) * kReadPiece;
-                    const uint64_t len = chunk_bytes - off < kReadPiece ? chunk_bytes - off : kReadPiece;
-                    r = read_full(fds[i], hstage + i * (uint64_t)chunk_bytes + off, len, (off_t)(meta_bytes + off));
+                if (!fst[i].load(std::memory_order_relaxed)) {
+                    int r;
+                    if (k == 0) {
+                        r = read_full(fds[i], hstage + nb * (uint64_t)chunk_bytes + i * (uint64_t)meta_bytes,
+                                      meta_bytes, 0);
+                    } else {
+                        const uint64_t off = (k - 1) * kReadPiece;
+                        const uint64_t len = chunk_bytes - off < kReadPiece ? chunk_bytes - off : kReadPiece;
+                        r = read_full(fds[i], hstage + i * (uint64_t)chunk_bytes + off, len,
+                                      (off_t)(meta_bytes + off));
+                    }
+                    if (r) {
+                        int zero = 0;
+                        fst[i].compare_exchange_strong(zero, r);
+                    }
                 }
-                if (r) {
-                    int zero = 0;
-                    fst[i].compare_exchange_strong(zero, r);
+                // the file's last item: its data (if it was read whole) leaves now
+                if (left[i].fetch_sub(1) == 1 && fst[i].load() == 0) {
+                    const hipError_t ce = hipMemcpyAsync(ddata + i * (uint64_t)chunk_bytes,
+                                                         hstage + i * (uint64_t)chunk_bytes, chunk_bytes,
+                                                         hipMemcpyHostToDevice, cs);
+                    int ok = (int)hipSuccess;
+                    if (ce != hipSuccess) herr.compare_exchange_strong(ok, (int)ce);
                 }
             }
         };
-        c->readers.run((uint32_t)(items < threads ? items : threads), [&](uint32_t) { reader(); });
+        const int dev = c->device;
+        c->readers.run((uint32_t)(items < threads ? items : threads), [&](uint32_t k) {
+            if (k) (void)hipSetDevice(dev);  // pool threads enqueue copies on this device's stream
+            reader();
+        });
+        if ((e = (hipError_t)herr.load()) != hipSuccess) return ring.fail(map_err(e));
+#ifdef CC_SCAN_TRACE
+        tr.push_back(trace_us());
+#endif
         for (uint64_t i = 0; i < nb; i++) {
             if (fds[i] >= 0) close(fds[i]);
             cc_file_result& fr = h_results[first + i];
@@ -1882,12 +1962,15 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
             if (fr.status) {  // keep the batch well-defined; its CRCs are discarded
                 memset(hstage + i * (uint64_t)chunk_bytes, 0, chunk_bytes);
                 memset(hstage + nb * (uint64_t)chunk_bytes + i * (uint64_t)meta_bytes, 0, meta_bytes);
+                if ((e = hipMemcpyAsync(ddata + i * (uint64_t)chunk_bytes, hstage + i * (uint64_t)chunk_bytes,
+                                        chunk_bytes, hipMemcpyHostToDevice, cs)) != hipSuccess)
+                    return ring.fail(map_err(e));
             }
         }
-        hipStream_t s = st.stream[slot];
-        unsigned char* ddata = static_cast<unsigned char*>(st.dev[slot]);
-        unsigned char* dmeta = ddata + nb * (uint64_t)chunk_bytes;
-        if ((e = hipMemcpyAsync(ddata, hstage, nb * per_file, hipMemcpyHostToDevice, s)) != hipSuccess)
+        // the batch's metapages: one copy
+        if ((e = hipMemcpyAsync(dmeta, hstage + nb * (uint64_t)chunk_bytes, nb * (uint64_t)meta_bytes,
+                                hipMemcpyHostToDevice, cs)) != hipSuccess ||
+            (e = hipEventRecord(st.copied[slot], cs)) != hipSuccess || (e = hipStreamWaitEvent(s, st.copied[slot], 0)) != hipSuccess)
             return ring.fail(map_err(e));
         uint32_t* res = st.dcrc[slot];
         uint32_t* d_pages = res + nb * (3 + (uint64_t)slices);
@@ -1938,7 +2021,20 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
         ring.first[slot] = first;
         ring.n[slot] = nb;
         slot ^= 1;
+#ifdef CC_SCAN_TRACE
+        tr.push_back(trace_us());
+#endif
     }
+#ifdef CC_SCAN_TRACE
+    // per batch: loop start, drain done, the drained batch's host function, reads done, enqueued
+    if (FILE* f = fopen("/tmp/cc_scan_trace.txt", "a")) {
+        for (size_t q = 0; q + 5 <= tr.size(); q += 5)
+            fprintf(f, "%.1f %.1f %.1f %.1f %.1f\n", tr[q] - tr[0], tr[q + 1] - tr[0], tr[q + 2] ? tr[q + 2] - tr[0] : -1.0,
+                    tr[q + 3] - tr[0], tr[q + 4] - tr[0]);
+        fprintf(f, "end\n");
+        fclose(f);
+    }
+#endif
     if ((rc = ring.drain(slot, take(slot)))) return rc;
     return ring.drain(slot ^ 1, take(slot ^ 1));
 }
