@@ -399,18 +399,12 @@ int get_ctx(CtxRef* out) {
     build_lds_image(img.data());
     // device image: the LDS image, then for t < kXinvEntries the 32 products
     // x^(-8t) * x^i, i = 0..31 (range kernel: a lane-parallel multiply by x^(-8t))
-    img.resize(kLdsBytes / 4 + kXinvEntries * 32 + kRowShiftEntries * 32);
+    img.resize(kLdsBytes / 4 + kXinvEntries * 32);
     uint32_t r = xinv_bytes(0);
     for (uint32_t t = 0; t < kXinvEntries; t++, r = div_x8(r)) {  // r = x^(-8t)
         uint32_t b = r;
         for (uint32_t i = 0; i < 32; i++, b = (b >> 1) ^ (kPoly & (0u - (b & 1u))))  // b *= x
             img[kLdsBytes / 4 + t * 32 + i] = b;
-    }
-    // x^(2048 t) * x^i (row shifts of the write log's delta mode)
-    for (uint32_t t = 0; t < kRowShiftEntries; t++) {
-        uint32_t b = xpow(2048ull * t);
-        for (uint32_t i = 0; i < 32; i++, b = (b >> 1) ^ (kPoly & (0u - (b & 1u))))
-            img[kRowShiftByteOff / 4 + t * 32 + i] = b;
     }
     if ((e = hipMalloc(&c->image, img.size() * 4)) != hipSuccess) return map_err(e);
     if ((e = hipMemcpy(c->image, img.data(), img.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) return map_err(e);

@@ -218,11 +218,6 @@ struct RangeLaunch {
 hipError_t launch_range_flat(const RangeLaunch& a, hipStream_t s);
 // x^(-8t) mod P for t = 0..kXinvEntries-1 (undoing the zero pad after a range in its last 4 KiB block)
 constexpr uint32_t kXinvEntries = 4100;  // x^(-8t), t < 4096 + 4: the zero pad after a range in its last 4 KiB block
-// then, for t = 0..kRowShiftEntries-1, the 32 products x^(2048 t) * x^i: a
-// lane-parallel multiply by the shift over t zero 256-byte rows (the write
-// log's delta mode hashes only a piece's rows and shifts over the rows after it)
-constexpr uint32_t kRowShiftEntries = 32;
-constexpr uint32_t kRowShiftByteOff = kLdsBytes + kXinvEntries * 32 * 4;  // byte offset in the device image
 
 // Fused scan epilogue: one 256-thread block per chunk.
 struct EpilogueLaunch {

@@ -1528,22 +1528,7 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         // delta mode: rows of page h to read (the head piece's if it is the
         // page's only piece) and the page's stored CRC (a vector load: a scalar
         // one would share lgkmcnt with the chain's LDS lookups)
-        // delta mode, a page with one piece: old ^ new is zero outside the piece's
-        // rows [row0, row1], so the chain runs over those rows only (leading zero
-        // rows add nothing to a zero-init chain) and the M-1-row1 trailing zero
-        // rows become one multiply by x^(2048 (M-1-row1)) of the wave's reduced
-        // value: lane i < 32 holds x^(2048 t) x^i (loaded here, with the page)
-        const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<unsigned char*>(static_cast<const unsigned char*>(a.image)) + kRowShiftByteOff, 0,
-            kRowShiftEntries * 128u, kBufFlags);
-        // (pages <= 4 KiB: at 8 KiB the extra registers spill at 12 waves, and
-        // the whole-page chain is kept)
-        constexpr bool kRowChain = M <= 16;
-        auto tail_rows = [&](const Piece& p, uint32_t h) {  // trailing zero rows of old ^ new (uniform)
-            return (kRowChain && ((singles >> h) & 1ull)) ? (uint32_t)M - 1u - piece_rows(p).row1 : 0u;
-        };
-        auto load_next = [&](uint32_t (&Y)[M], const Piece& py, uint32_t pgy, uint32_t h, uint32_t& ocy,
-                             uint32_t& tsy) {
+        auto load_next = [&](uint32_t (&Y)[M], const Piece& py, uint32_t pgy, uint32_t h, uint32_t& ocy) {
             if constexpr (Delta) {
                 const PieceRows r = piece_rows(py);
                 const uint32_t top = r.row1 >= 31 ? 0xFFFFFFFFu : (2u << r.row1) - 1u;
@@ -1552,21 +1537,14 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
                 uint32_t vz = 0;
                 asm volatile("" : "+v"(vz));
                 ocy = a.page_crcs[pgy + vz];
-                if constexpr (kRowChain) {
-                    const uint32_t t = tail_rows(py, h);
-                    tsy = __builtin_amdgcn_raw_buffer_load_b32(rsr, (t && lane < 32u) ? 128u * t + 4u * lane : kBufOOB,
-                                                               0, 0);
-                }
             } else {
-                (void)tsy;
                 // rows the page's only piece covers whole come straight from the source
                 load_rows_sel<M>(Y, a.pool + (uint64_t)pgy * pb, py.sp, ((singles >> h) & 1ull) ? covered_rows(py) : 0u,
                                  lane);
             }
         };
         auto step = [&](uint32_t (&X)[M], Src& SX, const Piece& px, uint32_t pg, uint32_t hh, uint32_t ocx,
-                        uint32_t tsx, uint32_t (&Y)[M], Src& SY, Piece& py, uint32_t& pgy, uint32_t& ocy,
-                        uint32_t& tsy) {
+                        uint32_t (&Y)[M], Src& SY, Piece& py, uint32_t& pgy, uint32_t& ocy) {
             const bool more = hh + 1 < cnt;
             // next page + its first piece's source bytes in flight (clamped to the
             // last page: a harmless re-read, so every step issues the same loads
@@ -1574,7 +1552,7 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
             const uint32_t h1 = more ? hh + 1 : hh;
             pgy = __builtin_amdgcn_readlane(key, h1);
             py = head_piece(h1);
-            load_next(Y, py, pgy, h1, ocy, tsy);
+            load_next(Y, py, pgy, h1, ocy);
             fetch(SY, py);
             const uint64_t pbase = (uint64_t)pg * pb;
             uint32_t dirty = 0;
@@ -1671,23 +1649,7 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
             if constexpr (Delta) {
 #pragma unroll
                 for (int j = 0; j < M; j++) O[j] ^= X[j];  // old ^ new: 0 outside the changed bytes
-                // rows [r0, r1] of old ^ new (a page with several pieces: all)
-                const bool one = kRowChain && ((singles >> hh) & 1ull);
-                const uint32_t r0 = one ? piece_rows(px).row0 : 0u, r1 = one ? piece_rows(px).row1 : M - 1u;
-                uint32_t s = 0;
-#pragma unroll
-                for (int j = 0; j < M; j++) {  // uniform branches: skipped rows cost no LDS lookup
-                    if ((uint32_t)j == r0)
-                        s = O[j];
-                    else if ((uint32_t)j > r0 && (uint32_t)j <= r1)
-                        s = apply_g_xor(tab, s, O[j], c0, c1);
-                }
-                uint32_t raw = wave_xor(apply_fin(tab, s, cf));
-                if (M - 1u - r1) {  // x^(2048 t) * raw = XOR over i of bit (31 - i) of raw ? x^(2048 t) x^i : 0
-                    const uint32_t bit = lane < 32u ? (raw >> (31u - lane)) & 1u : 0u;
-                    raw = wave_xor(bit ? tsx : 0u);
-                }
-                crc = raw ^ ocx;
+                crc = wave_xor(apply_fin(tab, chain<M>(tab, O, c0, c1), cf)) ^ ocx;
             } else {
                 crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
             }
@@ -1697,13 +1659,13 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         // the two register sets alternate (no copies): page k in one while page
         // k+1's loads land in the other
         uint32_t pgA = __builtin_amdgcn_readlane(key, 0), pgB = pgA;
-        uint32_t ocA = 0, ocB = 0, tsA = 0, tsB = 0;
+        uint32_t ocA = 0, ocB = 0;
         Piece pA = head_piece(0), pB = pA;
-        load_next(A, pA, pgA, 0, ocA, tsA);
+        load_next(A, pA, pgA, 0, ocA);
         fetch(S0, pA);
         for (uint32_t h = 0;; h += 2) {
-            if (!step(A, S0, pA, pgA, h, ocA, tsA, B, S1, pB, pgB, ocB, tsB)) break;
-            if (!step(B, S1, pB, pgB, h + 1, ocB, tsB, A, S0, pA, pgA, ocA, tsA)) break;
+            if (!step(A, S0, pA, pgA, h, ocA, B, S1, pB, pgB, ocB)) break;
+            if (!step(B, S1, pB, pgB, h + 1, ocB, A, S0, pA, pgA, ocA)) break;
         }
     }
 }
