@@ -611,11 +611,18 @@ __device__ __forceinline__ uint64_t wave_scan_incl(uint64_t v, uint32_t lane) {
 
 // Every tile count of this call into tb (lane l: tiles kTpl*l .. kTpl*l + kTpl-1):
 // poll the epoch-tagged words (sc1 loads: a data-tagged granule needs no
-// fence), and count a tile whose word is still missing after kTileWaitTicks
-// with count(t) -- its workgroup is not running, and no wave waits on another
-// without a bound.
+// fence).  A tile whose word is still missing after kTileWaitTicks belongs to
+// a workgroup that is not running (a kernel on another stream holds the CUs,
+// or a CU mask): the waiting wave CLAIMS it -- one CAS of the word to this
+// call's tag with kTileClaim set -- counts it with count(t) and publishes the
+// count, so each missing tile is counted once, by the first wave to claim it,
+// while the others keep polling (round 4 had every waiting wave count every
+// missing tile itself: unbounded in practice when many workgroups wait).  The
+// owner's own later store writes the same count.  No wave waits on another
+// without a bound: every claimed tile is counted by a running wave.
+constexpr uint64_t kTileClaim = 1ull << (kEpochShift - 1);  // tile word: claimed, count pending
 template <int kTpl, typename Count>
-__device__ __forceinline__ void wait_tiles(uint64_t (&tb)[kTpl], const uint64_t* tiles, uint64_t tag, uint32_t lane,
+__device__ __forceinline__ void wait_tiles(uint64_t (&tb)[kTpl], uint64_t* tiles, uint64_t tag, uint32_t lane,
                                            Count count) {
     constexpr uint64_t kCountMask = (1ull << kEpochShift) - 1;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -624,21 +631,36 @@ __device__ __forceinline__ void wait_tiles(uint64_t (&tb)[kTpl], const uint64_t*
 #pragma unroll
         for (int j = 0; j < kTpl; j++) {
             const uint64_t v = __hip_atomic_load(tiles + kTpl * lane + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const bool ok = (v & ~kCountMask) == tag;
+            const bool ok = (v & ~kCountMask) == tag && !(v & kTileClaim);
             tb[j] = ok ? v & kCountMask : tb[j];
             have |= ok ? 1u << j : 0u;
         }
         if (!__ballot(have != (1u << kTpl) - 1u)) return;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kTileWaitTicks) break;
-        __builtin_amdgcn_s_sleep(2);
-    }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kTileWaitTicks) {
 #pragma unroll
-    for (int j = 0; j < kTpl; j++) {
-        for (uint64_t m = __ballot(!((have >> j) & 1u)); m; m &= m - 1) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(m);
-            const uint64_t cnt = count(kTpl * l + j);
-            tb[j] = lane == l ? cnt : tb[j];
+            for (int j = 0; j < kTpl; j++) {
+                for (uint64_t m = __ballot(!((have >> j) & 1u)); m; m &= m - 1) {
+                    const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                    const uint32_t t = kTpl * l + j;
+                    uint32_t mine = 0;
+                    if (lane == 0) {  // neither published nor claimed this call: claim it
+                        const uint64_t cur = __hip_atomic_load(tiles + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        uint64_t exp = cur;
+                        mine = (cur & ~kCountMask) != tag &&
+                               __hip_atomic_compare_exchange_strong(tiles + t, &exp, tag | kTileClaim,
+                                                                    __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    if (__builtin_amdgcn_readlane(mine, 0)) {
+                        const uint64_t cnt = count(t);
+                        if (lane == 0) __hip_atomic_store(tiles + t, tag | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        tb[j] = lane == l ? cnt : tb[j];
+                        have |= lane == l ? 1u << j : 0u;
+                    }
+                }
+            }
         }
+        __builtin_amdgcn_s_sleep(2);
     }
 }
 
@@ -1764,14 +1786,17 @@ __global__ __launch_bounds__(64 * log_small_waves(M, Delta)) void log_small_kern
 // covers whole, read from the source as the real kernel reads them; rows the
 // page's pieces dirty, stored back nt).  Same grid and occupancy as
 // log_pages_kernel<16, false> (one workgroup of kLogWavesFull waves per CU),
-// each wave an equal contiguous share of the pages, two pages in flight (page
-// k+1's rows load while page k's dirty rows are stored).  The stores write back
+// each wave an equal contiguous share of the pages, kProbeDepth pages in
+// flight (the next pages' rows load while page k's dirty rows are stored; 2,
+// as the page pass holds).  The stores write back
 // what was loaded, so run right after the log it describes was applied, the
 // probe changes no byte; `out` gets an XOR of each page's words (keeps every
 // load live).  Its time is the ceiling of the write log's access pattern.
 // ---------------------------------------------------------------------------
+constexpr int kProbeDepth = 2;
 template <int M>
 __global__ __launch_bounds__(64 * kLogWavesFull) void log_probe_kernel(LogProbeLaunch a) {
+    constexpr int D = kProbeDepth;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t W = (uint64_t)gridDim.x * kLogWavesFull, gw = (uint64_t)blockIdx.x * kLogWavesFull + wave;
@@ -1780,7 +1805,7 @@ __global__ __launch_bounds__(64 * kLogWavesFull) void log_probe_kernel(LogProbeL
         const uint64_t ih = base + lane;
         const LogProbeDesc d = a.desc[ih < last ? ih : base];
         const uint32_t cnt = (uint32_t)(last - base < 64 ? last - base : 64);
-        uint32_t A[M], B[M];
+        uint32_t ring[D][M];
         auto load = [&](uint32_t (&Y)[M], uint32_t k) {
             const uint64_t pg = readlane64(d.page, k);
             const uint64_t so = readlane64(d.src_off, k);
@@ -1801,14 +1826,20 @@ __global__ __launch_bounds__(64 * kLogWavesFull) void log_probe_kernel(LogProbeL
             x = wave_xor(x);
             if (lane == 0) a.out[base + k] = x;
         };
-        load(A, 0);
-        for (uint32_t k = 0;; k += 2) {
-            load(B, k + 1 < cnt ? k + 1 : k);  // clamped: every step issues the same loads
-            finish(A, k);
-            if (k + 1 >= cnt) break;
-            load(A, k + 2 < cnt ? k + 2 : k + 1);
-            finish(B, k + 1);
-            if (k + 2 >= cnt) break;
+#pragma unroll
+        for (int st = 0; st < D - 1; st++) load(ring[st], (uint32_t)st < cnt ? st : cnt - 1);
+        for (uint32_t k = 0;; k += D) {
+            bool done = false;
+#pragma unroll
+            for (int st = 0; st < D; st++) {
+                if (!done) {  // uniform
+                    const uint32_t kn = k + st + D - 1;
+                    load(ring[(st + D - 1) % D], kn < cnt ? kn : cnt - 1);  // clamped: every step issues the same loads
+                    finish(ring[st], k + st);
+                    done = k + st + 1 >= cnt;
+                }
+            }
+            if (done) break;
         }
     }
 }

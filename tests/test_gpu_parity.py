@@ -1652,3 +1652,49 @@ def test_per_thread_stream_entries_dropped_at_thread_exit(dev, oracle):
         t.join()
     assert not errs, errs[:5]
     assert int(L.cc_engine_stream_entries()) <= base
+
+
+def test_ranges_and_verify_on_a_cu_masked_stream(dev, oracle):
+    """on a stream limited to 32 CUs the range and verify kernels'
+    256-workgroup grids run 32 workgroups at a time, so the first waves wait
+    for tile counts of workgroups that are not resident; after the bound they
+    claim those tiles (one CAS each), count and publish them (kernels.hip
+    wait_tiles).  Results must equal the oracle's (ranges: CRC32C of every range,
+    butil Value; verify: exactly the corrupted page flagged)."""
+    import ctypes
+    from curve_amd import crc as C
+    from curve_amd import _lib
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                                 ctypes.POINTER(ctypes.c_uint32)]
+    h = ctypes.c_void_p()
+    mask = (ctypes.c_uint32 * 8)(0xFFFFFFFF, 0, 0, 0, 0, 0, 0, 0)
+    assert hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), 8, mask) == 0
+    st = torch.cuda.ExternalStream(h.value)
+    rng = np.random.default_rng(31)
+    host = rng.integers(0, 256, 64 << 20, dtype=np.uint8)
+    d = to_dev(host, dev)
+    n = 5000
+    off = rng.integers(0, host.size - 20000, n).astype(np.uint64)
+    ln = rng.integers(0, 20000, n).astype(np.uint64)
+    rec = to_dev(np.stack([off, ln], axis=1).reshape(-1).view(np.uint8), dev)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    L = _lib.lib()
+    torch.cuda.synchronize()
+    for _ in range(3):  # the scratch's epochs alternate: several calls
+        assert L.cc_crc_ranges_dev(d.data_ptr(), rec.data_ptr(), n, out.data_ptr(), ctypes.c_void_p(h.value)) == 0
+    st.synchronize()
+    want = [oracle.crc32c(host[o:o + k].tobytes()) for o, k in zip(off.tolist(), ln.tolist())]
+    assert u32(out).tolist() == want
+    crcs = C.page_crc(d, 4096)
+    torch.cuda.synchronize()
+    d[4096 * 777 + 5] ^= 1  # corrupt page 777
+    torch.cuda.synchronize()
+    roff = rng.integers(0, host.size // 4096 - 40, n) * 4096
+    rlen = rng.integers(1, 40, n) * 4096
+    roff[17], rlen[17] = 4096 * 770, 4096 * 10
+    bad, total = C.verify_reads(d, crcs, roff, rlen, 4096, stream=st)
+    st.synchronize()
+    hits = [i for i in range(n) if roff[i] <= 4096 * 777 < roff[i] + rlen[i]]
+    assert int(total.item()) == len(hits)
+    assert sorted(np.nonzero(bad.cpu().numpy())[0].tolist()) == hits
