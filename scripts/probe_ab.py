@@ -15,7 +15,12 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from curve_amd import crc as C  # noqa: E402
 
-args = sys.argv[1:]
+argv = sys.argv[1:]
+order_mode = "head"
+if "--sorted" in argv:  # descriptors in page (address) order instead of head order
+    order_mode = "sorted"
+    argv.remove("--sorted")
+args = argv
 dev = torch.device("cuda", 0)
 pb, U = 4096, 65536
 pool = torch.empty(16 << 30, dtype=torch.uint8, device=dev).random_(0, 256)
@@ -26,6 +31,8 @@ logs = []
 for _ in range(8):
     dst, so, ln = rng.integers(0, pool.numel() - pb, U), rng.integers(0, U * pb - pb, U), rng.integers(512, 4097, U)
     d = C.log_probe_descs(dst, so, ln)
+    if order_mode == "sorted":
+        d = np.sort(d, order="page")
     logs.append((torch.from_numpy(C.log_records(dst, so, ln).view(np.uint8)).to(dev),
                  torch.from_numpy(d.view(np.uint8)).to(dev), d.size))
 out = torch.empty(U * 2, dtype=torch.int32, device=dev)
@@ -62,5 +69,5 @@ for r in range(40):
             ms[p].append(e0.elapsed_time(e1) / 3)
 ok = bool(torch.equal(crcs, C.page_crc(pool, pb)))
 for p, v in ms.items():
-    print(f"probe {os.path.basename(p)}: median {sorted(v)[len(v) // 2]:.4f} ms min {min(v):.4f} pool_consistent {ok}",
+    print(f"probe ({order_mode} order) {os.path.basename(p)}: median {sorted(v)[len(v) // 2]:.4f} ms min {min(v):.4f} pool_consistent {ok}",
           flush=True)
