@@ -113,3 +113,33 @@ def test_write_log_work_sizing_limits():
         need = L.cc_apply_log_work_bytes(n, max_len, 4096)
         assert need >= pieces * 4 + segs * cap * 8 + 256 * 4, (n, max_len, need)
         assert need <= pieces * 4 + segs * cap * 8 + 256 * 4 + 3 * 256, (n, max_len, need)
+
+
+def test_default_io_threads_from_affinity_and_quota():
+    """cc_default_io_threads (host arithmetic, no GPU): half the CPUs this
+    process may use -- its affinity mask, capped by the cgroup v2 cpu.max quota
+    -- within [2, 8]; scan_files(io_threads=0) uses it."""
+    from curve_amd import _lib
+    from curve_amd import crc as C
+    cpus = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max" and int(q) // int(per) >= 1:
+            cpus = min(cpus, int(q) // int(per))
+    except (OSError, ValueError):
+        pass
+    want = min(8, max(2, cpus // 2))
+    assert _lib.lib().cc_default_io_threads() == want == C.default_io_threads()
+
+
+def test_log_probe_and_stream_entries_need_no_gpu():
+    """The diagnostic entry points check their arguments before touching a
+    device; with no context the engine holds no per-stream entries."""
+    from curve_amd import _lib
+    L = _lib.lib()
+    assert L.cc_apply_log_probe_dev(None, 4096, None, None, 0, None, None) == _lib.CC_OK  # empty list
+    assert L.cc_apply_log_probe_dev(None, 4096, None, None, 1, None, None) == _lib.CC_EINVAL
+    buf = ctypes.create_string_buffer(8192)
+    assert L.cc_apply_log_probe_dev(buf, 100, buf, buf, 1, buf, None) == _lib.CC_EINVAL  # pool not whole pages
+    if L.cc_device_count() == 0:
+        assert L.cc_engine_stream_entries() == 0

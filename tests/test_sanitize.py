@@ -26,3 +26,24 @@ def test_parser_fuzz_plain(tmp_path):
     r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "parser_fuzz: ok" in r.stdout
+
+
+def test_reader_pool_under_thread_sanitizer(tmp_path):
+    """cc_scan_files' persistent io threads (curve_amd/csrc/reader_pool.h) under
+    ThreadSanitizer: thousands of batches of 1..24 participants, each index run
+    once, each work item taken once, results visible after run() returns, pools
+    torn down while idle (tests/native/reader_pool_stress.cpp).  Host only."""
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("no g++")
+    exe = str(tmp_path / "reader_pool_stress")
+    src = os.path.join(ROOT, "tests", "native", "reader_pool_stress.cpp")
+    b = subprocess.run([cxx, "-O1", "-g", "-std=c++17", "-fsanitize=thread", "-o", exe, src, "-lpthread"],
+                       capture_output=True, text=True)
+    if b.returncode != 0 and "tsan" in (b.stderr or "").lower():
+        pytest.skip("no ThreadSanitizer runtime")
+    assert b.returncode == 0, b.stderr
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "reader_pool_stress: ok" in r.stdout and "ThreadSanitizer" not in r.stderr
