@@ -22,7 +22,6 @@
 #include <unistd.h>
 
 #include <atomic>
-#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -70,15 +69,7 @@ struct SlotSignal {
     std::mutex m;
     std::condition_variable cv;
     bool fired = true;
-#ifdef CC_SCAN_TRACE
-    double fired_us = 0;  // diagnostic build only: when the host function ran
-#endif
 };
-#ifdef CC_SCAN_TRACE
-inline double trace_us() {
-    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-#endif
 
 struct Staging {
     bool ready = false;
@@ -485,9 +476,6 @@ void fire_slot(void* p) {
     {
         std::lock_guard<std::mutex> lk(sg->m);
         sg->fired = true;
-#ifdef CC_SCAN_TRACE
-        sg->fired_us = trace_us();
-#endif
     }
     sg->cv.notify_all();
 }
@@ -1794,19 +1782,9 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
     };
     int slot = 0;
     hipError_t e;
-#ifdef CC_SCAN_TRACE
-    std::vector<double> tr;
-#endif
     for (uint64_t first = 0; first < n_files; first += batch) {
         const uint64_t nb = (n_files - first < batch) ? n_files - first : batch;
-#ifdef CC_SCAN_TRACE
-        tr.push_back(trace_us());
-#endif
         if ((rc = ring.drain(slot, take(slot)))) return rc;  // slot's previous batch done: its staging is free
-#ifdef CC_SCAN_TRACE
-        tr.push_back(trace_us());
-        tr.push_back(st.sig[slot].fired_us);
-#endif
         unsigned char* hstage = static_cast<unsigned char*>(st.host[slot]);
         // open + size check serially (cheap), then the reads as ~2 MiB pieces
         // pulled by the io threads (a batch holds only a few 16 MiB files)
@@ -1878,9 +1856,6 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
             reader();
         });
         if ((e = (hipError_t)herr.load()) != hipSuccess) return ring.fail(map_err(e));
-#ifdef CC_SCAN_TRACE
-        tr.push_back(trace_us());
-#endif
         for (uint64_t i = 0; i < nb; i++) {
             if (fds[i] >= 0) close(fds[i]);
             cc_file_result& fr = h_results[first + i];
@@ -1947,20 +1922,7 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
         ring.first[slot] = first;
         ring.n[slot] = nb;
         slot ^= 1;
-#ifdef CC_SCAN_TRACE
-        tr.push_back(trace_us());
-#endif
     }
-#ifdef CC_SCAN_TRACE
-    // per batch: loop start, drain done, the drained batch's host function, reads done, enqueued
-    if (FILE* f = fopen("/tmp/cc_scan_trace.txt", "a")) {
-        for (size_t q = 0; q + 5 <= tr.size(); q += 5)
-            fprintf(f, "%.1f %.1f %.1f %.1f %.1f\n", tr[q] - tr[0], tr[q + 1] - tr[0], tr[q + 2] ? tr[q + 2] - tr[0] : -1.0,
-                    tr[q + 3] - tr[0], tr[q + 4] - tr[0]);
-        fprintf(f, "end\n");
-        fclose(f);
-    }
-#endif
     if ((rc = ring.drain(slot, take(slot)))) return rc;
     return ring.drain(slot ^ 1, take(slot ^ 1));
 }

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""cc_scan_files timeline (diagnostic): the CC_SCAN_TRACE build of the library
+"""cc_scan_files timeline (diagnostic): the trace build of the library
+(scripts/make_variant.sh trace py scripts/patches/scan_files_trace.py)
 writes per-batch host timestamps (loop start, drain done, the drained batch's
 host function, reads done, enqueued) to /tmp/cc_scan_trace.txt; this runs
 scan_files over 128 page-cache-resident chunk files with it (argv: labels of
