@@ -1698,3 +1698,48 @@ def test_ranges_and_verify_on_a_cu_masked_stream(dev, oracle):
     hits = [i for i in range(n) if roff[i] <= 4096 * 777 < roff[i] + rlen[i]]
     assert int(total.item()) == len(hits)
     assert sorted(np.nonzero(bad.cpu().numpy())[0].tolist()) == hits
+
+
+def test_scan_files_reader_pool_threads_and_counts(dev, oracle, tmp_path):
+    """cc_scan_files' persistent reader pool (curve_amd/csrc/reader_pool.h):
+    three threads at once (the per-device submission lock serialises them),
+    each with a different io_threads -- 1, 64 (more readers than a batch has
+    pieces: the pool grows, the run is capped) and 0 (the default) -- and calls
+    over 1, 2 and 9 files (one batch short of a slot, two batches); every file
+    CRC and slice CRC == the oracle's.  1 MiB chunks keep it small."""
+    import threading
+    from curve_amd import crc as C
+    chunk, meta_b, sl = 1 << 20, 4096, 256 << 10
+    rng = np.random.default_rng(81)
+    raws, paths = [], []
+    for i in range(40):
+        raw = rng.integers(0, 256, meta_b + chunk, dtype=np.uint8).tobytes()
+        p = tmp_path / f"chunk_{i}"
+        p.write_bytes(raw)
+        raws.append(raw)
+        paths.append(str(p))
+    jobs = [(1, paths[:1]), (64, paths[1:3]), (0, paths[3:12]), (64, paths[12:40]), (1, paths[:40]), (0, paths[5:6])]
+    out = [None] * len(jobs)
+    errs = []
+
+    def work(k):
+        try:
+            io, ps = jobs[k]
+            for _ in range(2):
+                out[k] = C.scan_files(ps, chunk, meta_b, 4096, sl, io_threads=io)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(len(jobs))]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errs, errs
+    index = {p: i for i, p in enumerate(paths)}
+    for k, (_, ps) in enumerate(jobs):
+        st, mc, sc, fc = out[k]
+        assert (st == 0).all()
+        for j, p in enumerate(ps):
+            raw = raws[index[p]]
+            want = oracle.scan_slices(raw[:meta_b], raw[meta_b:], sl)
+            assert int(mc[j]) == want[0][2] and [int(x) for x in sc[j]] == [w[2] for w in want[1:]]
+            assert int(fc[j]) == oracle.crc32c(raw)
