@@ -83,6 +83,39 @@ def host_cores():
     return aff, quota
 
 
+def _cpulist(text):
+    cpus = set()
+    for part in text.strip().split(","):
+        if part:
+            lo, _, hi = part.partition("-")
+            cpus.update(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def bind_to_gpu_numa(dev):
+    """N > 1: run this rank's threads on the CPUs of the NUMA node its GPU hangs
+    off (sysfs local_cpulist of the GPU's PCI function, within the CPUs this
+    process may use), before any pinned buffer exists, so the rank's pinned
+    staging and stream-leg chunks are placed, and its host-side CRC checks run,
+    next to its PCIe link -- eight ranks' H2D streams otherwise cross the socket
+    interconnect at random.  Threads made afterwards inherit it.  Never fatal:
+    reports what it did ("bound" false and why otherwise)."""
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        path = f"/sys/bus/pci/devices/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        node = int(open(path + "/numa_node").read())
+        local = _cpulist(open(path + "/local_cpulist").read())
+        allowed = os.sched_getaffinity(0)
+        use = local & allowed
+        if node < 0 or not use or use == allowed:
+            return {"numa_node": node, "bound": False,
+                    "why": "no NUMA node" if node < 0 else "no local CPU allowed" if not use else "already local"}
+        os.sched_setaffinity(0, use)
+        return {"numa_node": node, "bound": True, "cpus": len(use), "of_allowed": len(allowed)}
+    except Exception as e:  # report, never fail the run on it
+        return {"bound": False, "why": repr(e)}
+
+
 def cpu_baseline(pool, args, rank):
     """Reference CPU path restated (oracle, single-stream SSE4.2 crc32q as butil
     builds it, one CRC32(page, 4096) call per page) timed on this host over a
@@ -727,6 +760,7 @@ def main():
     local = local % max(1, ndev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    numa = bind_to_gpu_numa(dev) if world > 1 else None
     if world > 1:
         # collectives outside the native exchange (barriers, timing all-reduces,
         # the torch.distributed digest path) are bounded by the group's timeout
@@ -976,6 +1010,7 @@ def main():
     }
     out["digest_check_cpu"] = cpu_digest
     if world > 1:
+        out["numa_binding_rank0"] = numa
         out["digest_exchange"] = {"path": comm_note, "matches_torch_distributed": digest_check,
                                   "matches_cpu_chain": cpu_digest["ok"]}
         # aggregate roofline over the node: every rank's algorithmic bytes over the

@@ -247,3 +247,4 @@ def test_bench_world8_gloo_rehearsal(tmp_path):
     covered = [c for lo, hi in ranges for c in range(lo, hi)]
     assert covered == list(range(world * chunks))
     assert d["verify"]["bad_pages"] == 0
+    assert "bound" in d["numa_binding_rank0"]  # the rank's NUMA binding is reported (bound or why not)
