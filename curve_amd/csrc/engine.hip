@@ -1855,9 +1855,10 @@ int cc_scan_files(const char* const* paths, uint64_t n_files, uint32_t chunk_byt
             if (k) (void)hipSetDevice(dev);  // pool threads enqueue copies on this device's stream
             reader();
         });
+        for (uint64_t i = 0; i < nb; i++)
+            if (fds[i] >= 0) close(fds[i]);  // before any early return below
         if ((e = (hipError_t)herr.load()) != hipSuccess) return ring.fail(map_err(e));
         for (uint64_t i = 0; i < nb; i++) {
-            if (fds[i] >= 0) close(fds[i]);
             cc_file_result& fr = h_results[first + i];
             fr = cc_file_result{fst[i].load(), 0, 0, 0};
             if (fr.status) {  // keep the batch well-defined; its CRCs are discarded

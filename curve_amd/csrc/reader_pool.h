@@ -7,6 +7,7 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -28,30 +29,40 @@ class ReaderPool {
         go_.notify_all();
         for (auto& t : threads_) t.join();
     }
-    // run fn(k) for k in [0, n): k = 0 on the calling thread
+    // run fn(k) for k in [0, m): k = 0 on the calling thread, m <= n (fewer
+    // when the system refuses a new thread: the callers' fn take their work
+    // from a shared counter, so any m >= 1 does it all).  Returns m.  fn must
+    // not throw (cc_scan_files' readers call C functions only).
     template <class F>
-    void run(uint32_t n, F&& fn) {
+    uint32_t run(uint32_t n, F&& fn) {
         std::lock_guard<std::mutex> one(run_mu_);  // one batch at a time per pool
-        if (n > 1) grow(n - 1);
+        const uint32_t helpers = n > 1 ? grow(n - 1) : 0u;
         std::function<void(uint32_t)> job = fn;
         {
             std::lock_guard<std::mutex> lk(mu_);
             job_ = &job;
-            want_ = n - 1;
+            want_ = helpers;
             taken_ = 0;
-            left_ = n - 1;
+            left_ = helpers;
             gen_++;
         }
-        if (n > 1) go_.notify_all();
+        if (helpers) go_.notify_all();
         fn(0);
         std::unique_lock<std::mutex> lk(mu_);
         done_.wait(lk, [&] { return left_ == 0; });
         job_ = nullptr;
+        return helpers + 1;
     }
 
    private:
-    void grow(uint32_t n) {
-        while (threads_.size() < n) threads_.emplace_back([this] { loop(); });
+    // pool threads available for a batch wanting n helpers (creation stops at
+    // the first refusal, e.g. a thread limit; those made so far are kept)
+    uint32_t grow(uint32_t n) {
+        try {
+            while (threads_.size() < n) threads_.emplace_back([this] { loop(); });
+        } catch (const std::system_error&) {
+        }
+        return threads_.size() < n ? (uint32_t)threads_.size() : n;
     }
     void loop() {
         uint64_t seen = 0;

@@ -37,7 +37,7 @@ int main() {
             for (auto& x : taken) x.store(0);
             std::atomic<uint64_t> next{0};
             std::vector<uint64_t> plain(items, 0);  // written by the workers, read after run(): needs run()'s ordering
-            pool.run(n, [&](uint32_t k) {
+            const uint32_t m = pool.run(n, [&](uint32_t k) {
                 CHECK(k < n);
                 ran[k].fetch_add(1);
                 for (uint64_t it; (it = next.fetch_add(1)) < items;) {
@@ -45,6 +45,7 @@ int main() {
                     plain[it] = it * 3 + 1;
                 }
             });
+            CHECK(m == n);  // no thread refused here
             for (uint32_t k = 0; k < n; k++) CHECK(ran[k].load() == 1);
             for (uint64_t i = 0; i < items; i++) CHECK(taken[i].load() == 1 && plain[i] == i * 3 + 1);
         }
