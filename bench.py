@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--file-chunks", type=int, default=128, help="datastore read-path leg (0 = skip)")
     p.add_argument("--file-passes", type=int, default=5, help="datastore read-path leg: passes per io-thread count")
     p.add_argument("--wal-entries", type=int, default=65536, help="WAL replay leg: entries per batch (0 = skip)")
+    p.add_argument("--no-numa-bind", action="store_true",
+                   help="leave the CPU affinity alone (default: bind to the GPU's NUMA node, see bind_to_gpu_numa)")
     p.add_argument("--comm-timeout-ms", type=int, default=60000, help="N>1: bound on the native RCCL init")
     p.add_argument("--exchange-timeout-ms", type=int, default=120000,
                    help="N>1: bound on waiting for the steps' digest exchanges (a peer lost after init)")
@@ -93,13 +95,18 @@ def _cpulist(text):
 
 
 def bind_to_gpu_numa(dev):
-    """N > 1: run this rank's threads on the CPUs of the NUMA node its GPU hangs
-    off (sysfs local_cpulist of the GPU's PCI function, within the CPUs this
+    """Run this rank's threads on the CPUs of the NUMA node its GPU hangs off
+    (sysfs local_cpulist of the GPU's PCI function, within the CPUs this
     process may use), before any pinned buffer exists, so the rank's pinned
-    staging and stream-leg chunks are placed, and its host-side CRC checks run,
-    next to its PCIe link -- eight ranks' H2D streams otherwise cross the socket
-    interconnect at random.  Threads made afterwards inherit it.  Never fatal:
-    reports what it did ("bound" false and why otherwise)."""
+    staging and stream-leg chunks are placed, its chunk files' page cache is
+    written, its reader threads run and its host-side CRC checks run next to
+    its PCIe link.  N > 1: eight ranks' H2D streams otherwise cross the socket
+    interconnect at random.  N = 1 too: unbound, the files leg (page cache ->
+    pinned staging by the reader threads) measured 47.0 / 32.5 / 41.8 GiB/s in
+    three processes on one box, bound 46.7 / 45.9 / 48.4; the pinned H2D legs
+    are the same either way (profiles/numa_files_ab_r05.jsonl).  Threads made
+    afterwards inherit it.  Never fatal: reports what it did ("bound" false
+    and why otherwise)."""
     try:
         p = torch.cuda.get_device_properties(dev)
         path = f"/sys/bus/pci/devices/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
@@ -760,7 +767,7 @@ def main():
     local = local % max(1, ndev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    numa = bind_to_gpu_numa(dev) if world > 1 else None
+    numa = None if args.no_numa_bind else bind_to_gpu_numa(dev)
     if world > 1:
         # collectives outside the native exchange (barriers, timing all-reduces,
         # the torch.distributed digest path) are bounded by the group's timeout
@@ -1009,8 +1016,8 @@ def main():
         "shard_ranges": shard_ranges,
     }
     out["digest_check_cpu"] = cpu_digest
+    out["numa_binding_rank0"] = numa
     if world > 1:
-        out["numa_binding_rank0"] = numa
         out["digest_exchange"] = {"path": comm_note, "matches_torch_distributed": digest_check,
                                   "matches_cpu_chain": cpu_digest["ok"]}
         # aggregate roofline over the node: every rank's algorithmic bytes over the
