@@ -16,3 +16,17 @@ def test_world_size_mismatch_refused():
     assert p.returncode == 2, p.stderr[-2000:]
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert "WORLD_SIZE=2" in line["error"]
+
+
+def test_numa_binding_helpers_never_fail():
+    """bench.bind_to_gpu_numa parses sysfs cpulists and never fails the run: with
+    no GPU (here) it reports why it did not bind and leaves the affinity alone."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench._cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert bench._cpulist("5") == {5}
+    assert bench._cpulist("\n") == set()
+    before = os.sched_getaffinity(0)
+    r = bench.bind_to_gpu_numa(0)
+    assert r["bound"] is False and r["why"]
+    assert os.sched_getaffinity(0) == before
