@@ -193,27 +193,16 @@ def test_bench_rank_lost_after_init_ends_with_an_error_line(tmp_path):
     assert el < 200, el  # the 15 s group timeout, rendezvous and two torch imports
 
 
-@pytest.mark.timeout(420)
-def test_bench_world8_gloo_rehearsal(tmp_path):
-    """The driver's 8-GPU bench path rehearsed at world 8 on the one-GPU box:
-    `bench.py --gpus 8` (it starts torch.distributed.run itself, as a child),
-    8 gloo ranks sharing cuda:0, 16 chunks a rank.  Everything the N>1 line
-    holds is produced by the same code the driver's node runs -- the shard
-    layout, the digest exchange and its checks (against torch.distributed and
-    against libcurvecrc's CPU chain over the whole pool), the stream leg of
-    every rank, the aggregate roofline over every rank's kernel time -- only
-    the transport differs: RCCL refuses 8 ranks on one device, so the ranks
-    agree on the torch.distributed exchange (pool.agreed_comm).  The native
-    RCCL exchange at N>1 is therefore NOT measured here.
-    Reference exchange: CopysetNode::GetHash, copyset_node.cpp:925-975."""
+def _bench_world8(tmp_path, log_name, extra_env=None):
+    """`bench.py --gpus 8` (it starts torch.distributed.run itself, as a child),
+    8 gloo ranks sharing cuda:0, 16 chunks a rank; returns rank 0's line after
+    checking everything the N>1 line must hold."""
     import json
     import subprocess
     import sys
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     world, chunks = 8, 16
-    env = dict(os.environ, BENCH_DIST_BACKEND="gloo", BENCH_DIST_TIMEOUT_S="240")
+    env = dict(os.environ, BENCH_DIST_BACKEND="gloo", BENCH_DIST_TIMEOUT_S="240", **(extra_env or {}))
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--chunks", str(chunks),
            "--steps", "3", "--warmup", "1", "--clock-warm-ms", "0", "--comm-timeout-ms", "5000", "--no-pmc",
            "--stream-chunks-per-rank", "4", "--file-chunks", "0"]
@@ -222,7 +211,7 @@ def test_bench_world8_gloo_rehearsal(tmp_path):
     out_dir = os.path.join(os.environ["GRAFT_REPO_ROOT"], "gpurun_out") if "GRAFT_REPO_ROOT" in os.environ \
         else str(tmp_path)
     os.makedirs(out_dir, exist_ok=True)
-    log_path = os.path.join(out_dir, "bench_world8_gloo.log")
+    log_path = os.path.join(out_dir, log_name)
     with open(log_path, "w") as logf:
         r = subprocess.run(cmd, cwd=str(tmp_path), env=env, stdout=logf, stderr=subprocess.STDOUT, timeout=360)
     text = open(log_path).read()
@@ -238,7 +227,6 @@ def test_bench_world8_gloo_rehearsal(tmp_path):
     assert abs(roof["aggregate_achieved"] - want_agg) <= 0.2 + 1e-3 * want_agg
     assert d["digest_check_cpu"]["ok"] is True
     assert d["digest_exchange"]["matches_cpu_chain"] is True
-    assert "torch.distributed" in d["digest_exchange"]["path"]
     sa = d["stream_all_ranks"]
     assert sa.get("digest_check_ok") is True and sa["ranks"] == world, sa
     # every chunk of the whole pool in exactly one rank's shard, in rank order
@@ -248,3 +236,43 @@ def test_bench_world8_gloo_rehearsal(tmp_path):
     assert covered == list(range(world * chunks))
     assert d["verify"]["bad_pages"] == 0
     assert "bound" in d["numa_binding_rank0"]  # the rank's NUMA binding is reported (bound or why not)
+    return d
+
+
+@pytest.mark.timeout(420)
+def test_bench_world8_gloo_rehearsal(tmp_path):
+    """The driver's 8-GPU bench path rehearsed at world 8 on the one-GPU box.
+    Everything the N>1 line holds is produced by the same code the driver's
+    node runs -- the shard layout, the digest exchange and its checks (against
+    torch.distributed and against libcurvecrc's CPU chain over the whole pool),
+    the stream leg of every rank, the aggregate roofline over every rank's
+    kernel time -- only the transport differs: RCCL refuses 8 ranks on one
+    device, so the ranks agree on the torch.distributed exchange
+    (pool.agreed_comm).  Reference exchange: CopysetNode::GetHash,
+    copyset_node.cpp:925-975."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    d = _bench_world8(tmp_path, "bench_world8_gloo.log")
+    assert "torch.distributed" in d["digest_exchange"]["path"]
+
+
+@pytest.mark.timeout(420)
+def test_bench_world8_native_exchange_over_stub_rccl(tmp_path):
+    """The same world-8 run with the NATIVE digest exchange taken: a build of
+    libcurvecrc linked against tests/native/rccl_stub.cpp (the seven RCCL calls
+    pool.hip makes, over shared memory, synchronous) instead of librccl, which
+    refuses 8 ranks on one GPU.  So cc_comm_init_timeout at nranks 8 (the id
+    carried over torch.distributed), cc_pool_scan_dev's all-gather of every
+    rank's partials into [rank][n] and the device XOR fold over 8 ranks,
+    cc_comm_wait and the teardown all run as at the driver's N = 8, and the
+    exchanged digests must equal torch.distributed's and the CPU chain's.
+    RCCL's own transport is the one part not exercised."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    stub = os.path.join(root, "build", "stub", "libcurvecrc_stubrccl.so")
+    assert os.path.exists(stub), "make -C curve_amd/csrc stubrccl (done by __graft_entry__.build())"
+    d = _bench_world8(tmp_path, "bench_world8_stubrccl.log", {"CURVE_AMD_LIB": stub})
+    ex = d["digest_exchange"]
+    assert ex["path"].startswith("native RCCL"), ex
+    assert ex["matches_torch_distributed"] is True and ex["matches_cpu_chain"] is True, ex
