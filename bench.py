@@ -446,6 +446,21 @@ def partial_write_leg(pool, args):
         e1.record(stream)
     torch.cuda.synchronize()
     dev_ms = [a.elapsed_time(b) for a, b in ev]
+    # the same batches as ONE queue (cc_apply_logs_dev: each page kernel also
+    # groups the next batch in its tail, so only the queue's first batch pays the
+    # grouping launch): re-applying the logs in order leaves the pool as it is.
+    # Five queue calls enqueued back to back (each behind the previous one's
+    # work), HIP events around each, ms per batch
+    qb = [(src, d_log, U) for d_log, _ in logs[1:]]
+    C.apply_logs(flat, pool.page_crcs, qb, 4096, 4096)  # warm (work buffer, table pair), not waited for
+    ev_q = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+    for e0, e1 in ev_q:
+        e0.record(stream)
+        C.apply_logs(flat, pool.page_crcs, qb, 4096, 4096)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    q_each = [a.elapsed_time(b) / len(qb) for a, b in ev_q]
+    q_ms = float(np.mean(q_each))
     # host-log entry point: the records cross PCIe first
     walls = []
     for _, (dst, src_off, lens) in logs[1:]:
@@ -509,6 +524,13 @@ def partial_write_leg(pool, args):
                       "frac_of_random_probe": round(probe_ms / delta_ms, 4),
                       "all_pages_verify_after": delta_ok,
                       "path": "cc_apply_log_delta_dev: stored CRCs updated by linearity, touched rows read only"},
+            "queue": {"batches_per_call": len(qb), "device_ms_per_batch": round(q_ms, 4),
+                      "ms_each": [round(x, 4) for x in q_each],
+                      "updates_per_s": round(U / (q_ms * 1e-3), 1),
+                      "alg_frac_of_hbm_peak": round(alg / (q_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "frac_of_random_probe": round(probe_ms / q_ms, 4),
+                      "path": "cc_apply_logs_dev: the batches as one queue; each batch's page kernel also groups "
+                              "the next batch in its tail (one grouping launch a queue instead of one a batch)"},
             "random_probe": {"ms_per_batch": round(probe_ms, 4), "ms_median": round(float(np.median(probe_each)), 4),
                              "ms_each": [round(x, 4) for x in probe_each],
                              "pages_per_batch": int(np.mean([d.size for d in descs])),

@@ -73,6 +73,11 @@ CC_PCRC_HEADER_BYTES = 64
 TABLE_STATES = {0: "ok", 1: "created", 2: "corrupt", 3: "stale", 4: "refreshed", 5: "missing", 6: "rebuilt"}
 
 
+class CcLogBatch(ctypes.Structure):
+    """cc_log_batch (include/curve_crc.h): one write log of a cc_apply_logs_dev queue."""
+    _fields_ = [("d_src", ctypes.c_void_p), ("d_log", ctypes.c_void_p), ("n_updates", ctypes.c_uint64)]
+
+
 class CcPoolShard(ctypes.Structure):  # include/curve_crc.h cc_pool_shard
     _fields_ = [("d_data", _vp), ("d_meta", _vp), ("n_chunks", _u64), ("chunk_bytes", _u32),
                 ("meta_bytes", _u32), ("page_bytes", _u32), ("slice_bytes", _u32), ("d_after_mult", _vp),
@@ -123,6 +128,8 @@ SIGNATURES = {
     "cc_apply_log_delta_dev": (_int, [_vp, _u64, _u32, _vp, _vp, _u64, _u32, _vp, _vp, _u64, _vp]),
     "cc_engine_stream_entries": (_u64, []),
     "cc_apply_log_probe_dev": (_int, [_vp, _u64, _vp, _vp, _u64, _vp, _vp]),
+    "cc_apply_logs_work_bytes": (_u64, [_u64, _u32, _u32]),
+    "cc_apply_logs_dev": (_int, [_vp, _u64, _u32, _vp, _u32, _u32, _vp, _int, _vp, _u64, _vp]),
     "cc_verify_reads_work_bytes": (_u64, [_u64]),
     "cc_verify_reads_dev": (_int, [_vp, _u64, _u32, _vp, _u64, _vp, _vp, _vp, _vp, _u64, _vp]),
     "cc_comm_unique_id": (_int, [_vp, _sz]),

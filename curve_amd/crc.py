@@ -486,6 +486,40 @@ def apply_log(pool, page_crcs, src, d_log, n_updates: int, max_len: int, page_by
     return 1
 
 
+def apply_logs(pool, page_crcs, batches, max_len: int, page_bytes: int = PAGE_SIZE, stream=None,
+               delta: bool = False):
+    """cc_apply_logs_dev: a QUEUE of write logs applied in order -- the same
+    pool bytes and page CRCs as one apply_log call per batch, pipelined (each
+    batch's page kernel also groups the next batch's pieces).  `batches`: a
+    list of (src, d_log, n_updates) -- device tensors as for apply_log."""
+    import ctypes
+    torch = _torch()
+    if not batches:
+        return 0
+    n_max = max(int(n) for _, _, n in batches)
+    need = int(lib().cc_apply_logs_work_bytes(max(n_max, 1), max_len, page_bytes))
+    if need == 0:
+        raise CurveCrcError(_lib.CC_EINVAL, "unsupported log geometry")
+    key = ("logs",) + tuple(_stream_key(pool.device, stream))
+    work = _log_work.get(key)
+    if work is None or work.numel() < need:
+        with _on_stream(stream):
+            work = torch.empty(need, dtype=torch.uint8, device=pool.device)
+        _log_work[key] = work
+    arr = (_lib.CcLogBatch * len(batches))()
+    for i, (src, d_log, n) in enumerate(batches):
+        arr[i].d_src = _dev_ptr(src, "src").value if int(n) else None
+        arr[i].d_log = _dev_ptr(d_log, "log").value if int(n) else None
+        arr[i].n_updates = int(n)
+    with torch.cuda.device(pool.device):
+        check(lib().cc_apply_logs_dev(_dev_ptr(pool, "pool"), _nbytes(pool), page_bytes, ctypes.cast(arr, ctypes.c_void_p),
+                                      len(batches), max_len, _dev_ptr(page_crcs, "page_crcs"), 1 if delta else 0,
+                                      _dev_ptr(work, "work"), work.numel(), _stream_handle(stream)), "cc_apply_logs_dev")
+    if stream is not None:
+        work.record_stream(stream)
+    return 1
+
+
 def apply_updates(pool, page_crcs, src, dst_off, src_off, lens, page_bytes: int = PAGE_SIZE, stream=None,
                   delta: bool = False):
     """Client partial-write path: host-side write log -> device (one copy of the

@@ -1388,6 +1388,195 @@ int cc_apply_log_delta_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_byte
                      work_bytes, stream, 1);
 }
 
+// ---- a queue of write logs, pipelined (cc_apply_logs_dev) ----
+namespace {
+// Head segments of a batch grouped in chunks of T pieces by G blocks (block b
+// takes chunks b, b + G, ...): G segments of seg_cap records.
+struct SegLayout {
+    uint32_t n_segs, seg_cap;
+};
+bool seg_layout(uint64_t n_pieces, uint32_t T, uint32_t G, SegLayout* l) {
+    if (G == 0 || G > kInsertBlocks) return false;
+    const uint64_t chunks = (n_pieces + T - 1) / T;
+    const uint64_t cap = (chunks + G - 1) / G * T;
+    if (cap >= (1ull << 32)) return false;
+    l->n_segs = G;
+    l->seg_cap = (uint32_t)cap;
+    return true;
+}
+
+// The caller's work buffer of cc_apply_logs_dev: two regions (batches
+// alternate between them) of next links | head segments | segment counts,
+// sized for the largest batch under either grouping (the insert kernel's
+// chunks of kInsertThreads, or a page kernel's tail over <= kInsertBlocks
+// blocks), then the three chunk counters of the tail groupings.  The two hash
+// tables are the two halves of the stream's engine table (kept zero).
+struct LogsWork {
+    uint64_t max_pieces, table_entries, heads_off, counts_off, region, ctr_off, bytes;
+};
+bool logs_work(uint64_t max_updates, uint32_t max_len, uint32_t page_bytes, LogsWork* w) {
+    LogWork one;
+    if (!log_work(max_updates, max_len, page_bytes, &one)) return false;
+    w->max_pieces = one.n_pieces;
+    w->table_entries = one.table_entries;
+    // head records: the insert kernel's layout <= pieces + 512 (kInsertBlocks + 1);
+    // a page kernel's tail grouping G x rounds x T, rounds = 2 ceil(chunks / G):
+    // <= 2 (pieces + T (G + 1)), T <= 1024, G <= kInsertBlocks
+    const uint64_t recs = 2 * (w->max_pieces + 1024ull * (kInsertBlocks + 1));
+    w->heads_off = align256(w->max_pieces * 4);
+    w->counts_off = w->heads_off + align256(recs * 8);
+    w->region = w->counts_off + align256(kInsertBlocks * 4);
+    w->ctr_off = 2 * w->region;
+    w->bytes = w->ctr_off + 256;
+    return true;
+}
+}  // namespace
+
+uint64_t cc_apply_logs_work_bytes(uint64_t max_updates, uint32_t max_len, uint32_t page_bytes) {
+    LogsWork w;
+    return logs_work(max_updates, max_len, page_bytes, &w) ? w.bytes : 0;
+}
+
+int cc_apply_logs_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const cc_log_batch* batches,
+                      uint32_t n_batches, uint32_t max_len, uint32_t* d_page_crcs, int delta, void* d_work,
+                      uint64_t work_bytes, void* stream) {
+    if (!log_page_ok(page_bytes)) return CC_EINVAL;
+    if (n_batches == 0) return CC_OK;
+    if (!batches || !d_pool || !d_page_crcs || !d_work || max_len == 0) return CC_EINVAL;
+    if (pool_bytes % page_bytes || ((uintptr_t)d_pool & 3u)) return CC_EINVAL;
+    if (pool_bytes / page_bytes >= kNoPiece) return CC_EINVAL;
+    uint64_t max_n = 0;
+    for (uint32_t k = 0; k < n_batches; k++) {
+        const cc_log_batch& b = batches[k];
+        if (b.n_updates && (!b.d_log || !b.d_src || ((uintptr_t)b.d_src & 3u))) return CC_EINVAL;
+        max_n = b.n_updates > max_n ? b.n_updates : max_n;
+    }
+    if (max_n == 0) return CC_OK;
+    LogsWork W;
+    if (!logs_work(max_n, max_len, page_bytes, &W) || work_bytes < W.bytes) return CC_EINVAL;
+    CtxRef c;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint32_t slots = log_slots(max_len, page_bytes);
+    auto small = [&](uint64_t n) { return n <= 64 && slots <= 2; };
+    const uint32_t M = page_bytes / kWaveBytes;
+    const uint32_t T = 64u * (uint32_t)(M > 16 ? kLogWaves : (delta ? kLogWavesDelta : kLogWavesFull));
+    auto base = [&](const cc_log_batch& b) {
+        LogLaunch a = {};
+        a.pool = static_cast<unsigned char*>(d_pool);
+        a.pool_bytes = pool_bytes;
+        a.src = static_cast<const unsigned char*>(b.d_src);
+        a.upd = reinterpret_cast<const UpdateDesc*>(b.d_log);
+        a.n_updates = b.n_updates;
+        a.page_bytes = page_bytes;
+        a.max_len = max_len;
+        a.slots = slots;
+        a.n_pieces = b.n_updates * slots;
+        a.image = c->image;
+        a.kconst = kconst_for(page_bytes);
+        a.page_crcs = d_page_crcs;
+        a.delta = delta;
+        const uint64_t blocks = (a.n_pieces + kLogWaves - 1) / kLogWaves;
+        a.blocks = (int)(blocks < (uint64_t)c->cus ? (blocks ? blocks : 1) : (uint64_t)c->cus);
+        return a;
+    };
+    std::unique_lock<std::mutex> lk(c->log_mu);
+    hipError_t e;
+    DevCtx::LogTable* t = log_table(c.get(), s, 2 * W.table_entries, &e);  // two tables: its halves
+    if (e != hipSuccess) return map_err(e);
+    if (!t) {  // no engine table for this stream (kMaxTailBlocks streams hold one, or a huge log): one call a batch
+        lk.unlock();
+        for (uint32_t k = 0; k < n_batches; k++)
+            if (batches[k].n_updates &&
+                (rc = apply_log(d_pool, pool_bytes, page_bytes, batches[k].d_src, batches[k].d_log, batches[k].n_updates,
+                                max_len, d_page_crcs, d_work, W.region, stream, delta)))
+                return rc;
+        return CC_OK;
+    }
+    unsigned char* w = static_cast<unsigned char*>(d_work);
+    uint64_t* const t0 = reinterpret_cast<uint64_t*>(t->p + kLogTableHeader);
+    uint64_t* tabs[2] = {t0, t0 + W.table_entries};
+    const uint32_t masks[2] = {(uint32_t)(W.table_entries - 1), (uint32_t)(W.table_entries - 1)};
+    // the three chunk counters of the tail groupings: grouping kernel q takes
+    // from counter q % 3 and zeroes counter (q + 2) % 3; every insert kernel of
+    // the call zeroes all three (one precedes every grouping on the stream)
+    unsigned long long* ctrs = reinterpret_cast<unsigned long long*>(w + W.ctr_off);
+    uint64_t gq = 0;  // tail groupings so far
+    auto region = [&](LogLaunch& a, int r, const SegLayout& l) {
+        unsigned char* q = w + (uint64_t)r * W.region;
+        a.table = tabs[r];
+        a.table_mask = masks[r];
+        a.clear_table = 1;  // both tables are left zero for the batch after next
+        a.next = reinterpret_cast<uint32_t*>(q);
+        a.heads = reinterpret_cast<uint32_t*>(q + W.heads_off);
+        a.seg_count = reinterpret_cast<uint32_t*>(q + W.counts_off);
+        a.n_segs = l.n_segs;
+        a.seg_cap = l.seg_cap;
+    };
+    int r = 0;             // region (and table) of the batch being applied
+    bool grouped = false;  // batch k already grouped (by the page kernel before it)
+    SegLayout lay = {};
+    for (uint32_t k = 0; k < n_batches && e == hipSuccess; k++) {
+        const cc_log_batch& b = batches[k];
+        if (b.n_updates == 0) continue;
+        LogLaunch a = base(b);
+        if (small(b.n_updates)) {
+            e = launch_log_small(a, s);
+            grouped = false;
+            continue;
+        }
+        if (!grouped) {  // the first batch (or one after a small batch): the insert kernel
+            const uint64_t chunks = (a.n_pieces + kInsertThreads - 1) / kInsertThreads;
+            if (!seg_layout(a.n_pieces, kInsertThreads, (uint32_t)(chunks < kInsertBlocks ? chunks : kInsertBlocks), &lay))
+                return CC_EINVAL;
+            region(a, r, lay);
+            a.zero_ctrs = ctrs;
+            if ((e = launch_log_insert(a, s)) != hipSuccess) break;
+            a.zero_ctrs = nullptr;
+        } else {
+            region(a, r, lay);
+        }
+        // the next non-empty batch, grouped inside this page kernel when it takes the table path
+        uint32_t j = k + 1;
+        while (j < n_batches && batches[j].n_updates == 0) j++;
+        grouped = false;
+        if (j < n_batches && !small(batches[j].n_updates)) {
+            const LogLaunch nb = base(batches[j]);
+            // a workgroup may take up to twice its even share of the chunks
+            const uint64_t chunks = (nb.n_pieces + T - 1) / T;
+            const uint32_t G = (uint32_t)a.blocks;
+            const uint64_t rounds = 2 * ((chunks + G - 1) / G);
+            SegLayout nl = {G, (uint32_t)(rounds * T)};
+            if (G <= kInsertBlocks && rounds * T < (1ull << 32)) {
+                unsigned char* q = w + (uint64_t)(r ^ 1) * W.region;
+                a.nx.upd = nb.upd;
+                a.nx.n_pieces = nb.n_pieces;
+                a.nx.pool_bytes = pool_bytes;
+                a.nx.page_bytes = page_bytes;
+                a.nx.max_len = max_len;
+                a.nx.slots = slots;
+                a.nx.table = tabs[r ^ 1];
+                a.nx.table_mask = masks[r ^ 1];
+                a.nx.next = reinterpret_cast<uint32_t*>(q);
+                a.nx.heads = reinterpret_cast<uint32_t*>(q + W.heads_off);
+                a.nx.seg_count = reinterpret_cast<uint32_t*>(q + W.counts_off);
+                a.nx.seg_cap = nl.seg_cap;
+                a.nx.rounds = (uint32_t)rounds;
+                a.nx.take = ctrs + gq % 3;
+                a.nx.zero = ctrs + (gq + 2) % 3;
+                gq++;
+                lay = nl;
+                grouped = true;
+            }
+        }
+        e = launch_log_pages(a, s);
+        r ^= 1;
+    }
+    if (e != hipSuccess) t->dirty = true;  // a launch may have run in part: clear the engine table before its next use
+    return map_err(e);
+}
+
 int cc_apply_log_probe_dev(void* d_pool, uint64_t pool_bytes, const void* d_src, const cc_log_probe_desc* d_desc,
                            uint64_t n, uint32_t* d_out, void* stream) {
     static_assert(sizeof(cc_log_probe_desc) == sizeof(LogProbeDesc), "probe descriptor layout");

@@ -116,6 +116,26 @@ constexpr int kLogWavesDelta = 16;  // delta mode, pages <= 4 KiB: 120 VGPRs at 
 constexpr int log_waves(int m, bool delta) { return m > 16 ? kLogWaves : (delta ? kLogWavesDelta : kLogWavesFull); }
 // waves per workgroup of log_small_kernel<M, Delta>
 constexpr int log_small_waves(int m, bool delta) { return (!delta && m <= 16) ? kLogWavesFull : kLogWaves; }
+// The NEXT batch's grouping, done by the page kernel of the current one
+// (cc_apply_logs_dev): its pieces go into its own table and head segments, in
+// the kernel's tail -- a workgroup done with its pages takes chunks of the next
+// batch (one counter) while the slower ones finish -- so the kernel boundary
+// before the next page kernel is the only barrier the next batch needs.  The
+// fields insert_piece reads, for that batch; n_pieces = 0: nothing to insert.
+struct LogInsert {
+    const UpdateDesc* upd;
+    uint64_t n_pieces;
+    uint64_t pool_bytes;
+    uint32_t page_bytes, max_len, slots, table_mask;
+    uint64_t* table;
+    uint32_t* next;
+    uint32_t* heads;            // one segment of seg_cap records per block of the inserting kernel
+    uint32_t* seg_count;        // [gridDim.x of the inserting kernel]
+    uint32_t seg_cap;           // >= rounds x the block's threads
+    uint32_t rounds;            // chunks (of the block's threads) one workgroup may take
+    unsigned long long* take;   // the chunk counter, zero at launch (the grouping kernel before zeroed it)
+    unsigned long long* zero;   // the counter the grouping kernel after next takes from: zeroed here
+};
 struct LogLaunch {
     unsigned char* pool;
     uint64_t pool_bytes;
@@ -142,6 +162,8 @@ struct LogLaunch {
     uint32_t* page_crcs;        // out; in delta mode also in (the CRCs before the batch)
     int blocks;
     int delta;                  // 1: update the stored CRCs through linearity (reads touched rows only)
+    LogInsert nx;               // the next batch's grouping, in this batch's page kernel (launch_log_pages)
+    unsigned long long* zero_ctrs;  // log_insert_kernel zeroes these 3 words (the queue's chunk counters) or null
 };
 hipError_t launch_log_insert(const LogLaunch& a, hipStream_t s);
 hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s);

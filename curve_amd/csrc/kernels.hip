@@ -1088,7 +1088,10 @@ __device__ __forceinline__ uint32_t page_hash(uint32_t page, uint32_t mask) {
 // us, and even one per block was a returning atomic on the critical path).
 // Every thread of the block calls it; `wcount` = LDS scratch of blockDim/64 + 1
 // words; `used` = the segment's records so far (uniform), advanced here.
-__device__ __forceinline__ void insert_piece(const LogLaunch& a, uint64_t t, uint32_t* wcount, uint32_t& used) {
+// (A = LogLaunch for log_insert_kernel, LogInsert for the next batch's grouping
+// inside log_pages_kernel: the same field names.)
+template <class A>
+__device__ __forceinline__ void insert_piece(const A& a, uint64_t t, uint32_t* wcount, uint32_t& used) {
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
     bool fresh = false;
     uint32_t slot = 0;
@@ -1144,6 +1147,7 @@ __device__ __forceinline__ void insert_piece(const LogLaunch& a, uint64_t t, uin
 // head segment and leaves its record count in seg_count[b].
 __global__ __launch_bounds__(kInsertThreads) void log_insert_kernel(LogLaunch a) {
     __shared__ uint32_t wcount[kInsertThreads / 64 + 1];
+    if (a.zero_ctrs && blockIdx.x == 0 && threadIdx.x < 3) a.zero_ctrs[threadIdx.x] = 0ull;  // the queue's counters
     uint32_t used = 0;
     const uint64_t chunks = (a.n_pieces + kInsertThreads - 1) / kInsertThreads;
     for (uint64_t c = blockIdx.x; c < chunks; c += gridDim.x)
@@ -1408,6 +1412,32 @@ __device__ __forceinline__ void load_rows(uint32_t (&w)[M], const unsigned char*
         w[j] = __builtin_amdgcn_raw_buffer_load_b32(rp, row_sel(((rows >> j) & 1u) ? 4u * lane : kBufOOB) + 256u * j, 0, 2);
 }
 
+// cc_apply_logs_dev: the next batch's grouping in this page kernel's tail.  A
+// workgroup whose waves are all done with their pages (its LDS image no longer
+// read: the insert's scratch) takes chunks of 64*WV pieces from one counter
+// until none is left or it holds `rounds` of them (its head segment's bound);
+// the workgroups that finish first take them while the slow ones finish, so
+// the grouping costs no kernel time and no launch.  Every workgroup stores its
+// segment's count.  Block 0 zeroes the counter the grouping after next uses
+// (the one before this used it; it has completed).
+template <int WV>
+__device__ __forceinline__ void group_next(const LogInsert& nx, uint32_t* tab) {
+    if (!nx.n_pieces) return;  // uniform
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(nx.zero, 0ull);
+    __syncthreads();  // every wave of the workgroup is past its pages
+    constexpr uint32_t T = 64u * WV;
+    const uint64_t chunks = (nx.n_pieces + T - 1) / T;
+    uint32_t used = 0;
+    for (uint32_t r = 0; r < nx.rounds; r++) {
+        if (threadIdx.x == 0) tab[T] = (uint32_t)atomicAdd(nx.take, 1ull);  // (< 2^32 chunks: n_pieces < 2^31)
+        __syncthreads();
+        const uint64_t c = tab[T];
+        if (c >= chunks) break;  // uniform
+        insert_piece(nx, c * T + threadIdx.x, tab, used);  // ends with a barrier: tab[T] free again
+    }
+    if (threadIdx.x == 0) nx.seg_count[blockIdx.x] = used;
+}
+
 template <int M, bool Delta>
 __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab) {
     constexpr int WV = log_waves(M, Delta);
@@ -1417,13 +1447,14 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
     constexpr int kSpl = kInsertBlocks / 64;
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t sc[kSpl];  // (32-bit: these stay live over the page loop)
-    uint32_t ssum = 0;
 #pragma unroll
     for (int j = 0; j < kSpl; j++) {
         const uint32_t sg = kSpl * lane + j;
         sc[j] = sg < a.n_segs ? a.seg_count[sg] : 0u;
-        ssum += sc[j];
     }
+    uint32_t ssum = 0;
+#pragma unroll
+    for (int j = 0; j < kSpl; j++) ssum += sc[j];
     uint32_t scum = ssum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -1435,7 +1466,10 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
     const uint32_t Hall = __builtin_amdgcn_readlane(scum, 63);
     const uint32_t hb0 = (uint32_t)((uint64_t)Hall * blockIdx.x / gridDim.x);
     const uint32_t hb1 = (uint32_t)((uint64_t)Hall * (blockIdx.x + 1) / gridDim.x);
-    if (hb0 >= hb1) return;
+    if (hb0 >= hb1) {
+        group_next<WV>(a.nx, tab);
+        return;
+    }
     fill_lds<64 * WV>(tab, static_cast<const uint4*>(a.image));
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t c0 = lane << 2 & 0x7Cu;
@@ -1690,6 +1724,7 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
             if (!step(B, S1, pB, pgB, h + 1, ocB, A, S0, pA, pgA, ocA)) break;
         }
     }
+    group_next<WV>(a.nx, tab);
 }
 
 template <int M, bool Delta>

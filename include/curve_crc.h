@@ -281,6 +281,29 @@ int cc_apply_log_delta_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_byte
                            const cc_update* d_log, uint64_t n_updates, uint32_t max_len, uint32_t* d_page_crcs,
                            void* d_work, uint64_t work_bytes, void* stream);
 
+/* A QUEUE of write logs applied in order, as n_batches cc_apply_log_dev calls
+ * (delta = 0) or cc_apply_log_delta_dev calls (delta = 1) would be on `stream`:
+ * the same pool bytes and page CRCs, bit for bit.  Pipelined: the page kernel
+ * of batch k also groups batch k+1's pieces (its hash table and head records,
+ * in the second of two alternating work regions), so only the first batch (and
+ * one after a <= 64-write batch, which takes the one-launch path) pays the
+ * separate grouping launch and the kernel boundary behind it.  `batches` is a
+ * HOST array (its device pointers: as for cc_apply_log_dev, valid until the
+ * stream has run the call's work); empty batches are skipped.  d_work: >=
+ * cc_apply_logs_work_bytes(largest batch's n_updates, max_len, page_bytes).
+ * A stream without an engine table (more than 256 streams hold one) takes one
+ * call per batch.  Replaces a chunkserver's apply loop over its queued write
+ * requests (ChunkOpRequest::OnApply per write, op_request.cpp:429-481). */
+typedef struct cc_log_batch {
+    const void* d_src;        /* device: the batch's data (its records' src offsets) */
+    const cc_update* d_log;   /* device: the batch's records, log order */
+    uint64_t n_updates;
+} cc_log_batch;
+uint64_t cc_apply_logs_work_bytes(uint64_t max_updates, uint32_t max_len, uint32_t page_bytes);
+int cc_apply_logs_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const cc_log_batch* batches,
+                      uint32_t n_batches, uint32_t max_len, uint32_t* d_page_crcs, int delta, void* d_work,
+                      uint64_t work_bytes, void* stream);
+
 /* Verify-on-read for a batch of datastore reads (the read path of
  * CSChunkFile::Read, chunkserver_chunkfile.cpp:497-536, which today returns the
  * bytes unchecked): every page that read i = d_reads[i] (pool byte range, any

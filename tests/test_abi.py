@@ -143,3 +143,31 @@ def test_log_probe_and_stream_entries_need_no_gpu():
     assert L.cc_apply_log_probe_dev(buf, 100, buf, buf, 1, buf, None) == _lib.CC_EINVAL  # pool not whole pages
     if L.cc_device_count() == 0:
         assert L.cc_engine_stream_entries() == 0
+
+
+def test_log_queue_sizing_and_arguments_need_no_gpu():
+    """cc_apply_logs_work_bytes (host arithmetic): two regions, each a link per
+    piece plus head segments for either grouping -- the insert kernel's, or a
+    page kernel's tail over <= 256 workgroups of <= 1024 threads taking up to
+    twice their even share -- and 256 counts, then the three chunk counters;
+    cc_apply_logs_dev checks its arguments before it needs a device."""
+    import ctypes
+    from curve_amd import _lib
+    L = _lib.lib()
+    for n, max_len in ((1, 1), (65536, 4096), (200000, 3 * 4096)):
+        pieces = n * ((max_len - 1) // 4096 + 2)
+        recs = 2 * (pieces + 1024 * 257)
+        region = -(-pieces * 4 // 256) * 256 + -(-recs * 8 // 256) * 256 + 1024
+        assert L.cc_apply_logs_work_bytes(n, max_len, 4096) == 2 * region + 256, (n, max_len)
+    assert L.cc_apply_logs_work_bytes(0, 4096, 4096) == 0
+    assert L.cc_apply_logs_work_bytes(10, 0, 4096) == 0
+    assert L.cc_apply_logs_work_bytes((1 << 29) + 1, 4096, 4096) == 0
+    arr = (_lib.CcLogBatch * 1)()
+    arr[0].n_updates = 3  # records but no pointers
+    buf = ctypes.c_void_p(4096)
+    assert L.cc_apply_logs_dev(None, 4096, 4096, None, 0, 4096, None, 0, None, 0, None) == _lib.CC_OK
+    assert L.cc_apply_logs_dev(buf, 4096, 4096, None, 1, 4096, buf, 0, buf, 1 << 30, None) == _lib.CC_EINVAL
+    assert L.cc_apply_logs_dev(buf, 4096, 4096, ctypes.cast(arr, ctypes.c_void_p), 1, 4096, buf, 0, buf, 1 << 30,
+                               None) == _lib.CC_EINVAL
+    assert L.cc_apply_logs_dev(buf, 4096, 1000, ctypes.cast(arr, ctypes.c_void_p), 1, 4096, buf, 0, buf, 1 << 30,
+                               None) == _lib.CC_EINVAL  # page size
