@@ -271,7 +271,9 @@ def test_bench_world8_native_exchange_over_stub_rccl(tmp_path):
         pytest.skip("no GPU")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     stub = os.path.join(root, "build", "stub", "libcurvecrc_stubrccl.so")
-    assert os.path.exists(stub), "make -C curve_amd/csrc stubrccl (done by __graft_entry__.build())"
+    assert os.path.exists(stub), "make -C curve_amd/csrc (builds the stub too; __graft_entry__.build())"
+    main_lib = os.path.join(root, "curve_amd", "libcurvecrc.so")
+    assert os.path.getmtime(stub) >= os.path.getmtime(main_lib) - 1, "stub build older than libcurvecrc.so: make"
     d = _bench_world8(tmp_path, "bench_world8_stubrccl.log", {"CURVE_AMD_LIB": stub})
     ex = d["digest_exchange"]
     assert ex["path"].startswith("native RCCL"), ex
