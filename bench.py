@@ -479,8 +479,15 @@ def partial_write_leg(pool, args):
         e0.record(stream)
         C.apply_log(flat, pool.page_crcs, src, d_log, U, 4096, 4096, delta=True)
         e1.record(stream)
+    # and the delta queue (cc_apply_logs_dev, delta = 1): three calls back to back
+    ev_dq = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+    for e0, e1 in ev_dq:
+        e0.record(stream)
+        C.apply_logs(flat, pool.page_crcs, qb, 4096, 4096, delta=True)
+        e1.record(stream)
     torch.cuda.synchronize()
     delta_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_d]))
+    delta_q_ms = float(np.mean([a.elapsed_time(b) / len(qb) for a, b in ev_dq]))
     # the write log's access pattern alone (cc_apply_log_probe_dev): per log,
     # the log re-applied (untimed), then the same touched pages read -- covered
     # rows from the source -- and their dirty rows stored back, no table, no
@@ -522,6 +529,8 @@ def partial_write_leg(pool, args):
                       "updates_per_s": round(U / (delta_ms * 1e-3), 1),
                       "alg_frac_of_hbm_peak": round(alg / (delta_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                       "frac_of_random_probe": round(probe_ms / delta_ms, 4),
+                      "queue_device_ms_per_batch": round(delta_q_ms, 4),
+                      "queue_frac_of_random_probe": round(probe_ms / delta_q_ms, 4),
                       "all_pages_verify_after": delta_ok,
                       "path": "cc_apply_log_delta_dev: stored CRCs updated by linearity, touched rows read only"},
             "queue": {"batches_per_call": len(qb), "device_ms_per_batch": round(q_ms, 4),
