@@ -1528,8 +1528,10 @@ int cc_apply_logs_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, co
         }
         if (!grouped) {  // the first batch (or one after a small batch): the insert kernel
             const uint64_t chunks = (a.n_pieces + kInsertThreads - 1) / kInsertThreads;
-            if (!seg_layout(a.n_pieces, kInsertThreads, (uint32_t)(chunks < kInsertBlocks ? chunks : kInsertBlocks), &lay))
-                return CC_EINVAL;
+            if (!seg_layout(a.n_pieces, kInsertThreads, (uint32_t)(chunks < kInsertBlocks ? chunks : kInsertBlocks), &lay)) {
+                e = hipErrorInvalidValue;  // (not reached: log_work accepted the largest batch)
+                break;
+            }
             region(a, r, lay);
             a.zero_ctrs = ctrs;
             if ((e = launch_log_insert(a, s)) != hipSuccess) break;
