@@ -1420,9 +1420,10 @@ bool logs_work(uint64_t max_updates, uint32_t max_len, uint32_t page_bytes, Logs
     w->max_pieces = one.n_pieces;
     w->table_entries = one.table_entries;
     // head records: the insert kernel's layout <= pieces + 512 (kInsertBlocks + 1);
-    // a page kernel's tail grouping G x rounds x T, rounds = 2 ceil(chunks / G):
-    // <= 2 (pieces + T (G + 1)), T <= 1024, G <= kInsertBlocks
-    const uint64_t recs = 2 * (w->max_pieces + 1024ull * (kInsertBlocks + 1));
+    // a page kernel's tail grouping G x rounds x T, rounds = 2 ceil(chunks / G)
+    // rounded up to kGroupTake: <= 2 (pieces + T (G + 1)) + (kGroupTake - 1) G T,
+    // T <= 1024, G <= kInsertBlocks
+    const uint64_t recs = 2 * (w->max_pieces + 1024ull * (kInsertBlocks + 1)) + (kGroupTake - 1) * 1024ull * kInsertBlocks;
     w->heads_off = align256(w->max_pieces * 4);
     w->counts_off = w->heads_off + align256(recs * 8);
     w->region = w->counts_off + align256(kInsertBlocks * 4);
@@ -1545,10 +1546,12 @@ int cc_apply_logs_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, co
         grouped = false;
         if (j < n_batches && !small(batches[j].n_updates)) {
             const LogLaunch nb = base(batches[j]);
-            // a workgroup may take up to twice its even share of the chunks
+            // a workgroup may take up to twice its even share of the chunks, in
+            // takes of kGroupTake
             const uint64_t chunks = (nb.n_pieces + T - 1) / T;
             const uint32_t G = (uint32_t)a.blocks;
-            const uint64_t rounds = 2 * ((chunks + G - 1) / G);
+            uint64_t rounds = 2 * ((chunks + G - 1) / G);
+            rounds = (rounds + kGroupTake - 1) / kGroupTake * kGroupTake;
             SegLayout nl = {G, (uint32_t)(rounds * T)};
             if (G <= kInsertBlocks && rounds * T < (1ull << 32)) {
                 unsigned char* q = w + (uint64_t)(r ^ 1) * W.region;

@@ -122,6 +122,13 @@ constexpr int log_small_waves(int m, bool delta) { return (!delta && m <= 16) ? 
 // batch (one counter) while the slower ones finish -- so the kernel boundary
 // before the next page kernel is the only barrier the next batch needs.  The
 // fields insert_piece reads, for that batch; n_pieces = 0: nothing to insert.
+// chunks a workgroup claims per take of the tail grouping's counter (A/B: 2 beats
+// 1 by ~0.6 %: half as many, earlier-finishing workgroups do the inserts); a
+// compile-time knob for the A/B builds
+#ifndef CC_GROUP_TAKE
+#define CC_GROUP_TAKE 2
+#endif
+constexpr uint32_t kGroupTake = CC_GROUP_TAKE;
 struct LogInsert {
     const UpdateDesc* upd;
     uint64_t n_pieces;
@@ -132,7 +139,7 @@ struct LogInsert {
     uint32_t* heads;            // one segment of seg_cap records per block of the inserting kernel
     uint32_t* seg_count;        // [gridDim.x of the inserting kernel]
     uint32_t seg_cap;           // >= rounds x the block's threads
-    uint32_t rounds;            // chunks (of the block's threads) one workgroup may take
+    uint32_t rounds;            // chunks (of the block's threads) one workgroup may take: a multiple of kGroupTake
     unsigned long long* take;   // the chunk counter, zero at launch (the grouping kernel before zeroed it)
     unsigned long long* zero;   // the counter the grouping kernel after next takes from: zeroed here
 };

@@ -1414,8 +1414,9 @@ __device__ __forceinline__ void load_rows(uint32_t (&w)[M], const unsigned char*
 
 // cc_apply_logs_dev: the next batch's grouping in this page kernel's tail.  A
 // workgroup whose waves are all done with their pages (its LDS image no longer
-// read: the insert's scratch) takes chunks of 64*WV pieces from one counter
-// until none is left or it holds `rounds` of them (its head segment's bound);
+// read: the insert's scratch) takes kGroupTake chunks of 64*WV pieces at a time
+// from one counter until none is left or it holds `rounds` of them (its head
+// segment's bound);
 // the workgroups that finish first take them while the slow ones finish, so
 // the grouping costs no kernel time and no launch.  Every workgroup stores its
 // segment's count.  Block 0 zeroes the counter the grouping after next uses
@@ -1428,12 +1429,13 @@ __device__ __forceinline__ void group_next(const LogInsert& nx, uint32_t* tab) {
     constexpr uint32_t T = 64u * WV;
     const uint64_t chunks = (nx.n_pieces + T - 1) / T;
     uint32_t used = 0;
-    for (uint32_t r = 0; r < nx.rounds; r++) {
-        if (threadIdx.x == 0) tab[T] = (uint32_t)atomicAdd(nx.take, 1ull);  // (< 2^32 chunks: n_pieces < 2^31)
+    for (uint32_t r = 0; r + kGroupTake <= nx.rounds; r += kGroupTake) {
+        if (threadIdx.x == 0) tab[T] = (uint32_t)atomicAdd(nx.take, 1ull);  // (< 2^32 takes: n_pieces < 2^31)
         __syncthreads();
-        const uint64_t c = tab[T];
+        const uint64_t c = (uint64_t)kGroupTake * tab[T];
         if (c >= chunks) break;  // uniform
-        insert_piece(nx, c * T + threadIdx.x, tab, used);  // ends with a barrier: tab[T] free again
+        for (uint32_t i = 0; i < kGroupTake && c + i < chunks; i++)
+            insert_piece(nx, (c + i) * T + threadIdx.x, tab, used);  // ends with a barrier: tab[T] free again
     }
     if (threadIdx.x == 0) nx.seg_count[blockIdx.x] = used;
 }

@@ -18,6 +18,7 @@ from curve_amd import crc as C  # noqa: E402
 p = argparse.ArgumentParser()
 p.add_argument("--rounds", type=int, default=20)
 p.add_argument("--delta", action="store_true")
+p.add_argument("--only", choices=("singles", "queue"), default=None, help="time one form only (kernel traces)")
 a = p.parse_args()
 dev = torch.device("cuda", 0)
 pb, U, B = 4096, 65536, 10
@@ -44,9 +45,10 @@ def queue():
 for f in (singles, queue, singles, queue):
     f()
 torch.cuda.synchronize()
-ms = {"singles": [], "queue": []}
+ms = {"singles": [], "queue": []} if a.only is None else {a.only: []}
 for r in range(a.rounds):
-    for name, f in ((("singles", singles), ("queue", queue)) if r % 2 == 0 else (("queue", queue), ("singles", singles))):
+    pairs = (("singles", singles), ("queue", queue)) if r % 2 == 0 else (("queue", queue), ("singles", singles))
+    for name, f in (x for x in pairs if x[0] in ms):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
         f()

@@ -149,14 +149,15 @@ def test_log_queue_sizing_and_arguments_need_no_gpu():
     """cc_apply_logs_work_bytes (host arithmetic): two regions, each a link per
     piece plus head segments for either grouping -- the insert kernel's, or a
     page kernel's tail over <= 256 workgroups of <= 1024 threads taking up to
-    twice their even share -- and 256 counts, then the three chunk counters;
+    twice their even share in takes of 2 chunks -- and 256 counts, then the
+    three chunk counters;
     cc_apply_logs_dev checks its arguments before it needs a device."""
     import ctypes
     from curve_amd import _lib
     L = _lib.lib()
     for n, max_len in ((1, 1), (65536, 4096), (200000, 3 * 4096)):
         pieces = n * ((max_len - 1) // 4096 + 2)
-        recs = 2 * (pieces + 1024 * 257)
+        recs = 2 * (pieces + 1024 * 257) + (2 - 1) * 1024 * 256  # kGroupTake = 2
         region = -(-pieces * 4 // 256) * 256 + -(-recs * 8 // 256) * 256 + 1024
         assert L.cc_apply_logs_work_bytes(n, max_len, 4096) == 2 * region + 256, (n, max_len)
     assert L.cc_apply_logs_work_bytes(0, 4096, 4096) == 0
