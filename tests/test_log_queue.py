@@ -154,3 +154,34 @@ def test_log_queue_arguments(dev):
     assert call(2) == 0  # 100 zero-length records (contract breakers: nothing applied) + an empty batch
     torch.cuda.synchronize()
     assert int(pool.sum()) == 0
+
+
+def test_log_queue_streams_trim_and_mixed_calls(dev, oracle):
+    """The queue's two tables are the halves of its stream's engine table: a
+    queue on a second stream, single calls on the same stream between queues
+    (they use the whole, larger table), and a queue after cc_engine_trim (the
+    table rebuilt) all leave the pool and CRCs of in-order application."""
+    from curve_amd import _lib
+    from curve_amd import crc as C
+    rng = np.random.default_rng(515)
+    pb, max_len, pool_bytes = 4096, 4096, 8 << 20
+    host = rng.integers(0, 256, pool_bytes, dtype=np.uint8)
+    bs = _batches(rng, [2000, 3000, 70, 2500, 1800, 4000], pool_bytes, max_len, pb)
+    dev_b = [(to_dev(sd, dev), torch.from_numpy(C.log_records(d, so, ln).view(np.uint8)).to(dev), len(ln))
+             for d, so, ln, sd, _ in bs]
+    d_pool = to_dev(host, dev)
+    crcs = C.page_crc(d_pool, pb)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        C.apply_logs(d_pool, crcs, dev_b[:2], max_len, pb, stream=side)  # a queue on another stream
+        src, d_log, n = dev_b[2]
+        C.apply_log(d_pool, crcs, src, d_log, n, max_len, pb, stream=side)  # a single call between queues
+        C.apply_logs(d_pool, crcs, dev_b[3:4], max_len, pb, stream=side)  # a queue of one
+    side.synchronize()
+    assert _lib.lib().cc_engine_trim() == 0
+    C.apply_logs(d_pool, crcs, dev_b[4:], max_len, pb)  # tables rebuilt after the trim
+    torch.cuda.synchronize()
+    want = _host_apply(host, bs)
+    assert (d_pool.cpu().numpy() == want).all()
+    assert (u32(crcs) == oracle.page_crcs(want, pb)).all()
