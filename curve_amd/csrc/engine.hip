@@ -739,8 +739,11 @@ int pool_page_launches(const void* d_data, uint64_t n_data_pages, uint32_t page_
         a.meta_out = d_meta_crcs;
         a.zero[0] = d_digest;
         a.zero_words[0] = d_digest ? digest_words : 0;
-        if (ev_begin) e = hipEventRecord(static_cast<hipEvent_t>(ev_begin), s);
-        if (e == hipSuccess) e = launch_page_tail(c.get(), a, false, s);
+        // the caller's event pair rides the data launch itself (no marker packets in the step)
+        a.ev_begin = static_cast<hipEvent_t>(ev_begin);
+        a.ev_end = static_cast<hipEvent_t>(ev_end);
+        e = launch_page_tail(c.get(), a, false, s);
+        return map_err(e);
     } else {
         // a metapage launch of its own (static walk; clears the digest), then the data
         PageLaunch m = {};
@@ -754,10 +757,10 @@ int pool_page_launches(const void* d_data, uint64_t n_data_pages, uint32_t page_
         m.zero_words[0] = d_digest ? digest_words : 0;
         geometry_for(c.get(), n_meta, &m);
         e = launch_page_meta(m, s);
-        if (e == hipSuccess && ev_begin) e = hipEventRecord(static_cast<hipEvent_t>(ev_begin), s);
+        a.ev_begin = static_cast<hipEvent_t>(ev_begin);
+        a.ev_end = static_cast<hipEvent_t>(ev_end);
         if (e == hipSuccess) e = launch_page_tail(c.get(), a, false, s);
     }
-    if (e == hipSuccess && ev_end) e = hipEventRecord(static_cast<hipEvent_t>(ev_end), s);
     return map_err(e);
 }
 }  // namespace cc

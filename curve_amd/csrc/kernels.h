@@ -63,6 +63,9 @@ struct PageLaunch {
     // kernels after it: the next launch's tail counter, a digest to XOR into)
     uint32_t* zero[2];
     uint64_t zero_words[2];
+    // non-null: timing events carried by the kernel's own dispatch
+    // (hipExtLaunchKernel), so timing it adds no marker packets to the stream
+    hipEvent_t ev_begin, ev_end;
 };
 
 hipError_t launch_page_crc(const PageLaunch& a, hipStream_t s);

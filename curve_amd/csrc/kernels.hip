@@ -24,6 +24,7 @@
 // (src/chunkserver/datastore/chunkserver_chunkfile.cpp:805,
 // src/chunkserver/copyset_node.cpp:964), all of which call
 // curve::common::CRC32 (src/common/crc32.h:40-55).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -2172,8 +2173,9 @@ hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
     const TailExtra ex = tail_extra(a);
 #define CC_CASE(MM)                                                                                     \
     case MM:                                                                                            \
-        hipLaunchKernelGGL((page_crc_kernel<MM, MODE>), grid, block, 0, s, a.pages, a.n_pages, img,    \
-                           a.kconst, a.out, a.expected, a.sink, a.tile_shift, a.dyn_ctr, a.static_tiles, zr, ex); \
+        hipExtLaunchKernelGGL((page_crc_kernel<MM, MODE>), grid, block, 0, s, a.ev_begin, a.ev_end, 0u,  \
+                              a.pages, a.n_pages, img, a.kconst, a.out, a.expected, a.sink, a.tile_shift, \
+                              a.dyn_ctr, a.static_tiles, zr, ex);                                       \
         break;
     switch (a.words_per_lane) {
         CC_CASE(1)
@@ -2183,8 +2185,8 @@ hipError_t launch_page(const PageLaunch& a, hipStream_t s) {
         CC_CASE(16)
         CC_CASE(32)
         default:
-            hipLaunchKernelGGL((page_crc_kernel_dyn<MODE>), grid, block, 0, s, a.pages, a.n_pages,
-                               a.words_per_lane, img, a.kconst, a.out, a.expected, a.sink, zr);
+            hipExtLaunchKernelGGL((page_crc_kernel_dyn<MODE>), grid, block, 0, s, a.ev_begin, a.ev_end, 0u, a.pages,
+                                  a.n_pages, a.words_per_lane, img, a.kconst, a.out, a.expected, a.sink, zr);
     }
 #undef CC_CASE
     return hipGetLastError();
