@@ -256,9 +256,9 @@ typedef struct cc_update {
  * enqueue.  Retained device memory: 8 B x the next power of two >= 8 x the
  * pieces (n_updates x ((max_len - 1) / page_bytes + 2)) per stream, at most
  * 64 MiB a stream (a log needing more takes a table for that call only), for
- * at most 256 streams; the null stream, hipStreamLegacy and
- * hipStreamPerThread count once per calling thread (one handle, a different
- * stream in each thread).  cc_engine_trim releases them.  Contract per entry: 1 <= len <= max_len and
+ * at most 256 streams; the null stream and hipStreamLegacy are one stream,
+ * hipStreamPerThread counts once per calling thread (its entry is dropped when
+ * the thread exits).  cc_engine_trim releases them.  Contract per entry: 1 <= len <= max_len and
  * dst + len <= pool_bytes -- an entry that breaks it is skipped whole (never
  * half-applied); d_src must not alias d_pool.  page_bytes = 256 * 2^k
  * (k = 0..5).  d_work: >= cc_apply_log_work_bytes(n, max_len, page_bytes) bytes
@@ -284,10 +284,12 @@ int cc_apply_log_delta_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_byte
 /* A QUEUE of write logs applied in order, as n_batches cc_apply_log_dev calls
  * (delta = 0) or cc_apply_log_delta_dev calls (delta = 1) would be on `stream`:
  * the same pool bytes and page CRCs, bit for bit.  Pipelined: the page kernel
- * of batch k also groups batch k+1's pieces (its hash table and head records,
- * in the second of two alternating work regions), so only the first batch (and
- * one after a <= 64-write batch, which takes the one-launch path) pays the
- * separate grouping launch and the kernel boundary behind it.  `batches` is a
+ * of batch k also groups batch k+1's pieces in its tail (workgroups done with
+ * their pages insert them into the other half of the stream's engine table,
+ * which is kept at twice the single-batch size, and the other of two work
+ * regions), so only the first batch (and one after a <= 64-write batch, which
+ * takes the one-launch path) pays the separate grouping launch and the kernel
+ * boundary behind it.  `batches` is a
  * HOST array (its device pointers: as for cc_apply_log_dev, valid until the
  * stream has run the call's work); empty batches are skipped.  d_work: >=
  * cc_apply_logs_work_bytes(largest batch's n_updates, max_len, page_bytes).
