@@ -596,6 +596,20 @@ def read_verify_leg(pool, args):
         walls.append(time.perf_counter() - t0)
     t = float(np.mean(ms))
     per = pages / len(ms)
+    # the access pattern's ceiling (cc_page_list_probe_dev): the same batches'
+    # pages read in read order with everything else removed, verify-on-read's
+    # grid and occupancy; events around each probe call, enqueued back to back
+    lists = [torch.from_numpy(C.read_pages_list(first * pb, npg * pb, pb)).to(dev) for _, first, npg in batches[1:]]
+    pout = torch.empty(max(x.numel() for x in lists), dtype=torch.int32, device=dev)
+    C.page_list_probe(flat, lists[0], lists[0].numel(), pout)  # warm, not waited for
+    ev_p = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in lists]
+    for lst, (e0, e1) in zip(lists, ev_p):
+        e0.record(stream)
+        C.page_list_probe(flat, lst, lst.numel(), pout)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    probe_each = [a.elapsed_time(b) for a, b in ev_p]
+    probe_ms = float(np.mean(probe_each))
     return {"reads_per_batch": n, "pages_per_batch": int(per), "ms_per_batch": round(t, 4),
             "ms_median": round(float(np.median(ms)), 4),
             "alg_frac_of_hbm_peak_at_median": round(per * (pb + 4) / (float(np.median(ms)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -603,6 +617,11 @@ def read_verify_leg(pool, args):
             "GiBps_verified": round(per * pb / GiB / (t * 1e-3), 1),
             "alg_frac_of_hbm_peak": round(per * (pb + 4) / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "wall_ms_incl_host_records": round(float(np.mean(walls)) * 1e3, 3),
+            "frac_of_run_probe": round(probe_ms / t, 4),
+            "run_probe": {"ms_per_batch": round(probe_ms, 4), "ms_each": [round(x, 4) for x in probe_each],
+                          "read_GBps": round(per * pb / (probe_ms * 1e-3) / 1e9, 1),
+                          "path": "cc_page_list_probe_dev: the batch's pages read in read order, verify-on-read's "
+                                  "grid and occupancy, no CRC, no stored CRCs -- the ceiling of this access pattern"},
             "note": "reads + pool + CRC table resident in HBM; one cc_verify_reads_dev call per batch "
                     "(count, scan, verify); alg bytes = 4100 per touched page"}
 

@@ -129,6 +129,7 @@ SIGNATURES = {
     "cc_engine_stream_entries": (_u64, []),
     "cc_apply_log_probe_dev": (_int, [_vp, _u64, _vp, _vp, _u64, _vp, _vp]),
     "cc_apply_logs_work_bytes": (_u64, [_u64, _u32, _u32]),
+    "cc_page_list_probe_dev": (_int, [_vp, _u64, _vp, _u64, _vp, _vp]),
     "cc_apply_logs_dev": (_int, [_vp, _u64, _u32, _vp, _u32, _u32, _vp, _int, _vp, _u64, _vp]),
     "cc_verify_reads_work_bytes": (_u64, [_u64]),
     "cc_verify_reads_dev": (_int, [_vp, _u64, _u32, _vp, _u64, _vp, _vp, _vp, _vp, _u64, _vp]),

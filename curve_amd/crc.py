@@ -486,6 +486,29 @@ def apply_log(pool, page_crcs, src, d_log, n_updates: int, max_len: int, page_by
     return 1
 
 
+def read_pages_list(offs, lens, page_bytes: int = PAGE_SIZE):
+    """Diagnostic helper (host): the pages a batch of reads touches, read after
+    read -- the list cc_page_list_probe_dev walks (int64 page indices; an empty
+    read adds none)."""
+    import numpy as np
+    offs = np.asarray(offs, dtype=np.int64)
+    lens = np.asarray(lens, dtype=np.int64)
+    keep = lens > 0
+    p0 = offs[keep] // page_bytes
+    cnt = (offs[keep] + lens[keep] - 1) // page_bytes - p0 + 1
+    start = np.repeat(p0 - np.concatenate(([0], np.cumsum(cnt)[:-1])), cnt)
+    return start + np.arange(int(cnt.sum()), dtype=np.int64)
+
+
+def page_list_probe(pool, d_pages, n: int, out, stream=None):
+    """cc_page_list_probe_dev (diagnostic): the read traffic of a page list alone
+    -- the ceiling of verify-on-read's access pattern.  `out` gets a word per page."""
+    torch = _torch()
+    with torch.cuda.device(pool.device):
+        check(lib().cc_page_list_probe_dev(_dev_ptr(pool, "pool"), _nbytes(pool), _dev_ptr(d_pages, "pages"), n,
+                                           _dev_ptr(out, "out"), _stream_handle(stream)), "cc_page_list_probe_dev")
+
+
 def apply_logs(pool, page_crcs, batches, max_len: int, page_bytes: int = PAGE_SIZE, stream=None,
                delta: bool = False):
     """cc_apply_logs_dev: a QUEUE of write logs applied in order -- the same

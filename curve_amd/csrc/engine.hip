@@ -1585,6 +1585,23 @@ int cc_apply_logs_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, co
     return map_err(e);
 }
 
+int cc_page_list_probe_dev(const void* d_pool, uint64_t pool_bytes, const uint64_t* d_pages, uint64_t n,
+                           uint32_t* d_out, void* stream) {
+    if (n == 0) return CC_OK;
+    if (!d_pool || !d_pages || !d_out || pool_bytes % 4096 || ((uintptr_t)d_pool & 3u) || ((uintptr_t)d_pages & 7u))
+        return CC_EINVAL;
+    CtxRef c;
+    int rc = get_ctx(&c);
+    if (rc) return rc;
+    PageListProbeLaunch a = {};
+    a.pool = static_cast<const uint32_t*>(d_pool);
+    a.pages = d_pages;
+    a.n = n;
+    a.out = d_out;
+    a.blocks = c->cus;  // one workgroup per CU, as verify-on-read
+    return map_err(launch_page_list_probe(a, static_cast<hipStream_t>(stream)));
+}
+
 int cc_apply_log_probe_dev(void* d_pool, uint64_t pool_bytes, const void* d_src, const cc_log_probe_desc* d_desc,
                            uint64_t n, uint32_t* d_out, void* stream) {
     static_assert(sizeof(cc_log_probe_desc) == sizeof(LogProbeDesc), "probe descriptor layout");

@@ -195,6 +195,15 @@ struct LogProbeLaunch {
     int blocks;
 };
 hipError_t launch_log_probe(const LogProbeLaunch& a, hipStream_t s);
+// diagnostic: the read traffic of a page list alone (4 KiB pages; kernels.hip page_list_probe_kernel)
+struct PageListProbeLaunch {
+    const uint32_t* pool;
+    const uint64_t* pages;
+    uint64_t n;
+    uint32_t* out;  // [n]
+    int blocks;
+};
+hipError_t launch_page_list_probe(const PageListProbeLaunch& a, hipStream_t s);
 
 struct RangeDesc {
     uint64_t off, len;

@@ -1883,6 +1883,47 @@ __global__ __launch_bounds__(64 * kLogWavesFull) void log_probe_kernel(LogProbeL
 }
 
 // ---------------------------------------------------------------------------
+// Diagnostic: the read traffic of a page list (cc_page_list_probe_dev) -- the
+// access pattern of a batch of datastore reads with everything else removed:
+// verify-on-read's grid and occupancy (kRvWaves waves a CU, LDS unused), each
+// wave an equal contiguous share of the list (64 indices a lane-load), two
+// pages in flight behind the one being reduced, a rotate-XOR instead of the
+// CRC, one word a page out.
+// ---------------------------------------------------------------------------
+constexpr int kListProbeWaves = 8;  // = kRvWaves (verify-on-read's occupancy)
+template <int M>
+__global__ __launch_bounds__(64 * kListProbeWaves) void page_list_probe_kernel(PageListProbeLaunch a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t W = (uint64_t)gridDim.x * kListProbeWaves, gw = (uint64_t)blockIdx.x * kListProbeWaves + wave;
+    const uint64_t first = a.n * gw / W, last = a.n * (gw + 1) / W;
+    const uint32_t* pages = a.pool + lane;
+    for (uint64_t base = first; base < last; base += 64) {
+        const uint64_t ih = base + lane;
+        const uint64_t pg = a.pages[ih < last ? ih : base];
+        const uint32_t cnt = (uint32_t)(last - base < 64 ? last - base : 64);
+        auto at = [&](uint32_t k) { return readlane64(pg, k < cnt ? k : cnt - 1); };  // clamped: same loads every step
+        uint32_t A[M], B[M], Cq[M];
+        load_page<M>(A, pages + at(0) * (64u * M));
+        load_page<M>(B, pages + at(1) * (64u * M));
+        auto step = [&](uint32_t (&X)[M], uint32_t k, uint32_t (&Y)[M]) {
+            load_page<M>(Y, pages + at(k + 2) * (64u * M));
+            uint32_t x = X[0];
+#pragma unroll
+            for (int j = 1; j < M; j++) x = ((x << 1) | (x >> 31)) ^ X[j];
+            x = wave_xor(x);
+            if (lane == 0) a.out[base + k] = x;
+            return k + 1 < cnt;
+        };
+        for (uint32_t k = 0;; k += 3) {
+            if (!step(A, k, Cq)) break;
+            if (!step(B, k + 1, A)) break;
+            if (!step(Cq, k + 2, B)) break;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Verify-on-read for a batch of datastore reads (cc_verify_reads_dev)
 // ---------------------------------------------------------------------------
 // Pages a read touches (0 for an empty read and for one past the pool).
@@ -2336,6 +2377,12 @@ hipError_t launch_log_small(const LogLaunch& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+
+hipError_t launch_page_list_probe(const PageListProbeLaunch& a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(page_list_probe_kernel<16>, dim3(a.blocks), dim3(64 * kListProbeWaves), 0, s, a);
+    return hipGetLastError();
+}
 
 hipError_t launch_log_probe(const LogProbeLaunch& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;

@@ -638,6 +638,17 @@ typedef struct cc_log_probe_desc {
 int cc_apply_log_probe_dev(void* d_pool, uint64_t pool_bytes, const void* d_src, const cc_log_probe_desc* d_desc,
                            uint64_t n, uint32_t* d_out, void* stream);
 
+/* Diagnostic (no reference counterpart): the read traffic of a list of 4 KiB
+ * pages alone -- d_pages[i] = a page index of the pool, in list order (for a
+ * batch of reads: each read's pages in turn) -- the ceiling cc_verify_reads_dev
+ * is held to on its access pattern.  Verify-on-read's grid and occupancy (a
+ * workgroup of 8 waves per CU, LDS unused), each wave an equal contiguous share
+ * of the list, two pages in flight, no CRC, no stored-CRC loads.  d_out[i] = an
+ * XOR of page i's words.  Indices past the pool: CC_EINVAL is not checked on
+ * the device -- the caller's list must hold pool pages.  Enqueue only. */
+int cc_page_list_probe_dev(const void* d_pool, uint64_t pool_bytes, const uint64_t* d_pages, uint64_t n,
+                           uint32_t* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,59 @@
+"""The verify-on-read access-pattern probe (diagnostic cc_page_list_probe_dev,
+the ceiling cc_verify_reads_dev is held to): its host-side page list -- the
+pages of a batch of reads, read after read, as CSChunkFile::Read's requests
+touch them (chunkserver_chunkfile.cpp:497-536; a partly covered page counts
+whole) -- against a per-read loop, its argument checks without a GPU, and on
+the device its per-page words against a numpy restatement of the reduction."""
+import ctypes
+
+import numpy as np
+import pytest
+
+
+def test_read_pages_list_matches_a_per_read_loop():
+    from curve_amd import crc as C
+    rng = np.random.default_rng(31)
+    for pb in (4096, 512):
+        offs = rng.integers(0, 1 << 24, 300)
+        lens = rng.integers(0, 40000, 300)
+        lens[::17] = 0
+        want = []
+        for o, n in zip(offs.tolist(), lens.tolist()):
+            if n:
+                want.extend(range(o // pb, (o + n - 1) // pb + 1))
+        got = C.read_pages_list(offs, lens, pb)
+        assert got.dtype == np.int64 and got.tolist() == want
+    assert C.read_pages_list([], [], 4096).size == 0
+
+
+def test_page_list_probe_arguments_need_no_gpu():
+    from curve_amd import _lib
+    L = _lib.lib()
+    buf = ctypes.c_void_p(4096)
+    assert L.cc_page_list_probe_dev(None, 0, None, 0, None, None) == _lib.CC_OK  # empty list
+    assert L.cc_page_list_probe_dev(None, 4096, buf, 1, buf, None) == _lib.CC_EINVAL
+    assert L.cc_page_list_probe_dev(buf, 100, buf, 1, buf, None) == _lib.CC_EINVAL  # pool not whole pages
+    assert L.cc_page_list_probe_dev(buf, 4096, ctypes.c_void_p(4100), 1, buf, None) == _lib.CC_EINVAL  # list alignment
+
+
+@pytest.mark.gpu
+def test_page_list_probe_words_on_device():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from curve_amd import crc as C
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(7)
+    host = rng.integers(0, 256, 64 << 20, dtype=np.uint8)
+    pool = torch.from_numpy(host).to(dev)
+    for n in (1, 2, 3, 63, 64, 65, 5000, 70000):
+        pages = rng.integers(0, (64 << 20) // 4096, n).astype(np.int64)
+        out = torch.full((n,), 7, dtype=torch.int32, device=dev)
+        C.page_list_probe(pool, torch.from_numpy(pages).to(dev), n, out)
+        torch.cuda.synchronize()
+        w = host.view(np.uint32).reshape(-1, 16, 64)[pages]  # [page][row j][lane]
+        x = w[:, 0, :].astype(np.uint64)
+        for j in range(1, 16):
+            x = (((x << 1) | (x >> 31)) & 0xFFFFFFFF) ^ w[:, j, :]
+        want = np.bitwise_xor.reduce(x.astype(np.uint32), axis=1)
+        assert (out.cpu().numpy().view(np.uint32) == want).all(), n
