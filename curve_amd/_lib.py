@@ -194,6 +194,19 @@ _lib = None
 _host = None
 
 
+def _one_hip_runtime():
+    """Load torch (if present) BEFORE libcurvecrc: torch's wheel carries its own
+    libamdhip64.so.7 / libhsa-runtime64 and loads them by path, so a process
+    that loaded /opt/rocm's first (through libcurvecrc) ends up with TWO HIP
+    runtimes, and the one libcurvecrc bound to finds no usable device
+    (CC_ENODEV on every call; scripts/load_order_probe.py).  With torch first,
+    libcurvecrc's libamdhip64.so.7 resolves to the runtime already loaded."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def host_lib():
     """libcurvehost.so (the C++ IntegrityService behind include/curve_integrity.h)."""
     global _host
@@ -229,6 +242,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise OSError(f"{LIB_PATH} missing: build it with `make -C {CSRC}` "
                           "(or __graft_entry__.build()); there is no CPU fallback")
+        _one_hip_runtime()
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)

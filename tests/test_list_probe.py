@@ -57,3 +57,23 @@ def test_page_list_probe_words_on_device():
             x = (((x << 1) | (x >> 31)) & 0xFFFFFFFF) ^ w[:, j, :]
         want = np.bitwise_xor.reduce(x.astype(np.uint32), axis=1)
         assert (out.cpu().numpy().view(np.uint32) == want).all(), n
+
+
+@pytest.mark.gpu
+def test_library_loaded_before_torch_still_finds_the_device():
+    """curve_amd._lib.lib() imports torch before it loads libcurvecrc, so a
+    process that touches the library first still has ONE HIP runtime (torch's
+    wheel loads its own libamdhip64 by path; two runtimes left libcurvecrc with
+    no usable device).  A child process loads the library, then torch, then
+    calls the device."""
+    import os
+    import subprocess
+    import sys
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "load_order_probe.py"), "lib"], cwd=root,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "lib probe ok" in r.stdout and "failed" not in r.stdout, r.stdout
