@@ -351,6 +351,7 @@ def files_leg(args):
     import shutil
     import tempfile
     from curve_amd import crc as C
+    from curve_amd.chunkfile import ChunkFileMetaPage
     n = args.file_chunks
     d = tempfile.mkdtemp(prefix="cc_files_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
@@ -358,7 +359,8 @@ def files_leg(args):
         body = rng.integers(0, 256, C.CHUNK_SIZE + C.META_PAGE_SIZE, dtype=np.uint8)
         paths = []
         for i in range(n):
-            body[:8] = np.frombuffer(np.uint64(i).tobytes(), dtype=np.uint8)
+            # a valid metapage (sn = i + 1: every file distinct), random data
+            body[:C.META_PAGE_SIZE] = np.frombuffer(ChunkFileMetaPage(sn=i + 1).encode(C.META_PAGE_SIZE), dtype=np.uint8)
             p = os.path.join(d, f"chunk_{i}")
             body.tofile(p)
             paths.append(p)
@@ -383,6 +385,23 @@ def files_leg(args):
             out[key + "_each"] = [round(x, 2) for x in runs[t]]
         out["default_io_threads"] = C.default_io_threads()
         out["passes"] = args.file_passes
+        # an integrity job's check of the same files against
+        # their per-page CRC tables (cc_integrity_check: the reads as above, page
+        # CRCs on the device, compared with the sidecar tables; the first pass
+        # creates the tables, untimed)
+        from curve_amd import integrity as I
+        tables = [q + ".pcrc" for q in paths]
+        first = I.check_files(paths, tables)
+        assert all(r.status == 0 and r.table == "created" for r in first), first[:2]
+        ic = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            res = I.check_files(paths, tables)
+            ic.append(fb / (time.perf_counter() - t0))
+            assert all(r.status == 0 and r.bad_pages == 0 and r.table == "ok" for r in res), res[:2]
+        out["integrity_check"] = {"GiBps": round(float(np.median(ic)), 2), "GiBps_each": [round(x, 2) for x in ic],
+                                  "path": "cc_integrity_check: the files read by the engine's readers, page CRCs on "
+                                          "the device, compared with their stored per-page CRC tables (0 bad pages)"}
         return out
     finally:
         shutil.rmtree(d, ignore_errors=True)
