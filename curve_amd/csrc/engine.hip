@@ -1595,6 +1595,7 @@ int cc_page_list_probe_dev(const void* d_pool, uint64_t pool_bytes, const uint64
     if (rc) return rc;
     PageListProbeLaunch a = {};
     a.pool = static_cast<const uint32_t*>(d_pool);
+    a.pool_pages = pool_bytes / 4096;
     a.pages = d_pages;
     a.n = n;
     a.out = d_out;

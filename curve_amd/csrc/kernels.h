@@ -198,6 +198,7 @@ hipError_t launch_log_probe(const LogProbeLaunch& a, hipStream_t s);
 // diagnostic: the read traffic of a page list alone (4 KiB pages; kernels.hip page_list_probe_kernel)
 struct PageListProbeLaunch {
     const uint32_t* pool;
+    uint64_t pool_pages;  // an index >= this reads page 0 instead (never outside the pool)
     const uint64_t* pages;
     uint64_t n;
     uint32_t* out;  // [n]

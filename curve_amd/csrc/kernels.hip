@@ -1900,7 +1900,8 @@ __global__ __launch_bounds__(64 * kListProbeWaves) void page_list_probe_kernel(P
     const uint32_t* pages = a.pool + lane;
     for (uint64_t base = first; base < last; base += 64) {
         const uint64_t ih = base + lane;
-        const uint64_t pg = a.pages[ih < last ? ih : base];
+        const uint64_t pg0 = a.pages[ih < last ? ih : base];
+        const uint64_t pg = pg0 < a.pool_pages ? pg0 : 0;  // a bad index reads page 0, never past the pool
         const uint32_t cnt = (uint32_t)(last - base < 64 ? last - base : 64);
         auto at = [&](uint32_t k) { return readlane64(pg, k < cnt ? k : cnt - 1); };  // clamped: same loads every step
         uint32_t A[M], B[M], Cq[M];

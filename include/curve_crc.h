@@ -644,8 +644,8 @@ int cc_apply_log_probe_dev(void* d_pool, uint64_t pool_bytes, const void* d_src,
  * is held to on its access pattern.  Verify-on-read's grid and occupancy (a
  * workgroup of 8 waves per CU, LDS unused), each wave an equal contiguous share
  * of the list, two pages in flight, no CRC, no stored-CRC loads.  d_out[i] = an
- * XOR of page i's words.  Indices past the pool: CC_EINVAL is not checked on
- * the device -- the caller's list must hold pool pages.  Enqueue only. */
+ * XOR of page i's words.  An index past the pool reads page 0 instead (never
+ * outside the pool).  Enqueue only. */
 int cc_page_list_probe_dev(const void* d_pool, uint64_t pool_bytes, const uint64_t* d_pages, uint64_t n,
                            uint32_t* d_out, void* stream);
 

@@ -57,6 +57,13 @@ def test_page_list_probe_words_on_device():
             x = (((x << 1) | (x >> 31)) & 0xFFFFFFFF) ^ w[:, j, :]
         want = np.bitwise_xor.reduce(x.astype(np.uint32), axis=1)
         assert (out.cpu().numpy().view(np.uint32) == want).all(), n
+    # an index past the pool reads page 0 (no access outside the pool)
+    bad = torch.tensor([3, (64 << 20) // 4096, 1 << 40], dtype=torch.int64, device=dev)
+    out = torch.zeros(3, dtype=torch.int32, device=dev)
+    C.page_list_probe(pool, bad, 3, out)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    assert o[1] == o[2] and o[0] != o[1]
 
 
 @pytest.mark.gpu
