@@ -1615,6 +1615,7 @@ int cc_apply_log_probe_dev(void* d_pool, uint64_t pool_bytes, const void* d_src,
     if (rc) return rc;
     LogProbeLaunch a = {};
     a.pool = static_cast<unsigned char*>(d_pool);
+    a.pool_pages = pool_bytes / 4096;
     a.src = static_cast<const unsigned char*>(d_src);
     a.desc = reinterpret_cast<const LogProbeDesc*>(d_desc);
     a.n = n;

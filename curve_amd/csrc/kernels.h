@@ -188,6 +188,7 @@ struct LogProbeDesc {
 };
 struct LogProbeLaunch {
     unsigned char* pool;
+    uint64_t pool_pages;  // a descriptor naming a page >= this touches nothing (reads page 0, stores none)
     const unsigned char* src;
     const LogProbeDesc* desc;
     uint64_t n;

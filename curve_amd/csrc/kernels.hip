@@ -1841,7 +1841,8 @@ __global__ __launch_bounds__(64 * kLogWavesFull) void log_probe_kernel(LogProbeL
     const uint64_t first = a.n * gw / W, last = a.n * (gw + 1) / W;
     for (uint64_t base = first; base < last; base += 64) {
         const uint64_t ih = base + lane;
-        const LogProbeDesc d = a.desc[ih < last ? ih : base];
+        LogProbeDesc d = a.desc[ih < last ? ih : base];
+        if (d.page >= a.pool_pages) d = LogProbeDesc{0, 0, 0u, 0u};  // past the pool: read page 0, store nothing
         const uint32_t cnt = (uint32_t)(last - base < 64 ? last - base : 64);
         uint32_t ring[D][M];
         auto load = [&](uint32_t (&Y)[M], uint32_t k) {

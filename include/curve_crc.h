@@ -628,7 +628,9 @@ int cc_page_load_probe_dev(const void* d_pages, uint64_t n_pages, uint32_t* d_ou
  * others from the page -- and the rows stored back.  Same grid and occupancy
  * as the write log's page pass, no table, no CRC.  It stores back the bytes it
  * loaded: run right after the log it describes was applied, it changes no
- * byte.  d_out[i] = an XOR of page i's words.  Enqueue only. */
+ * byte.  d_out[i] = an XOR of page i's words.  A descriptor naming a page past
+ * the pool touches nothing (page 0 read, no store); source offsets are the
+ * caller's to keep inside d_src.  Enqueue only. */
 typedef struct cc_log_probe_desc {
     uint64_t page;
     uint64_t src_off;

@@ -91,3 +91,16 @@ def test_probe_is_idempotent_after_its_log():
         want ^= words[:, j]
     assert torch.equal(out, want)
     assert int(C.page_verify(pool, crcs, 4096)[0]) == 0
+    # a descriptor naming a page past the pool touches nothing: page 0 read, no store
+    bad = d[:2].copy()
+    bad["page"] = [pool.numel() // 4096, 1 << 40]
+    bad["covered"], bad["dirty"] = 0xFFFF, 0xFFFF
+    out2 = torch.zeros(2, dtype=torch.int32, device=dev)
+    C.log_probe(pool, src, torch.from_numpy(bad.view(np.uint8)).to(dev), 2, out2)
+    torch.cuda.synchronize()
+    assert torch.equal(pool, before)
+    w0 = pool.view(torch.int32)[:1024]
+    x0 = w0[0].clone()
+    for j in range(1, 1024):
+        x0 ^= w0[j]
+    assert int(out2[0]) == int(x0) == int(out2[1])
