@@ -1600,7 +1600,22 @@ int cc_page_list_probe_dev(const void* d_pool, uint64_t pool_bytes, const uint64
     a.n = n;
     a.out = d_out;
     a.blocks = c->cus;  // one workgroup per CU, as verify-on-read
-    return map_err(launch_page_list_probe(a, static_cast<hipStream_t>(stream)));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // the dynamic tail's counter: one slot set of the stream's tail block, as the page kernel's
+    {
+        std::lock_guard<std::mutex> lk(c->tail_mu);
+        if (DevCtx::TailBlock* t = tail_block(c.get(), s)) {
+            a.dyn_ctr = t->p + t->parity * kDynCtrWords64;
+            a.dyn_next = t->p + (t->parity ^ 1u) * kDynCtrWords64;
+            const hipError_t e = launch_page_list_probe(a, s);
+            if (e == hipSuccess)
+                t->parity ^= 1u;
+            else
+                t->dirty = true;
+            return map_err(e);
+        }
+    }
+    return map_err(launch_page_list_probe(a, s));  // no tail block free: a static split
 }
 
 int cc_apply_log_probe_dev(void* d_pool, uint64_t pool_bytes, const void* d_src, const cc_log_probe_desc* d_desc,

@@ -204,6 +204,11 @@ struct PageListProbeLaunch {
     uint64_t n;
     uint32_t* out;  // [n]
     int blocks;
+    // dynamic tail, as verify-on-read's: the last 1/16 of the list in 32-page
+    // chunks through *dyn_ctr (zero at launch); the launch zeroes *dyn_next (the
+    // stream's other slot set) for the next one.  Null: a static split only.
+    unsigned long long* dyn_ctr;
+    unsigned long long* dyn_next;
 };
 hipError_t launch_page_list_probe(const PageListProbeLaunch& a, hipStream_t s);
 

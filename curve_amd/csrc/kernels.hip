@@ -1892,13 +1892,22 @@ __global__ __launch_bounds__(64 * kLogWavesFull) void log_probe_kernel(LogProbeL
 // CRC, one word a page out.
 // ---------------------------------------------------------------------------
 constexpr int kListProbeWaves = 8;  // = kRvWaves (verify-on-read's occupancy)
+constexpr uint64_t kRvDynDivList = 16;   // = kRvDynDiv: the last 1/16 of the list is the dynamic tail
+constexpr uint64_t kRvDynSlotsList = 32;  // = kRvDynSlots: pages per tail chunk
 template <int M>
 __global__ __launch_bounds__(64 * kListProbeWaves) void page_list_probe_kernel(PageListProbeLaunch a) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t W = (uint64_t)gridDim.x * kListProbeWaves, gw = (uint64_t)blockIdx.x * kListProbeWaves + wave;
-    const uint64_t first = a.n * gw / W, last = a.n * (gw + 1) / W;
+    // the stream's other slot set, every head of it (the page kernel's next launch may pull from all)
+    if (a.dyn_next && blockIdx.x == 0 && threadIdx.x < kDynHeads) atomicExch(a.dyn_next + threadIdx.x * kDynHeadStride, 0ull);
+    // static shares of the first Ts entries, then 32-entry chunks of the rest from
+    // one counter (verify-on-read's tail: kRvDynDiv, kRvDynSlots)
+    const uint64_t Ts = a.dyn_ctr ? a.n - a.n / kRvDynDivList : a.n;
+    const uint64_t n_dyn = (a.n - Ts + kRvDynSlotsList - 1) / kRvDynSlotsList;
+    uint64_t first = Ts * gw / W, last = Ts * (gw + 1) / W;
     const uint32_t* pages = a.pool + lane;
+    for (;;) {
     for (uint64_t base = first; base < last; base += 64) {
         const uint64_t ih = base + lane;
         const uint64_t pg0 = a.pages[ih < last ? ih : base];
@@ -1922,6 +1931,14 @@ __global__ __launch_bounds__(64 * kListProbeWaves) void page_list_probe_kernel(P
             if (!step(B, k + 1, A)) break;
             if (!step(Cq, k + 2, B)) break;
         }
+    }
+    if (!a.dyn_ctr) break;
+    unsigned long long c = 0;
+    if (lane == 0) c = atomicAdd(a.dyn_ctr, 1ull);
+    c = readlane64(c, 0);
+    if (c >= n_dyn) break;
+    first = Ts + c * kRvDynSlotsList;
+    last = first + kRvDynSlotsList < a.n ? first + kRvDynSlotsList : a.n;
     }
 }
 

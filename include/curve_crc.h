@@ -643,9 +643,11 @@ int cc_apply_log_probe_dev(void* d_pool, uint64_t pool_bytes, const void* d_src,
 /* Diagnostic (no reference counterpart): the read traffic of a list of 4 KiB
  * pages alone -- d_pages[i] = a page index of the pool, in list order (for a
  * batch of reads: each read's pages in turn) -- the ceiling cc_verify_reads_dev
- * is held to on its access pattern.  Verify-on-read's grid and occupancy (a
- * workgroup of 8 waves per CU, LDS unused), each wave an equal contiguous share
- * of the list, two pages in flight, no CRC, no stored-CRC loads.  d_out[i] = an
+ * is held to on its access pattern.  Verify-on-read's grid, occupancy and
+ * schedule (a workgroup of 8 waves per CU, LDS unused; each wave an equal
+ * contiguous share of the first 15/16 of the list, the rest in 32-page chunks
+ * to whichever waves finish first), two pages in flight, no CRC, no stored-CRC
+ * loads.  d_out[i] = an
  * XOR of page i's words.  An index past the pool reads page 0 instead (never
  * outside the pool).  Enqueue only. */
 int cc_page_list_probe_dev(const void* d_pool, uint64_t pool_bytes, const uint64_t* d_pages, uint64_t n,

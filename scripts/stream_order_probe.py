@@ -25,7 +25,7 @@ a = p.parse_args()
 dev = torch.device("cuda", 0)
 pool = torch.empty(16 << 30, dtype=torch.uint8, device=dev).random_(0, 256)
 W = torch.cuda.get_device_properties(dev).multi_processor_count * 8
-n = 1058816 // W * W  # a whole number of pages per wave
+n = 1058816 // (W * 64) * W * 64  # a whole number of 64-page tiles per wave (~the WAL leg's size)
 base = np.arange(n, dtype=np.int64) + 4096
 
 

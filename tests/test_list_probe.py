@@ -84,3 +84,27 @@ def test_library_loaded_before_torch_still_finds_the_device():
                        capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "lib probe ok" in r.stdout and "failed" not in r.stdout, r.stdout
+
+
+@pytest.mark.gpu
+def test_page_list_probe_shares_the_streams_tail_block():
+    """The probe's dynamic tail takes a slot set of the stream's tail block, as
+    the page kernel does, and leaves the other one zero: page CRC launches
+    interleaved with probe launches on one stream stay exact."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from curve_amd import crc as C
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(17)
+    host = rng.integers(0, 256, 256 << 20, dtype=np.uint8)
+    pool = torch.from_numpy(host).to(dev)
+    want = C.page_crc(pool, 4096).clone()
+    pages = torch.from_numpy(rng.integers(0, (256 << 20) // 4096, 200000).astype(np.int64)).to(dev)
+    out = torch.empty(200000, dtype=torch.int32, device=dev)
+    for _ in range(5):
+        C.page_list_probe(pool, pages, 200000, out)
+        got = C.page_crc(pool, 4096)
+        C.page_list_probe(pool, pages, 200000, out)
+        C.page_list_probe(pool, pages, 200000, out)
+        assert torch.equal(got, want)
