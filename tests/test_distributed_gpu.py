@@ -274,7 +274,13 @@ def test_bench_world8_native_exchange_over_stub_rccl(tmp_path):
     assert os.path.exists(stub), "make -C curve_amd/csrc (builds the stub too; __graft_entry__.build())"
     main_lib = os.path.join(root, "curve_amd", "libcurvecrc.so")
     assert os.path.getmtime(stub) >= os.path.getmtime(main_lib) - 1, "stub build older than libcurvecrc.so: make"
-    d = _bench_world8(tmp_path, "bench_world8_stubrccl.log", {"CURVE_AMD_LIB": stub})
+    import glob
+    before = set(glob.glob("/dev/shm/ccrcclstub-*"))
+    try:
+        d = _bench_world8(tmp_path, "bench_world8_stubrccl.log", {"CURVE_AMD_LIB": stub})
+    finally:  # a rank that died before its destroy leaves its segment behind: remove it
+        for f in set(glob.glob("/dev/shm/ccrcclstub-*")) - before:
+            os.unlink(f)
     ex = d["digest_exchange"]
     assert ex["path"].startswith("native RCCL"), ex
     assert ex["matches_torch_distributed"] is True and ex["matches_cpu_chain"] is True, ex
