@@ -280,7 +280,10 @@ def test_bench_world8_native_exchange_over_stub_rccl(tmp_path):
         d = _bench_world8(tmp_path, "bench_world8_stubrccl.log", {"CURVE_AMD_LIB": stub})
     finally:  # a rank that died before its destroy leaves its segment behind: remove it
         for f in set(glob.glob("/dev/shm/ccrcclstub-*")) - before:
-            os.unlink(f)
+            try:
+                os.unlink(f)
+            except FileNotFoundError:
+                pass
     ex = d["digest_exchange"]
     assert ex["path"].startswith("native RCCL"), ex
     assert ex["matches_torch_distributed"] is True and ex["matches_cpu_chain"] is True, ex
