@@ -55,6 +55,9 @@ def parse():
     p.add_argument("--stream-chunks-per-rank", type=int, default=2000, help="N>1: streamed chunks per rank")
     p.add_argument("--file-chunks", type=int, default=128, help="datastore read-path leg (0 = skip)")
     p.add_argument("--file-passes", type=int, default=5, help="datastore read-path leg: passes per io-thread count")
+    p.add_argument("--scan-op-threads", type=int, default=10,
+                   help="scan-op leg: apply threads (wconcurrentapply.size, conf/chunkserver.conf:183; 0 = skip)")
+    p.add_argument("--scan-op-calls", type=int, default=500, help="scan-op leg: ops per thread")
     p.add_argument("--wal-entries", type=int, default=65536, help="WAL replay leg: entries per batch (0 = skip)")
     p.add_argument("--no-numa-bind", action="store_true",
                    help="leave the CPU affinity alone (default: bind to the GPU's NUMA node, see bind_to_gpu_numa)")
@@ -104,8 +107,9 @@ def bind_to_gpu_numa(dev):
     interconnect at random.  N = 1 too: unbound, the files leg (page cache ->
     pinned staging by the reader threads) measured 47.0 / 32.5 / 41.8 GiB/s in
     three processes on one box, bound 46.7 / 45.9 / 48.4; the pinned H2D legs
-    are the same either way (profiles/numa_files_ab_r05.jsonl).  Threads made
-    afterwards inherit it.  Never fatal: reports what it did ("bound" false
+    are the same either way (profiles/numa_files_ab_r05.jsonl).  Every thread
+    the process has at that point (the HIP runtime's included) is bound, and
+    threads made afterwards inherit the mask.  Never fatal: reports what it did ("bound" false
     and why otherwise)."""
     try:
         p = torch.cuda.get_device_properties(dev)
@@ -117,8 +121,19 @@ def bind_to_gpu_numa(dev):
         if node < 0 or not use or use == allowed:
             return {"numa_node": node, "bound": False,
                     "why": "no NUMA node" if node < 0 else "no local CPU allowed" if not use else "already local"}
-        os.sched_setaffinity(0, use)
-        return {"numa_node": node, "bound": True, "cpus": len(use), "of_allowed": len(allowed)}
+        # every thread of the process, not only this one: the HIP runtime's
+        # threads already exist (started by the device query above) and keep
+        # their own masks otherwise; threads made later inherit the mask
+        tids = [int(t) for t in os.listdir("/proc/self/task")]
+        bound = 0
+        for tid in tids:
+            try:
+                os.sched_setaffinity(tid, use)
+                bound += 1
+            except OSError:
+                pass  # a thread that exited meanwhile
+        return {"numa_node": node, "bound": True, "cpus": len(use), "of_allowed": len(allowed),
+                "threads_bound": bound, "threads_seen": len(tids)}
     except Exception as e:  # report, never fail the run on it
         return {"bound": False, "why": repr(e)}
 
@@ -207,6 +222,121 @@ def e2e_leg(args, dev):
         reps += 1
     el = time.perf_counter() - t0
     return round(reps * nb / GiB / el, 2)
+
+
+def _scan_op_lib():
+    import ctypes
+    L = ctypes.CDLL(os.path.join(ROOT, "curve_amd", "host", "libscanop_bench.so"))
+    L.sob_run.restype = ctypes.c_int
+    L.sob_run.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                          ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    return L
+
+
+SCAN_OP_MODES = {"cpu": 0, "gpu": 1, "routed": 2}
+
+
+def run_scan_ops(bufs, offs, lens, calls, mode):
+    """curve_amd/host/scan_op_bench.cpp sob_run: thread t (one per buffer) runs
+    `calls` ops over bufs[t], op i = (offs[i % n], lens[i % n]); mode "cpu"
+    (crc32c_value), "gpu" (cc_page_crc_host + cc_fold_host) or "routed"
+    (cchost::ScanOpCrc).  Returns (rc, latency us [t, i], crcs [t, i], wall s,
+    summed calling-thread CPU s); run_scan_ops.last_process_cpu_s = the whole
+    process's CPU s over the run (HIP runtime threads included, and the
+    launching thread's spin while it waits for the start)."""
+    import ctypes
+    L = _scan_op_lib()
+    t = len(bufs)
+    ptrs = (ctypes.c_void_p * t)(*[b.ctypes.data for b in bufs])
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    lat = np.zeros(t * calls, dtype=np.float64)
+    crcs = np.zeros(t * calls, dtype=np.uint32)
+    out = np.zeros(3, dtype=np.float64)
+    rc = L.sob_run(t, ptrs, offs.ctypes.data, lens.ctypes.data, len(offs), calls, SCAN_OP_MODES[mode],
+                   lat.ctypes.data, crcs.ctypes.data, out.ctypes.data)
+    run_scan_ops.last_process_cpu_s = float(out[2])
+    return rc, lat.reshape(t, calls), crcs.reshape(t, calls), float(out[0]), float(out[1])
+
+
+def scan_op_leg(args):
+    """Row f1 at the reference's own call shape: ScanChunkRequest::OnApply hashes
+    ONE scan op per raft-applied request -- the 4 KiB metapage or one 4 MiB data
+    slice, `crc = CRC32(readBuffer, size)` (op_request.cpp:776-794, :847) -- on
+    the write apply pool, wconcurrentapply.size = 10 threads
+    (conf/chunkserver.conf:183, op_request.cpp:179-187); a 16 MiB chunk is 5 ops
+    (scan_manager_test.cpp:107-142).  Here 1 and 10 native threads (no
+    interpreter between calls) each run a chunk file's 5 ops in turn over a
+    pinned chunk file of their own, per call: the CPU primitive crc32c_value
+    (the drop-in for CRC32), cc_page_crc_host + cc_fold_host,
+    and the routed call cchost::ScanOpCrc (metapage on the CPU, slices on the
+    GPU).  Every op's CRC is checked against the CPU primitive's.  Then one
+    thread's per-call latency by op size, CPU vs GPU, for the size cutoff."""
+    T = args.scan_op_threads
+    calls = args.scan_op_calls
+    file_bytes = 4096 + (16 << 20)
+    hs = [torch.empty(file_bytes, dtype=torch.uint8, pin_memory=True).random_(0, 256) for _ in range(T)]
+    bufs = [h.numpy() for h in hs]
+    offs = [0] + [4096 + k * (4 << 20) for k in range(4)]
+    lens = [4096] + [4 << 20] * 4
+    op_bytes = np.array(lens * (calls // len(lens) + 1))[:calls]
+    # the CPU primitive's CRC of every op of every thread's file: the check
+    rc, _, c0, _, _ = run_scan_ops(bufs, offs, lens, len(offs), "cpu")
+    assert rc == 0
+    want = c0
+    res = {"threads": {}, "ops_per_thread": calls,
+           "op_mix": "per chunk file: 4 KiB metapage + 4 x 4 MiB slices (5 ScanChunkRequests)"}
+    for nt in sorted({1, T}):
+        per = {}
+        for mode in ("cpu", "gpu", "routed"):
+            run_scan_ops(bufs[:nt], offs, lens, 2 * len(offs), mode)  # warm: lanes, staging, pages
+            rc, lat, crcs, wall, cpu_s = run_scan_ops(bufs[:nt], offs, lens, calls, mode)
+            ok = rc == 0 and bool(all((crcs[t][: calls] == np.resize(want[t], calls)).all() for t in range(nt)))
+            total = float(op_bytes.sum()) * nt
+            sl = lat[:, op_bytes == (4 << 20)].ravel()
+            mp = lat[:, op_bytes == 4096].ravel()
+            per[mode] = {"agg_GiBps": round(total / GiB / wall, 2),
+                         "slice_us_p50": round(float(np.percentile(sl, 50)), 1),
+                         "slice_us_p99": round(float(np.percentile(sl, 99)), 1),
+                         "metapage_us_p50": round(float(np.percentile(mp, 50)), 2),
+                         "metapage_us_p99": round(float(np.percentile(mp, 99)), 2),
+                         "cpu_s_per_GiB": round(cpu_s / (total / GiB), 4),
+                         "process_cpu_s_per_GiB": round(run_scan_ops.last_process_cpu_s / (total / GiB), 4),
+                         "crc_ok": ok, "rc": rc}
+        res["threads"][str(nt)] = per
+    # one thread's per-call latency by size (the cutoff): median of `n` calls
+    sweep = {}
+    for size in (4096, 16384, 65536, 262144, 1 << 20, 4 << 20, 16 << 20):
+        row = {}
+        for mode in ("cpu", "gpu"):
+            n = 64 if size >= (4 << 20) else 200
+            run_scan_ops(bufs[:1], [4096], [size], 4, mode)
+            rc, lat, crcs, _, cpu_s = run_scan_ops(bufs[:1], [4096], [size], n, mode)
+            row[mode + "_us_p50"] = round(float(np.median(lat)), 2) if rc == 0 else None
+            row[mode + "_thread_cpu_us_per_call"] = round(cpu_s / n * 1e6, 2)
+            row[mode + "_process_cpu_us_per_call"] = round(run_scan_ops.last_process_cpu_s / n * 1e6, 2)
+            row[mode + "_crc"] = int(crcs[0, 0])
+        row["crc_ok"] = row.pop("cpu_crc") == row.pop("gpu_crc")
+        sweep[str(size)] = row
+    res["latency_by_size_1thread"] = sweep
+    faster = [int(k) for k, r in sweep.items() if r["gpu_us_p50"] and r["gpu_us_p50"] < r["cpu_us_p50"]]
+    res["gpu_faster_per_call_from_bytes"] = min(faster) if faster else None
+    cheaper = [int(k) for k, r in sweep.items()
+               if r["gpu_process_cpu_us_per_call"] < r["cpu_process_cpu_us_per_call"]]
+    res["gpu_cheaper_in_process_cpu_from_bytes"] = min(cheaper) if cheaper else None
+    # the reference's own buffer kind: `new char[size]` (pageable), 10 threads
+    pg = [np.random.default_rng(t).integers(0, 256, file_bytes, dtype=np.uint8) for t in range(T)]
+    run_scan_ops(pg, offs, lens, 2 * len(offs), "gpu")
+    rc, lat, _, wall, cpu_s = run_scan_ops(pg, offs, lens, calls, "gpu")
+    total = float(op_bytes.sum()) * T
+    res["pageable_gpu"] = {"threads": T, "agg_GiBps": round(total / GiB / wall, 2),
+                           "slice_us_p50": round(float(np.percentile(lat[:, op_bytes == (4 << 20)], 50)), 1),
+                           "cpu_s_per_GiB": round(cpu_s / (total / GiB), 4),
+                           "process_cpu_s_per_GiB": round(run_scan_ops.last_process_cpu_s / (total / GiB), 4),
+                           "rc": rc}
+    res["path"] = ("curve_amd/host/scan_op_bench.cpp sob_run: native threads; gpu = cc_page_crc_host (a lane of its "
+                   "own per concurrent caller: engine.hip page_crc_lane) + cc_fold_host")
+    return res
 
 
 def _stream_sources(n, pool_n, rank=0):
@@ -533,7 +663,14 @@ def partial_write_leg(pool, args):
     delta_ok = int(cnt[0]) == 0
     nb = len(dev_ms)
     ms = float(np.mean(dev_ms))
-    alg = (2 * upd_bytes + touched * (4096 + 4)) / nb
+    # update bytes read + 4096 read and 4 written per touched page
+    # (covered rows come from the source, not the page, so an update byte is
+    # read once).  moved_2u: the round-5 figure, every update byte counted twice
+    alg = (upd_bytes + touched * (4096 + 4)) / nb
+    moved_2u = (2 * upd_bytes + touched * (4096 + 4)) / nb
+
+    def frac(b, t_ms):
+        return round(b / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     return {"updates_per_batch": U, "batches": nb,
             "device_ms_per_batch": round(ms, 4),
             "ms_median": round(float(np.median(dev_ms)), 4),
@@ -541,12 +678,15 @@ def partial_write_leg(pool, args):
             "updates_per_s": round(U / (ms * 1e-3), 1),
             "touched_pages_per_batch": touched // nb,
             "alg_GBps": round(alg / (ms * 1e-3) / 1e9, 1),
-            "alg_frac_of_hbm_peak": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "alg_frac_of_hbm_peak": frac(alg, ms),
+            "moved_frac_2u": frac(moved_2u, ms),
+            "alg_bytes_per_batch": int(alg),
             "wall_ms_incl_log_upload": round(float(np.mean(walls)) * 1e3, 3),
             "frac_of_random_probe": round(probe_ms / ms, 4),
             "delta": {"device_ms_per_batch": round(delta_ms, 4),
                       "updates_per_s": round(U / (delta_ms * 1e-3), 1),
-                      "alg_frac_of_hbm_peak": round(alg / (delta_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "alg_frac_of_hbm_peak": frac(alg, delta_ms),
+                      "moved_frac_2u": frac(moved_2u, delta_ms),
                       "frac_of_random_probe": round(probe_ms / delta_ms, 4),
                       "queue_device_ms_per_batch": round(delta_q_ms, 4),
                       "queue_frac_of_random_probe": round(probe_ms / delta_q_ms, 4),
@@ -555,20 +695,23 @@ def partial_write_leg(pool, args):
             "queue": {"batches_per_call": len(qb), "device_ms_per_batch": round(q_ms, 4),
                       "ms_each": [round(x, 4) for x in q_each],
                       "updates_per_s": round(U / (q_ms * 1e-3), 1),
-                      "alg_frac_of_hbm_peak": round(alg / (q_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "alg_frac_of_hbm_peak": frac(alg, q_ms),
+                      "moved_frac_2u": frac(moved_2u, q_ms),
                       "frac_of_random_probe": round(probe_ms / q_ms, 4),
                       "path": "cc_apply_logs_dev: the batches as one queue; each batch's page kernel also groups "
                               "the next batch in its tail (one grouping launch a queue instead of one a batch)"},
             "random_probe": {"ms_per_batch": round(probe_ms, 4), "ms_median": round(float(np.median(probe_each)), 4),
                              "ms_each": [round(x, 4) for x in probe_each],
                              "pages_per_batch": int(np.mean([d.size for d in descs])),
-                             "alg_frac_of_hbm_peak": round(alg / (probe_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "alg_frac_of_hbm_peak": frac(alg, probe_ms),
+                             "moved_frac_2u": frac(moved_2u, probe_ms),
                              "moved_GBps": round(probe_moved / (probe_ms * 1e-3) / 1e9, 1),
                              "path": "cc_apply_log_probe_dev: the same touched pages read (covered rows from the "
                                      "source) and their dirty rows stored nt, write-log page-pass grid, no table, "
                                      "no CRC -- the ceiling of this access pattern"},
             "path": "cc_apply_log_dev: pieces grouped by page in a device hash table (one CAS per piece, no sort) + one wave per touched page",
-            "note": "alg bytes = 2*update bytes + 4100*touched pages; log + data resident in HBM"}
+            "note": "alg bytes (SURVEY 8d) = update bytes + 4100 x touched pages; moved_frac_2u = (2 x update "
+                    "bytes + 4100 x touched pages) / t / 8 TB/s, the round-5 accounting; log + data resident in HBM"}
 
 
 def read_verify_leg(pool, args):
@@ -892,6 +1035,16 @@ def main():
     for a, b in ev:
         a.record(stream)
         b.record(stream)
+    # and one around each timed step's digest exchange at N > 1: HIP events
+    # recorded inside the native call around the all-gather + XOR fold, or the
+    # host wall of the torch.distributed exchange (reduce_digests; the step's
+    # kernels drained first, so only the exchange is inside it)
+    xev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)] if world > 1 else []
+    for a, b in xev:
+        a.record(stream)
+        b.record(stream)
+    x_host_ms = [0.0] * args.steps
 
     # failure injection (the reference's libfiu failpoints play this role): the
     # rank named here stops participating in the digest exchange after init, as
@@ -904,9 +1057,16 @@ def main():
         # ONE C call: page CRCs + metapage CRCs + fused epilogue (slice CRCs,
         # file CRCs, digest partials) + the RCCL digest exchange (cc_pool_scan_dev)
         pool_scan(pool, after_mult, group, digest, comm=None if skip_exchange else comm, stream=stream,
-                  events=ev[k] if k is not None else None)
+                  events=ev[k] if k is not None else None,
+                  exchange_events=xev[k] if (k is not None and xev) else None)
         if world > 1 and comm is None and not skip_exchange:
+            if k is not None:
+                stream.synchronize()
+                t0 = time.perf_counter()
             full_digest[0] = reduce_digests(digest, dist)
+            if k is not None:
+                stream.synchronize()
+                x_host_ms[k] = (time.perf_counter() - t0) * 1e3
 
     def sync():
         # the steps' exchanges complete, or the run ends: cc_comm_wait polls the
@@ -1087,8 +1247,27 @@ def main():
     out["digest_check_cpu"] = cpu_digest
     out["numa_binding_rank0"] = numa
     if world > 1:
+        if comm is not None:
+            x_each = [a.elapsed_time(b) for a, b in xev]
+            x_how = "HIP events on the step stream around the all-gather + XOR fold inside cc_pool_scan_dev"
+        else:
+            x_each = x_host_ms
+            x_how = ("host wall of reduce_digests (torch.distributed all_gather + device XOR fold), the step's "
+                     "kernels drained before it")
+        x_ms = float(np.mean(x_each))
+        # every rank's mean exchange time (the slowest rank's sets the step)
+        xt = torch.tensor([x_ms], dtype=torch.float64, device="cpu" if backend == "gloo" else dev)
+        xg = torch.empty(world, dtype=torch.float64, device=xt.device)
+        dist.all_gather_into_tensor(xg, xt)
+        rank_x = [float(v) for v in xg.cpu().tolist()]
+        step_ms = el / args.steps * 1e3
         out["digest_exchange"] = {"path": comm_note, "matches_torch_distributed": digest_check,
-                                  "matches_cpu_chain": cpu_digest["ok"]}
+                                  "matches_cpu_chain": cpu_digest["ok"],
+                                  "ms_each": [round(x, 4) for x in x_each], "ms_avg": round(x_ms, 4),
+                                  "share_of_step": round(x_ms / step_ms, 4),
+                                  "rank_ms_avg": [round(x, 4) for x in rank_x],
+                                  "share_of_step_max_rank": round(max(rank_x) / step_ms, 4),
+                                  "timing": x_how}
         # aggregate roofline over the node: every rank's algorithmic bytes over the
         # slowest rank's page-kernel time, against N x the per-GPU peak
         agg = world * launch_pages * ALG_BYTES_PER_PAGE / (max(rank_kern) * 1e-3) / 1e9
@@ -1122,6 +1301,11 @@ def main():
                 out["stream"] = {"error": repr(e)}
         if args.file_chunks:
             out["files"] = files_leg(args)
+        if args.scan_op_threads:
+            try:
+                out["scan_op"] = scan_op_leg(args)
+            except Exception as e:  # report, never lose the main line
+                out["scan_op"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:

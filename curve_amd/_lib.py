@@ -83,7 +83,7 @@ class CcPoolShard(ctypes.Structure):  # include/curve_crc.h cc_pool_shard
                 ("meta_bytes", _u32), ("page_bytes", _u32), ("slice_bytes", _u32), ("d_after_mult", _vp),
                 ("d_group", _vp), ("n_groups", _u64), ("d_page_crcs", _vp), ("d_meta_crcs", _vp),
                 ("d_slice_crcs", _vp), ("d_file_crcs", _vp), ("d_digest", _vp), ("ev_pages_begin", _vp),
-                ("ev_pages_end", _vp)]
+                ("ev_pages_end", _vp), ("ev_exchange_begin", _vp), ("ev_exchange_end", _vp)]
 
 
 SIGNATURES = {
@@ -203,7 +203,7 @@ def _one_hip_runtime():
     libcurvecrc's libamdhip64.so.7 resolves to the runtime already loaded."""
     try:
         import torch  # noqa: F401
-    except ImportError:
+    except Exception:  # absent, or a broken install (OSError / RuntimeError at import): the plain load order
         pass
 
 

@@ -6,8 +6,10 @@
 // mutex and then reached through a lock-free shared_ptr load, so *_dev calls
 // take no lock (they only enqueue).  Every call holds its own reference to the
 // context: cc_engine_fini unpublishes the contexts and the last call still
-// using one frees it.  The blocking *_host calls serialise on a per-device
-// submission lock.
+// using one frees it.  A blocking cc_page_crc_host call of at most 16 MiB runs
+// on a lane of its own (device buffer, stream, completion signal), so
+// concurrent callers overlap; the other blocking *_host calls, and larger page
+// calls, serialise on a per-device submission lock over two shared staging slots.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -95,6 +97,35 @@ struct Staging {
     hipEvent_t aux_ready = nullptr;
 };
 
+// Per-caller lanes of the blocking page call (cc_page_crc_host) at the scan
+// op's call shape: one 4 MiB slice or the 4 KiB metapage per raft-applied op
+// (ScanChunkRequest::OnApply, op_request.cpp:776-794), from up to
+// wconcurrentapply.size = 10 apply threads at once (conf/chunkserver.conf:183,
+// op_request.cpp:179-187).  A call of at most kLaneBytes takes a lane of its
+// own -- device buffer, CRC buffers, stream, completion signal -- so concurrent
+// callers overlap their H2D, kernel and D2H instead of queueing one whole call
+// after another on the two shared staging slots.  Lanes are made on first
+// demand (up to kMaxLanes) and reused; a caller finding none idle waits for one.
+constexpr uint64_t kLaneBytes = 16ull << 20;
+constexpr size_t kMaxLanes = 16;
+constexpr uint64_t kLanePiece = 1ull << 20;  // pageable input: memcpy a piece, its DMA runs behind the next
+struct Lane {
+    void* dev = nullptr;        // kLaneBytes
+    uint32_t* dcrc = nullptr;   // kLaneBytes / 256 CRCs (256-byte pages at most)
+    uint32_t* hcrc = nullptr;   // pinned, as many
+    void* host = nullptr;       // pinned staging for pageable input, made on the first such call
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    SlotSignal sig;
+};
+struct LanePool {
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<Lane*> idle;
+    std::vector<std::unique_ptr<Lane>> all;
+    size_t making = 0;  // lanes being created outside the lock
+};
+
 // Product tables of the fused epilogue, one per (page_bytes, q): a small
 // lock-free cache (lookups from concurrent *_dev calls take no lock; the rare
 // insert takes the context's table mutex).
@@ -169,6 +200,7 @@ struct DevCtx : std::enable_shared_from_this<DevCtx> {
     std::mutex range_mu;
     std::vector<RangeWork> range_works;
     ReaderPool readers;  // cc_scan_files' io threads
+    LanePool lanes;      // cc_page_crc_host's per-caller lanes
     DevCtx() {
         for (int i = 0; i < kEpiSlots; i++) {
             epi_key[i].store(0);
@@ -182,8 +214,12 @@ using CtxRef = std::shared_ptr<DevCtx>;
 
 // A thread's hipStreamPerThread entries, dropped when the thread exits: taken
 // out of the context's lists under their mutexes (no call can reach them after
-// that), then freed once the exiting thread's own per-thread stream -- the
-// only stream that used them -- has drained.  No lock is held while waiting.
+// that), then handed to hipFreeAsync on the exiting thread's own per-thread
+// stream -- the only stream that used them -- so the memory goes back once
+// that stream's work is done.  Nothing here waits: a device-synchronising call
+// (hipFree, a stream sync) in a thread-exit destructor would make the exit,
+// and any join() on it, wait for every stream of the device, including a
+// collective stuck on a lost peer.  No lock is held while enqueueing.
 void drop_thread_entries(DevCtx* c, std::thread::id tid) {
     StreamKey key;
     key.s = hipStreamPerThread;
@@ -206,10 +242,8 @@ void drop_thread_entries(DevCtx* c, std::thread::id tid) {
     if (dead.empty()) return;
     int cur = -1;
     (void)hipGetDevice(&cur);
-    if (hipSetDevice(c->device) == hipSuccess) {
-        (void)hipStreamSynchronize(hipStreamPerThread);
-        for (void* p : dead) (void)hipFree(p);
-    }
+    if (hipSetDevice(c->device) == hipSuccess)
+        for (void* p : dead) (void)hipFreeAsync(p, hipStreamPerThread);  // stream-ordered: after the thread's work
     if (cur >= 0) (void)hipSetDevice(cur);
 }
 
@@ -276,6 +310,20 @@ void staging_free(Staging& st) {
     st.bytes = 0;
 }
 
+void lane_free(Lane* l) {
+    if (l->stream) (void)hipStreamSynchronize(l->stream);
+    if (l->dev) (void)hipFree(l->dev);
+    if (l->dcrc) (void)hipFree(l->dcrc);
+    if (l->hcrc) (void)hipHostFree(l->hcrc);
+    if (l->host) (void)hipHostFree(l->host);
+    if (l->stream) (void)hipStreamDestroy(l->stream);
+    if (l->done) (void)hipEventDestroy(l->done);
+    l->dev = l->host = nullptr;
+    l->dcrc = l->hcrc = nullptr;
+    l->stream = nullptr;
+    l->done = nullptr;
+}
+
 // Runs when the last reference drops (cc_engine_fini, or the last call still
 // holding the context after it): nothing can be enqueued on it any more, so
 // finish whatever was enqueued and free on the context's own device.
@@ -288,9 +336,10 @@ DevCtx::~DevCtx() {
         if (image) (void)hipFree(image);
         for (int i = 0; i < kEpiSlots; i++)
             if (void* p = epi_ptr[i].load()) (void)hipFree(p);
-        for (auto& t : tails) (void)hipFree(t.p);
+        for (auto& t : tails) (void)hipFreeAsync(t.p, nullptr);
         for (auto& t : log_tabs) (void)hipFreeAsync(t.p, nullptr);
         for (auto& t : range_works) (void)hipFreeAsync(t.p, nullptr);
+        for (auto& l : lanes.all) lane_free(l.get());
         (void)hipDeviceSynchronize();
     }
     if (cur >= 0) (void)hipSetDevice(cur);
@@ -318,6 +367,10 @@ int get_ctx(CtxRef* out) {
     hipError_t e = hipGetDeviceProperties(&prop, dev);
     if (e != hipSuccess) return map_err(e);
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    // test hook: $CC_TEST_CUS sizes every grid as if the device had that many
+    // CUs (e.g. a 304-CU part's grids on this 256-CU one); never needed in use
+    if (const char* v = getenv("CC_TEST_CUS"))
+        if (atoi(v) > 0 && atoi(v) <= 4096) c->cus = atoi(v);
     std::vector<uint32_t> img(kLdsBytes / 4);
     build_lds_image(img.data());
     // device image: the LDS image, then for t < kXinvEntries the 32 products
@@ -396,10 +449,10 @@ DevCtx::TailBlock* tail_block(DevCtx* c, hipStream_t s) {
             return &t;
         }
     if (c->tails.size() >= kMaxTailBlocks) return nullptr;
-    void* p = nullptr;
-    if (hipMalloc(&p, kTailBlockBytes) != hipSuccess) return nullptr;
+    void* p = nullptr;  // stream-ordered, like every per-stream entry (freed by hipFreeAsync)
+    if (hipMallocAsync(&p, kTailBlockBytes, s) != hipSuccess) return nullptr;
     if (hipMemsetAsync(p, 0, kTailBlockBytes, s) != hipSuccess) {
-        (void)hipFree(p);
+        (void)hipFreeAsync(p, s);
         return nullptr;
     }
     c->tails.push_back({key, static_cast<unsigned long long*>(p), 0u, false});
@@ -480,10 +533,9 @@ void fire_slot(void* p) {
     sg->cv.notify_all();
 }
 
-hipError_t arm_slot(Staging& st, int slot, hipStream_t s) {
-    hipError_t e = hipEventRecord(st.done[slot], s);
+hipError_t arm_signal(SlotSignal& sg, hipEvent_t done, hipStream_t s) {
+    hipError_t e = hipEventRecord(done, s);
     if (e != hipSuccess) return e;
-    SlotSignal& sg = st.sig[slot];
     {
         std::lock_guard<std::mutex> lk(sg.m);
         sg.fired = false;
@@ -496,13 +548,63 @@ hipError_t arm_slot(Staging& st, int slot, hipStream_t s) {
     return e;
 }
 
-hipError_t park_slot(Staging& st, int slot) {
-    SlotSignal& sg = st.sig[slot];
+hipError_t park_signal(SlotSignal& sg, hipEvent_t done) {
     {
         std::unique_lock<std::mutex> lk(sg.m);
         sg.cv.wait(lk, [&] { return sg.fired; });
     }
-    return hipEventSynchronize(st.done[slot]);  // already complete: returns its status
+    return hipEventSynchronize(done);  // already complete: returns its status
+}
+
+hipError_t arm_slot(Staging& st, int slot, hipStream_t s) { return arm_signal(st.sig[slot], st.done[slot], s); }
+hipError_t park_slot(Staging& st, int slot) { return park_signal(st.sig[slot], st.done[slot]); }
+
+int lane_make(Lane* l) {
+    hipError_t e;
+    if ((e = hipMalloc(&l->dev, kLaneBytes)) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void**>(&l->dcrc), kLaneBytes / 256 * 4)) != hipSuccess ||
+        (e = hipHostMalloc(reinterpret_cast<void**>(&l->hcrc), kLaneBytes / 256 * 4, hipHostMallocDefault)) !=
+            hipSuccess ||
+        (e = hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&l->done, hipEventDisableTiming)) != hipSuccess)
+        return map_err(e);
+    return CC_OK;
+}
+
+// An idle lane of the device, made if fewer than kMaxLanes exist, else the
+// next one released (the caller sleeps).  nullptr + *rc on an allocation failure.
+Lane* lane_get(DevCtx* c, int* rc) {
+    LanePool& lp = c->lanes;
+    std::unique_lock<std::mutex> lk(lp.m);
+    while (lp.idle.empty() && lp.all.size() + lp.making >= kMaxLanes) lp.cv.wait(lk);
+    if (!lp.idle.empty()) {
+        Lane* l = lp.idle.back();
+        lp.idle.pop_back();
+        return l;
+    }
+    lp.making++;
+    lk.unlock();
+    auto l = std::make_unique<Lane>();
+    const int r = lane_make(l.get());
+    if (r) lane_free(l.get());
+    lk.lock();
+    lp.making--;
+    if (r) {
+        lk.unlock();
+        lp.cv.notify_one();  // a waiter may make it instead
+        *rc = r;
+        return nullptr;
+    }
+    lp.all.push_back(std::move(l));
+    return lp.all.back().get();
+}
+
+void lane_put(DevCtx* c, Lane* l) {
+    {
+        std::lock_guard<std::mutex> lk(c->lanes.m);
+        c->lanes.idle.push_back(l);
+    }
+    c->lanes.cv.notify_one();
 }
 
 bool is_pinned(const void* p) {
@@ -1155,10 +1257,60 @@ int cc_digest_fold_dev(const uint32_t* d_gathered, uint32_t nranks, uint64_t n, 
     return map_err(launch_xor_fold(d_gathered, nranks, n, d_digest, static_cast<hipStream_t>(stream)));
 }
 
-// Host in / host out.  Two-slot pipeline: while slot i's pages are copied in
-// and hashed on stream i, the CPU fills slot i^1 (pageable input) or -- when
-// the caller's buffer is already pinned (chunk files pread into pinned memory)
-// -- the DMA reads it directly.
+namespace cc {
+namespace {
+// One call on a lane of its own (LanePool): H2D (straight from the caller's
+// buffer when it is pinned, else through the lane's pinned staging a piece at
+// a time, each piece's DMA running while the next is copied), the page kernel,
+// D2H of the CRCs, and the caller parked until the lane's stream is done.  The
+// lane goes back idle only with its stream drained.
+int page_crc_lane(DevCtx* c, const void* h_pages, uint64_t n_pages, uint32_t page_bytes, uint32_t* h_out) {
+    int rc = CC_OK;
+    Lane* l = lane_get(c, &rc);
+    if (!l) return rc;
+    const uint64_t bytes = n_pages * page_bytes;
+    hipError_t e = hipSuccess;
+    if (is_pinned(h_pages)) {
+        e = hipMemcpyAsync(l->dev, h_pages, bytes, hipMemcpyHostToDevice, l->stream);
+    } else {
+        if (!l->host) e = hipHostMalloc(&l->host, kLaneBytes, hipHostMallocDefault);
+        for (uint64_t o = 0; e == hipSuccess && o < bytes; o += kLanePiece) {
+            const uint64_t k = bytes - o < kLanePiece ? bytes - o : kLanePiece;
+            memcpy(static_cast<unsigned char*>(l->host) + o, static_cast<const unsigned char*>(h_pages) + o, k);
+            e = hipMemcpyAsync(static_cast<unsigned char*>(l->dev) + o, static_cast<unsigned char*>(l->host) + o, k,
+                               hipMemcpyHostToDevice, l->stream);
+        }
+    }
+    if (e == hipSuccess) {
+        PageLaunch a = {};
+        a.pages = static_cast<const uint32_t*>(l->dev);
+        a.n_pages = n_pages;
+        a.words_per_lane = page_bytes / kWaveBytes;
+        a.image = c->image;
+        a.kconst = kconst_for(page_bytes);
+        a.out = l->dcrc;
+        geometry_for(c, n_pages, &a);
+        e = launch_page_crc(a, l->stream);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(l->hcrc, l->dcrc, n_pages * 4, hipMemcpyDeviceToHost, l->stream);
+    if (e == hipSuccess) e = arm_signal(l->sig, l->done, l->stream);
+    if (e == hipSuccess)
+        e = park_signal(l->sig, l->done);
+    else
+        (void)hipStreamSynchronize(l->stream);  // whatever was enqueued finishes before the lane is reused
+    if (e == hipSuccess) memcpy(h_out, l->hcrc, n_pages * 4);
+    lane_put(c, l);
+    return map_err(e);
+}
+}  // namespace
+}  // namespace cc
+
+// Host in / host out.  A call of at most kLaneBytes runs on a lane of its own
+// (page_crc_lane: concurrent callers overlap).  A larger one takes the
+// device's two shared staging slots (held for the whole call): while slot i's
+// pages are copied in and hashed on stream i, the CPU fills slot i^1 (pageable
+// input) or -- when the caller's buffer is already pinned (chunk files pread
+// into pinned memory) -- the DMA reads it directly.
 int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes, uint32_t* h_out) {
     if (!page_size_ok(page_bytes)) return CC_EINVAL;
     if (n_pages == 0) return CC_OK;
@@ -1166,6 +1318,7 @@ int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
     CtxRef c;
     int rc = get_ctx(&c);
     if (rc) return rc;
+    if (n_pages <= kLaneBytes / page_bytes) return page_crc_lane(c.get(), h_pages, n_pages, page_bytes, h_out);
     std::lock_guard<std::mutex> lk(c->submit);
     if ((rc = staging_init(c.get()))) return rc;
     Staging& st = c->st;
@@ -1552,11 +1705,15 @@ int cc_apply_logs_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, co
             // a workgroup may take up to twice its even share of the chunks, in
             // takes of kGroupTake
             const uint64_t chunks = (nb.n_pieces + T - 1) / T;
-            const uint32_t G = (uint32_t)a.blocks;
+            // the grouping writes one head segment per workgroup: at most
+            // kInsertBlocks of them, so a device with more CUs runs this page
+            // kernel on kInsertBlocks workgroups rather than lose the grouping
+            const uint32_t G = a.blocks < (int)kInsertBlocks ? (uint32_t)a.blocks : kInsertBlocks;
             uint64_t rounds = 2 * ((chunks + G - 1) / G);
             rounds = (rounds + kGroupTake - 1) / kGroupTake * kGroupTake;
             SegLayout nl = {G, (uint32_t)(rounds * T)};
-            if (G <= kInsertBlocks && rounds * T < (1ull << 32)) {
+            if (rounds * T < (1ull << 32)) {
+                a.blocks = (int)G;
                 unsigned char* q = w + (uint64_t)(r ^ 1) * W.region;
                 a.nx.upd = nb.upd;
                 a.nx.n_pieces = nb.n_pieces;

@@ -303,22 +303,27 @@ int cc_pool_scan_dev(const cc_pool_shard* p, cc_comm* comm, void* stream) {
     hipError_t e;
     if (p->n_chunks == 0) {  // an empty shard: zero partials (full digests after the exchange)
         if (dig && (e = hipMemsetAsync(p->d_digest, 0, p->n_groups * 4, s)) != hipSuccess) return map_hip(e);
-        return comm ? cc_digest_allreduce_dev(comm, p->d_digest, p->n_groups, stream) : CC_OK;
+    } else {
+        // readMetaPage ops (one "page" of meta_bytes per chunk; this launch also
+        // zeroes the digest partials and the next launch's tail counter), then the
+        // hot kernel over every data page of the shard, bracketed by the caller's events
+        if ((rc = cc::pool_page_launches(p->d_data, pages, p->page_bytes, p->d_page_crcs, p->d_meta, p->n_chunks,
+                                         p->meta_bytes, p->d_meta_crcs, dig ? p->d_digest : nullptr,
+                                         dig ? p->n_groups : 0, s, p->ev_pages_begin, p->ev_pages_end)))
+            return rc;
+        // slices + file CRCs + digest partials in one launch
+        if ((rc = cc_scan_epilogue_dev(p->d_page_crcs, p->d_meta_crcs, p->n_chunks, p->chunk_bytes / p->page_bytes,
+                                       p->page_bytes, p->slice_bytes / p->page_bytes, p->d_slice_crcs,
+                                       p->d_file_crcs, dig ? p->d_after_mult : nullptr, dig ? p->d_group : nullptr,
+                                       dig ? p->d_digest : nullptr, stream)))
+            return rc;
     }
-    // readMetaPage ops (one "page" of meta_bytes per chunk; this launch also
-    // zeroes the digest partials and the next launch's tail counter), then the
-    // hot kernel over every data page of the shard, bracketed by the caller's events
-    if ((rc = cc::pool_page_launches(p->d_data, pages, p->page_bytes, p->d_page_crcs, p->d_meta, p->n_chunks,
-                                     p->meta_bytes, p->d_meta_crcs, dig ? p->d_digest : nullptr,
-                                     dig ? p->n_groups : 0, s, p->ev_pages_begin, p->ev_pages_end)))
-        return rc;
-    // slices + file CRCs + digest partials in one launch
-    if ((rc = cc_scan_epilogue_dev(p->d_page_crcs, p->d_meta_crcs, p->n_chunks, p->chunk_bytes / p->page_bytes,
-                                   p->page_bytes, p->slice_bytes / p->page_bytes, p->d_slice_crcs, p->d_file_crcs,
-                                   dig ? p->d_after_mult : nullptr, dig ? p->d_group : nullptr,
-                                   dig ? p->d_digest : nullptr, stream)))
-        return rc;
-    if (comm) return cc_digest_allreduce_dev(comm, p->d_digest, p->n_groups, stream);
+    if (!comm) return CC_OK;
+    if (p->ev_exchange_begin && (e = hipEventRecord(static_cast<hipEvent_t>(p->ev_exchange_begin), s)) != hipSuccess)
+        return map_hip(e);
+    if ((rc = cc_digest_allreduce_dev(comm, p->d_digest, p->n_groups, stream))) return rc;
+    if (p->ev_exchange_end && (e = hipEventRecord(static_cast<hipEvent_t>(p->ev_exchange_end), s)) != hipSuccess)
+        return map_hip(e);
     return CC_OK;
 }
 

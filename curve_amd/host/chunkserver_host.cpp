@@ -79,6 +79,8 @@ bool ParseChunkName(const std::string& name, uint64_t* id) {
 
 }  // namespace
 
+bool ScanOpCrc(const char* buf, size_t size, uint32_t* crc) { return HashBuffer(buf, size, crc); }
+
 void ChunkFileMetaPage::encode(char* buf) const {
     size_t len = 0;
     auto put = [&](const void* p, size_t n) {

@@ -106,6 +106,14 @@ struct ScanMap {
 // Fewer than two follower maps: not consistent, nothing failed (logged only).
 bool CompareMap(const ScanMap& local, const std::vector<ScanMap>& followers, std::vector<ScanMap>* failed);
 
+// The CRC ScanChunkRequest::OnApply / OnApplyFromLog puts in ScanMap.crc for
+// one scan op's buffer (`crc = CRC32(readBuffer, size)`, op_request.cpp:794,
+// :847): the 4 MiB slice's pages on the GPU engine (cc_page_crc_host, a lane
+// of its own per concurrent caller) folded on the host, a buffer under
+// kCpuHashMax (the 4 KiB metapage op) on the CPU primitive.  Thread-safe; false
+// when the engine call fails (the apply thread's InternalError, :813-815).
+bool ScanOpCrc(const char* buf, size_t size, uint32_t* crc);
+
 // One scan job over a copyset's chunk files: for every chunk_<id> (ascending
 // id; snapshots are not in the ChunkMap) whose metapage is FORMAT_VERSION_V2,
 // the metapage op then chunkSize/scanSize data slices, each a ScanMap as

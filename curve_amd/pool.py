@@ -203,12 +203,14 @@ def agreed_comm(dist, device=None, group=None, timeout_ms: int = 0):
     return None, f"torch.distributed all_gather_into_tensor + cc_digest_fold_dev (native comm not agreed: {why})"
 
 
-def pool_scan(pool, after_mult, group, digest, comm: "Comm" = None, stream=None, events=None):
+def pool_scan(pool, after_mult, group, digest, comm: "Comm" = None, stream=None, events=None,
+              exchange_events=None):
     """One integrity scan pass over a DevicePool shard as ONE native call
     (cc_pool_scan_dev): page CRCs, metapage CRCs, slice/file CRCs, digest
     partials and -- with a Comm -- the RCCL digest exchange.  `events` =
     (begin, end) torch.cuda.Event pair recorded around the page kernel (they
-    must already exist: record each once beforehand)."""
+    must already exist: record each once beforehand); `exchange_events` the
+    same around the exchange (all-gather + XOR fold; recorded only with a Comm)."""
     import ctypes
     from . import _lib
     from .crc import _dev_ptr, _stream_handle
@@ -228,6 +230,8 @@ def pool_scan(pool, after_mult, group, digest, comm: "Comm" = None, stream=None,
     s.d_digest = _dev_ptr(digest, "digest").value if digest is not None else None
     if events is not None:
         s.ev_pages_begin, s.ev_pages_end = events[0].cuda_event, events[1].cuda_event
+    if exchange_events is not None:
+        s.ev_exchange_begin, s.ev_exchange_end = exchange_events[0].cuda_event, exchange_events[1].cuda_event
     _lib.check(_lib.lib().cc_pool_scan_dev(ctypes.byref(s), comm.handle if comm is not None else None,
                                            _stream_handle(stream)), "cc_pool_scan_dev")
     return digest

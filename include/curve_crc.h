@@ -224,10 +224,18 @@ int cc_digest_dev(const uint32_t* d_file_crcs, const uint64_t* d_after_bytes,
 int cc_digest_fold_dev(const uint32_t* d_gathered, uint32_t nranks, uint64_t n, uint32_t* d_digest, void* stream);
 
 /* ------------------------------------------------------------------------
- * Host-in / host-out convenience (blocking; thread-safe: one internal
- * submission lock + pinned staging ring per device).  Starts and ends in host
- * memory like the reference's datastore read path (chunkserver_chunkfile.cpp:497-536).
+ * Host-in / host-out convenience (blocking; thread-safe).  Starts and ends in
+ * host memory like the reference's datastore read path (chunkserver_chunkfile.cpp:497-536).
  * ------------------------------------------------------------------------ */
+/* h_out[i] = crc32c_value(h_pages + i*page_bytes, page_bytes).  A call of at
+ * most 16 MiB (the scan op's shape: one 4 MiB slice or the 4 KiB metapage per
+ * ScanChunkRequest, op_request.cpp:776-794, from up to wconcurrentapply.size =
+ * 10 apply threads) runs on a LANE of its own -- device buffer, stream,
+ * completion signal; up to 16 lanes per device, made on first demand, a caller
+ * finding none idle waits -- so concurrent callers overlap their copies and
+ * kernels.  A larger call takes the device's two-slot pinned staging ring,
+ * held for the whole call.  Pinned input is DMA'd directly; pageable input is
+ * copied through pinned staging.  The caller sleeps (no spin) until done. */
 int cc_page_crc_host(const void* h_pages, uint64_t n_pages, uint32_t page_bytes,
                      uint32_t* h_out);
 
@@ -474,6 +482,11 @@ typedef struct cc_pool_shard {
      * inside the one call */
     void* ev_pages_begin;
     void* ev_pages_end;
+    /* optional hipEvent_t recorded on `stream` right before the digest
+     * exchange's all-gather and right after its XOR fold (comm non-NULL only;
+     * NULL = none): the exchange's own share of a scan step at N > 1 */
+    void* ev_exchange_begin;
+    void* ev_exchange_end;
 } cc_pool_shard;
 
 /* One integrity scan pass over the shard: page CRCs of every data page and

@@ -226,7 +226,13 @@ def _bench_world8(tmp_path, log_name, extra_env=None):
     want_agg = world * roof["alg_bytes_per_launch"] / (max(roof["rank_kernel_ms"]) * 1e-3) / 1e9
     assert abs(roof["aggregate_achieved"] - want_agg) <= 0.2 + 1e-3 * want_agg
     assert d["digest_check_cpu"]["ok"] is True
-    assert d["digest_exchange"]["matches_cpu_chain"] is True
+    ex = d["digest_exchange"]
+    assert ex["matches_cpu_chain"] is True
+    # the exchange's own time per timed step and its share of the step
+    assert len(ex["ms_each"]) == 3 and all(x > 0 for x in ex["ms_each"]), ex
+    assert len(ex["rank_ms_avg"]) == world and all(x > 0 for x in ex["rank_ms_avg"]), ex
+    assert 0 < ex["share_of_step"] <= ex["share_of_step_max_rank"] + 1e-9, ex
+    assert ex["share_of_step_max_rank"] < 1.5, ex  # an exchange inside the step (host wall may include some slack)
     sa = d["stream_all_ranks"]
     assert sa.get("digest_check_ok") is True and sa["ranks"] == world, sa
     # every chunk of the whole pool in exactly one rank's shard, in rank order
@@ -271,9 +277,15 @@ def test_bench_world8_native_exchange_over_stub_rccl(tmp_path):
         pytest.skip("no GPU")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     stub = os.path.join(root, "build", "stub", "libcurvecrc_stubrccl.so")
-    assert os.path.exists(stub), "make -C curve_amd/csrc (builds the stub too; __graft_entry__.build())"
     main_lib = os.path.join(root, "curve_amd", "libcurvecrc.so")
-    assert os.path.getmtime(stub) >= os.path.getmtime(main_lib) - 1, "stub build older than libcurvecrc.so: make"
+    if not os.path.exists(stub) or os.path.getmtime(stub) < os.path.getmtime(main_lib) - 1:
+        # missing or older than the library: build it now (make stubrccl; a test
+        # build kept out of the product's default target)
+        import subprocess
+        r = subprocess.run(["make", "-s", "-C", os.path.join(root, "curve_amd", "csrc"), "stubrccl"],
+                           capture_output=True, text=True)
+        if r.returncode or not os.path.exists(stub):
+            pytest.skip("stub-RCCL test build unavailable: " + (r.stderr or r.stdout)[-500:])
     import glob
     before = set(glob.glob("/dev/shm/ccrcclstub-*"))
     try:

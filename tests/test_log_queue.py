@@ -122,6 +122,26 @@ def test_log_queue_large_batches(dev, oracle):
     _run(dev, oracle, [65536] * 4, 4096, 4096, False, seed=4242, pool_bytes=256 << 20)
 
 
+@pytest.mark.timeout(300)
+def test_log_queue_grid_wider_than_insert_blocks(dev):
+    """A device with more CUs than kInsertBlocks (256; e.g. a 304-CU part):
+    the page kernel of a batch whose successor it groups runs on kInsertBlocks
+    workgroups (one head segment each) instead of skipping the grouping.  The
+    large-batch cases run again in a child process whose engine sizes every
+    grid for 304 CUs ($CC_TEST_CUS, read when the device context is made)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CC_TEST_CUS="304")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                        os.path.join(root, "tests", "test_log_queue.py") + "::test_log_queue_large_batches",
+                        os.path.join(root, "tests", "test_log_queue.py") + "::test_log_queue_hot_pages"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert "3 passed" in r.stdout, r.stdout[-2000:]
+
+
 def test_log_queue_arguments(dev):
     """Validation before anything is enqueued: a batch with records but no
     pointers, a misaligned source, too small a work buffer."""
