@@ -19,6 +19,7 @@
 #include <fcntl.h>
 #include <sched.h>
 #include <stdio.h>
+#include <sys/prctl.h>
 #include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
@@ -111,19 +112,19 @@ constexpr size_t kMaxLanes = 16;
 constexpr uint64_t kLanePiece = 1ull << 20;  // pageable input: memcpy a piece, its DMA runs behind the next
 struct Lane {
     void* dev = nullptr;        // kLaneBytes
-    uint32_t* dcrc = nullptr;   // kLaneBytes / 256 CRCs (256-byte pages at most)
-    uint32_t* hcrc = nullptr;   // pinned, as many
+    uint32_t* hcrc = nullptr;   // pinned: the page kernel stores the CRCs here directly (kLaneBytes / 256 of them)
     void* host = nullptr;       // pinned staging for pageable input, made on the first such call
+    uint32_t* hflag = nullptr;  // pinned completion word, written by the lane's stream after the kernel
+    uint32_t seq = 0;           // the last value asked of hflag
     hipStream_t stream = nullptr;
-    hipEvent_t done = nullptr;
-    SlotSignal sig;
 };
 struct LanePool {
     std::mutex m;
     std::condition_variable cv;
     std::vector<Lane*> idle;
     std::vector<std::unique_ptr<Lane>> all;
-    size_t making = 0;  // lanes being created outside the lock
+    size_t making = 0;                       // lanes being created outside the lock
+    std::atomic<uint64_t> inflight{0};       // bytes the lanes have enqueued and not yet seen complete
 };
 
 // Product tables of the fused epilogue, one per (page_bytes, q): a small
@@ -313,15 +314,13 @@ void staging_free(Staging& st) {
 void lane_free(Lane* l) {
     if (l->stream) (void)hipStreamSynchronize(l->stream);
     if (l->dev) (void)hipFree(l->dev);
-    if (l->dcrc) (void)hipFree(l->dcrc);
     if (l->hcrc) (void)hipHostFree(l->hcrc);
     if (l->host) (void)hipHostFree(l->host);
+    if (l->hflag) (void)hipHostFree(l->hflag);
     if (l->stream) (void)hipStreamDestroy(l->stream);
-    if (l->done) (void)hipEventDestroy(l->done);
     l->dev = l->host = nullptr;
-    l->dcrc = l->hcrc = nullptr;
+    l->hcrc = l->hflag = nullptr;
     l->stream = nullptr;
-    l->done = nullptr;
 }
 
 // Runs when the last reference drops (cc_engine_fini, or the last call still
@@ -562,13 +561,46 @@ hipError_t park_slot(Staging& st, int slot) { return park_signal(st.sig[slot], s
 int lane_make(Lane* l) {
     hipError_t e;
     if ((e = hipMalloc(&l->dev, kLaneBytes)) != hipSuccess ||
-        (e = hipMalloc(reinterpret_cast<void**>(&l->dcrc), kLaneBytes / 256 * 4)) != hipSuccess ||
         (e = hipHostMalloc(reinterpret_cast<void**>(&l->hcrc), kLaneBytes / 256 * 4, hipHostMallocDefault)) !=
             hipSuccess ||
-        (e = hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&l->done, hipEventDisableTiming)) != hipSuccess)
+        (e = hipHostMalloc(reinterpret_cast<void**>(&l->hflag), 256, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking)) != hipSuccess)
         return map_err(e);
+    __atomic_store_n(l->hflag, 0u, __ATOMIC_RELEASE);
     return CC_OK;
+}
+
+// Wait for the lane's completion word to reach `want`, sleeping, never
+// spinning and never in a HIP wait: hipStreamSynchronize / a blocking-sync
+// event spin the caller for the whole call, and a host function keeps a HIP
+// runtime thread busy while it is pending (process CPU ~= call time either
+// way: profiles/lane_wait_ab_r06.jsonl).  The caller sleeps ~80 % of the
+// expected time -- its bytes plus those the other lanes had enqueued, at
+// ~50 GB/s of H2D -- then polls with a growing sleep (2 .. 32 us) under a 1 us
+// timer slack (the default 50 us slack would add ~50 us to a 4 KiB call), the
+// thread's own slack restored on the way out.  A stream error ends the wait.
+hipError_t lane_wait(Lane* l, uint32_t want, uint64_t ahead_bytes) {
+    const int old = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+    (void)prctl(PR_SET_TIMERSLACK, 1000ul, 0, 0, 0);
+    const uint64_t est_ns = 15000 + ahead_bytes / 50;  // 15 us + bytes at 50 GB/s
+    timespec ts = {(time_t)(est_ns * 8 / 10 / 1000000000ull), (long)(est_ns * 8 / 10 % 1000000000ull)};
+    nanosleep(&ts, nullptr);
+    hipError_t r = hipSuccess;
+    long nap = 2000;
+    for (uint32_t k = 0; __atomic_load_n(l->hflag, __ATOMIC_ACQUIRE) != want; k++) {
+        if ((k & 15u) == 15u) {
+            const hipError_t q = hipStreamQuery(l->stream);
+            if (q != hipSuccess && q != hipErrorNotReady) {
+                r = q;
+                break;
+            }
+        }
+        timespec t2 = {0, nap};
+        nanosleep(&t2, nullptr);
+        if (nap < 32000) nap *= 2;
+    }
+    if (old > 0) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)old, 0, 0, 0);
+    return r;
 }
 
 // An idle lane of the device, made if fewer than kMaxLanes exist, else the
@@ -1261,14 +1293,16 @@ namespace cc {
 namespace {
 // One call on a lane of its own (LanePool): H2D (straight from the caller's
 // buffer when it is pinned, else through the lane's pinned staging a piece at
-// a time, each piece's DMA running while the next is copied), the page kernel,
-// D2H of the CRCs, and the caller parked until the lane's stream is done.  The
-// lane goes back idle only with its stream drained.
+// a time, each piece's DMA running while the next is copied), the page kernel
+// storing the CRCs straight into the lane's pinned CRC buffer (no D2H copy),
+// then a stream write of the lane's completion word, which the caller sleeps
+// on (lane_wait).  The lane goes back idle only with its stream drained.
 int page_crc_lane(DevCtx* c, const void* h_pages, uint64_t n_pages, uint32_t page_bytes, uint32_t* h_out) {
     int rc = CC_OK;
     Lane* l = lane_get(c, &rc);
     if (!l) return rc;
     const uint64_t bytes = n_pages * page_bytes;
+    const uint64_t ahead = c->lanes.inflight.fetch_add(bytes) + bytes;
     hipError_t e = hipSuccess;
     if (is_pinned(h_pages)) {
         e = hipMemcpyAsync(l->dev, h_pages, bytes, hipMemcpyHostToDevice, l->stream);
@@ -1288,16 +1322,17 @@ int page_crc_lane(DevCtx* c, const void* h_pages, uint64_t n_pages, uint32_t pag
         a.words_per_lane = page_bytes / kWaveBytes;
         a.image = c->image;
         a.kconst = kconst_for(page_bytes);
-        a.out = l->dcrc;
+        a.out = l->hcrc;
         geometry_for(c, n_pages, &a);
         e = launch_page_crc(a, l->stream);
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(l->hcrc, l->dcrc, n_pages * 4, hipMemcpyDeviceToHost, l->stream);
-    if (e == hipSuccess) e = arm_signal(l->sig, l->done, l->stream);
+    const uint32_t want = ++l->seq;
+    if (e == hipSuccess) e = hipStreamWriteValue32(l->stream, l->hflag, want, 0);
     if (e == hipSuccess)
-        e = park_signal(l->sig, l->done);
+        e = lane_wait(l, want, ahead);
     else
         (void)hipStreamSynchronize(l->stream);  // whatever was enqueued finishes before the lane is reused
+    c->lanes.inflight.fetch_sub(bytes);
     if (e == hipSuccess) memcpy(h_out, l->hcrc, n_pages * 4);
     lane_put(c, l);
     return map_err(e);

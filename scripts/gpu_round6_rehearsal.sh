@@ -1,11 +1,11 @@
-# Round-5 evidence in one GPU call, in the driver's order: every -m gpu test, smoke(), the
+# Round-6 evidence in one GPU call, in the driver's order: every -m gpu test, smoke(), the
 # bench with the driver's flags (its own live PMC traffic passes inside), then the same bench
 # command under rocprofv3 --kernel-trace --stats (no PMC: counters never ride with tracing; no host
 # legs: their page-kernel launches over staging batches would share the 16 GiB launches' stats row).
-# Each GPU step bounded; the first failure ends the call.  usage: bash scripts/gpu_round5_rehearsal.sh TAG
+# Each GPU step bounded; the first failure ends the call.  usage: bash scripts/gpu_round6_rehearsal.sh TAG
 set -u
 R=$(pwd)
-TAG=${1:-r05}
+TAG=${1:-r06}
 mkdir -p $R/gpurun_out
 if [ "${2:-}" != profile-only ]; then
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 420 --timeout-method thread > $R/gpurun_out/gpu_tests_$TAG.log 2>&1 || { echo TESTFAIL; tail -40 $R/gpurun_out/gpu_tests_$TAG.log; exit 1; }

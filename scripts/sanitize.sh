@@ -19,7 +19,7 @@ HIPCC="$ROCM/bin/hipcc"
 S=$R/build/san
 mkdir -p $S/obj
 SAN="-fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g"
-CXXF="-O1 -std=c++17 -fPIC -msse4.2 -Wall $SAN"
+CXXF="-O1 -std=c++17 -fPIC -msse4.2 -mpclmul -Wall $SAN"
 RT=$($CXX -print-file-name=libclang_rt.asan-x86_64.so)
 [ -f "$RT" ] || RT=$(ls $ROCM/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -1)
 cd $R/curve_amd/csrc

@@ -74,6 +74,28 @@ def test_fold_host(oracle, golden):
     assert CR.fold_host(np.array(s["crcs"], dtype=np.uint32), 4096) == oracle.crc32c(pages.tobytes())
 
 
+@pytest.mark.parametrize("page_bytes", [256, 512, 4096, 8192])
+def test_fold_host_every_count(oracle, page_bytes):
+    """cc_fold_host (four interleaved carry-less Horner chains merged at the
+    end) == CRC32 of the concatenation for every page count 1..40 (each
+    remainder of the 4-way split, the short path below 8) and 1024 (a 4 MiB slice)."""
+    data = oracle.splitmix64_bytes(0xF01D + page_bytes, 1024 * page_bytes)
+    crcs = oracle.page_crcs(data, page_bytes)
+    for n in list(range(1, 41)) + [1024]:
+        want = oracle.crc32c(data[:n * page_bytes].tobytes())
+        assert CR.fold_host(crcs[:n], page_bytes) == want, n
+
+
+def test_shift_random_registers(oracle):
+    """The carry-less multiply behind crc32c_shift / combine / zeros against the
+    oracle's GF(2) matrix squaring, over random registers and byte counts."""
+    rng = np.random.default_rng(0xC1)
+    for _ in range(300):
+        reg = int(rng.integers(0, 2**32))
+        n = int(rng.integers(0, 2**40)) if rng.random() < 0.5 else int(rng.integers(0, 70000))
+        assert C.shift(reg, n) == oracle.raw_shift(reg, n)
+
+
 @pytest.mark.parametrize("seed", range(5))
 def test_extend_iov_matches_concatenation(oracle, seed):
     """crc32c_extend_iov (the drop-in for braft::crc32(const butil::IOBuf&),
