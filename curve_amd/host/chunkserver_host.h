@@ -47,7 +47,14 @@ enum CHUNK_OP_STATUS {
 
 constexpr uint8_t FORMAT_VERSION = 1;     // datastore/define.h:39
 constexpr uint8_t FORMAT_VERSION_V2 = 2;  // datastore/define.h:40
-constexpr size_t kCpuHashMax = 64 << 10;  // hash ranges below this stay on the CPU primitive
+// Hash ranges below this stay on the CPU primitive.  Measured per call on the
+// MI355X box (bench.py scan_op.latency_by_size_1thread): below
+// ~512 KiB the CPU primitive (36 GiB/s a core) costs less host CPU AND less
+// latency than a GPU call (~10-12 us of host CPU, >= 22 us of latency); from
+// 1 MiB the GPU call costs less host CPU (16 vs 27 us at 1 MiB, 16 vs 110 us
+// for a 4 MiB scan slice) at about equal latency (4 MiB: 112 vs 108 us), and
+// from 16 MiB it is faster too (337 vs 431 us).
+constexpr size_t kCpuHashMax = 512 << 10;
 
 struct ChunkFileMetaPage {
     uint8_t version = FORMAT_VERSION_V2;
