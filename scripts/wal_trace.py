@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Per-wave timeline of range_flat_kernel in the bench's WAL-replay shape, from a
 trace build (scripts/patches/range_trace.py; never the shipped library): when each
-wave starts its first item, leaves its static pieces and ends, by XCD.
+wave enters the kernel, starts its first item, leaves its static pieces and ends,
+by XCD (times from the earliest entry), and the prologue's parts (tile counts,
+LDS fill, the wait for every tile count).
 usage: wal_trace.py LIB.so [--calls N]"""
 import ctypes
 import json
@@ -34,11 +36,12 @@ for c in range(40 + calls):
     if c < 40:
         continue
     torch.cuda.synchronize()
-    buf = np.zeros(4 * 8192, dtype=np.uint64)
+    buf = np.zeros(8 * 8192, dtype=np.uint64)
     assert L.cc_range_trace_read(buf.ctypes.data, buf.nbytes) == 0
-    t = buf.reshape(-1, 4)
+    t = buf.reshape(-1, 8)
     t = t[t[:, 2] != 0]
-    t0 = t[:, 0].min()
+    t0 = t[:, 4].min()
+    entry = (t[:, 4] - t0) / 100.0
     start = (t[:, 0] - t0) / 100.0  # us
     stat = (t[:, 1].astype(np.int64) - t0) / 100.0
     end = (t[:, 2] - t0) / 100.0
@@ -52,7 +55,11 @@ for c in range(40 + calls):
                       "us_per_block_static": round(float(np.median((stat[xcc == x] - start[xcc == x]) /
                                                                    np.maximum(blocks[xcc == x] - 16 * dyn[xcc == x], 1))), 3)}
              for x in sorted(set(xcc))}
-    res.append({"call": c - 40, "waves": int(len(t)), "start_us_p0_1_50_99_100": q(start),
+    res.append({"call": c - 40, "waves": int(len(t)), "entry_us_p0_1_50_99_100": q(entry),
+                "prologue_us": q(start - entry), "count_us": q((t[:, 5] - t[:, 4]) / 100.0),
+                "fill_us": q((t[:, 6] - t[:, 5]) / 100.0), "tile_wait_us": q((t[:, 7] - t[:, 6]) / 100.0),
+                "search_us": q((t[:, 0].astype(np.int64) - t[:, 7].astype(np.int64)) / 100.0),
+                "wait_done_us": q((t[:, 7] - t0) / 100.0), "start_us_p0_1_50_99_100": q(start),
                 "static_end_us": q(stat), "end_us": q(end), "blocks_per_wave": q(blocks), "dyn_chunks_per_wave": q(dyn),
                 "per_xcc": per_x})
 print(json.dumps(res, indent=1))
