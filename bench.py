@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--reads", type=int, default=65536, help="verify-on-read leg: reads per batch (0 = skip)")
     p.add_argument("--stream-chunks", type=int, default=10000, help="config-4 stream leg (0 = skip)")
     p.add_argument("--stream-chunks-per-rank", type=int, default=2000, help="N>1: streamed chunks per rank")
+    p.add_argument("--stream-distinct", type=int, default=10000,
+                   help="N=1 stream leg: distinct pinned 16 MiB data chunks (10000 = every chunk distinct, 156 GiB of "
+                        "pinned host memory; fewer if the host cannot spare that, see _host_chunk_budget)")
     p.add_argument("--file-chunks", type=int, default=128, help="datastore read-path leg (0 = skip)")
     p.add_argument("--file-passes", type=int, default=5, help="datastore read-path leg: passes per io-thread count")
     p.add_argument("--scan-op-threads", type=int, default=10,
@@ -339,15 +342,54 @@ def scan_op_leg(args):
     return res
 
 
-def _stream_sources(n, pool_n, rank=0):
-    """`pool_n` distinct pinned 16 MiB data chunks (re-referenced round robin:
-    10,000 distinct chunks would need 156 GiB of host RAM) and `n` DISTINCT
-    pinned metapages (sn = global chunk index), so every chunk FILE -- metapage
-    || data -- and its file CRC differ."""
+def _host_chunk_budget(want, margin=32 << 30):
+    """How many 16 MiB chunks of pinned host memory this process can take: `want`,
+    or fewer when MemAvailable or the cgroup's memory limit (less its current
+    use) minus `margin` is smaller -- never below 64."""
+    from curve_amd import crc as C
+    free = None
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemAvailable:"):
+                free = int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    for lim_f, cur_f in (("/sys/fs/cgroup/memory.max", "/sys/fs/cgroup/memory.current"),
+                         ("/sys/fs/cgroup/memory/memory.limit_in_bytes", "/sys/fs/cgroup/memory/memory.usage_in_bytes")):
+        try:
+            lim = open(lim_f).read().strip()
+            if lim != "max" and int(lim) < (1 << 60):
+                room = int(lim) - int(open(cur_f).read().strip())
+                free = room if free is None else min(free, room)
+            break
+        except (OSError, ValueError):
+            continue
+    if free is None:
+        return want
+    return max(64, min(want, (free - margin) // C.CHUNK_SIZE))
+
+
+def _stream_sources(n, pool_n, rank=0, dev=None):
+    """`pool_n` distinct pinned 16 MiB data chunks (re-referenced round robin
+    when fewer than n: 10,000 distinct chunks take 156 GiB of host RAM) and `n`
+    DISTINCT pinned metapages (sn = global chunk index), so every chunk FILE --
+    metapage || data -- and its file CRC differ.  The data are random bytes
+    made on the device (`dev`) 1 GiB at a time and copied down (a CPU random
+    fill of 16 GiB takes tens of seconds)."""
     from curve_amd import crc as C
     from curve_amd.chunkfile import ChunkFileMetaPage
     data = torch.empty((pool_n, C.CHUNK_SIZE), dtype=torch.uint8, pin_memory=True)
-    data.random_(0, 256)
+    if dev is None:
+        data.random_(0, 256)
+    else:
+        step = 64
+        tmp = torch.empty((min(step, pool_n), C.CHUNK_SIZE), dtype=torch.uint8, device=dev)
+        for k in range(0, pool_n, step):
+            m = min(step, pool_n - k)
+            tmp[:m].random_(0, 256)
+            data[k:k + m].copy_(tmp[:m])
+        torch.cuda.synchronize(dev)
+        del tmp
     meta = torch.zeros((n, C.META_PAGE_SIZE), dtype=torch.uint8, pin_memory=True)
     mn = meta.numpy()
     for i in range(n):
@@ -415,8 +457,9 @@ def stream_leg(args):
     checked afterwards against libcurvecrc's CPU primitive."""
     from curve_amd import crc as C
     from curve_amd.pool import copyset_layout
-    n, pool_n, per = args.stream_chunks, 64, 100
-    dn, mn, chunks = _stream_sources(n, pool_n)
+    n, per = args.stream_chunks, 100
+    pool_n = _host_chunk_budget(max(1, min(args.stream_distinct, n)))
+    dn, mn, chunks = _stream_sources(n, pool_n, dev=torch.device("cuda", 0))
     lay = copyset_layout(list(range(n)), [i // per for i in range(n)], [C.CHUNK_SIZE + C.META_PAGE_SIZE] * n)
     C.scan_host(chunks[:8])  # warm (staging)
     t0 = time.perf_counter()
@@ -429,7 +472,8 @@ def stream_leg(args):
            "seconds": round(el, 3), "copysets": lay.n_groups, "scan_maps": int(sc.size + mc.size),
            "digest": "device (fused epilogue, cc_scan_host_digest)",
            "crc_check": {"vs": "libcurvecrc CPU primitive", "mismatches": bad, "ok": not any(bad.values())},
-           "source": f"{n} distinct pinned metapages + {pool_n} distinct pinned 16 MiB data chunks (re-referenced)"}
+           "source": f"{n} distinct pinned metapages + {pool_n} distinct pinned 16 MiB data chunks "
+                     f"({pool_n * C.CHUNK_SIZE / GiB:.0f} GiB" + (", re-referenced round robin)" if pool_n < n else ")")}
     assert out["crc_check"]["ok"], f"stream leg CRC mismatch: {bad}"
     return out
 
