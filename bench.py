@@ -345,7 +345,7 @@ def scan_op_leg(args):
 def _host_chunk_budget(want, margin=32 << 30):
     """How many 16 MiB chunks of pinned host memory this process can take: `want`,
     or fewer when MemAvailable or the cgroup's memory limit (less its current
-    use) minus `margin` is smaller -- never below 64."""
+    use) minus `margin` is smaller -- never below min(64, want)."""
     from curve_amd import crc as C
     free = None
     try:
@@ -366,7 +366,7 @@ def _host_chunk_budget(want, margin=32 << 30):
             continue
     if free is None:
         return want
-    return max(64, min(want, (free - margin) // C.CHUNK_SIZE))
+    return max(min(64, want), min(want, (free - margin) // C.CHUNK_SIZE))
 
 
 def _stream_sources(n, pool_n, rank=0, dev=None):

@@ -30,3 +30,22 @@ def test_numa_binding_helpers_never_fail():
     r = bench.bind_to_gpu_numa(0)
     assert r["bound"] is False and r["why"]
     assert os.sched_getaffinity(0) == before
+
+
+def test_stream_distinct_bounded_by_free_host_memory():
+    """The C3 stream leg pins up to --stream-distinct 16 MiB chunks (156 GiB for
+    all 10,000 distinct): _host_chunk_budget keeps that under MemAvailable /
+    the cgroup limit less a margin, never below 64 chunks, never above the ask."""
+    sys.path.insert(0, ROOT)
+    import bench
+    want = 10000
+    got = bench._host_chunk_budget(want)
+    assert 64 <= got <= want
+    free = None
+    for line in open("/proc/meminfo"):
+        if line.startswith("MemAvailable:"):
+            free = int(line.split()[1]) * 1024
+    if free is not None:
+        assert got == want or got == 64 or got * (16 << 20) <= free
+    assert bench._host_chunk_budget(10) == 10
+    assert bench._host_chunk_budget(want, margin=1 << 62) == 64  # nothing to spare: the floor
