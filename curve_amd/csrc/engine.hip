@@ -2132,12 +2132,11 @@ uint32_t usable_cpus() {
 // Default reader count: half the usable CPUs (the HIP runtime's threads and the
 // caller need the rest), at least 2, at most kMaxDefaultReaders.
 constexpr uint32_t kMaxDefaultReaders = 8;
+// Computed per call (an affinity mask set after the first call -- a NUMA
+// binding -- counts; the mask and quota reads cost microseconds a batch call).
 uint32_t default_io_threads() {
-    static const uint32_t n = [] {
-        const uint32_t h = usable_cpus() / 2;
-        return h < 2 ? 2u : (h > kMaxDefaultReaders ? kMaxDefaultReaders : h);
-    }();
-    return n;
+    const uint32_t h = usable_cpus() / 2;
+    return h < 2 ? 2u : (h > kMaxDefaultReaders ? kMaxDefaultReaders : h);
 }
 
 int read_full(int fd, void* dst, size_t n, off_t off) {

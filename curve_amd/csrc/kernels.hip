@@ -1478,7 +1478,7 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
     const uint32_t c0 = lane << 2 & 0x7Cu;
     const uint32_t c1 = c0 | 0x10000u;
     const uint32_t cf = kFinBase + (lane << 2);
-    const uint32_t pb = a.page_bytes;
+    constexpr uint32_t pb = 256u * M;  // = a.page_bytes (launch_log_pages picks M = page_bytes / 256): shifts, not 64-bit multiplies
     // The workgroup's heads are cut among its waves by age.  Its waves sit 4 to a
     // SIMD (wave t on SIMD t % 4, the (t / 4)-th oldest there) and the SIMD
     // issues oldest-first: with equal shares the four age groups ended at 80, 92,
