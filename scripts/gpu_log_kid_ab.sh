@@ -5,7 +5,7 @@ R=$(pwd)
 A=$1; B=$2; TAG=${3:-ab}
 mkdir -p $R/gpurun_out
 O=$R/gpurun_out/log_kid_$TAG.txt
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "write_log or partial or probe" > $R/gpurun_out/log_kid_tests_$TAG.log 2>&1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "log or partial or write or probe" > $R/gpurun_out/log_kid_tests_$TAG.log 2>&1
 rc=$?; tail -2 $R/gpurun_out/log_kid_tests_$TAG.log; [ $rc = 0 ] || exit 1
 : > $O
 cd /tmp && export TMPDIR=/tmp

@@ -18,9 +18,9 @@ def rep(old, new):
     s = s.replace(old, new, 1)
 
 
-rep("""    if (hb0 >= hb1) return;
-    fill_lds<64 * WV>(tab, static_cast<const uint4*>(a.image));""", """    if (hb0 >= hb1) return;
-    fill_lds<64 * WV>(tab, static_cast<const uint4*>(a.image));
+rep("""    fill_lds<64 * WV>(tab, static_cast<const uint4*>(a.image));
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);""", """    fill_lds<64 * WV>(tab, static_cast<const uint4*>(a.image));
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();
     uint32_t tr_pages = 0, tr_steals = 0;""")
 rep("""            if (lane == 0) a.page_crcs[pg] = crc;
@@ -30,6 +30,7 @@ rep("""            if (lane == 0) a.page_crcs[pg] = crc;
 rep("""            if (!step(B, S1, pB, pgB, h + 1, ocB, A, S0, pA, pgA, ocA)) break;
         }
     }
+    group_next<WV>(a.nx, tab);
 }""", """            if (!step(B, S1, pB, pgB, h + 1, ocB, A, S0, pA, pgA, ocA)) break;
         }
     }
@@ -44,6 +45,7 @@ rep("""            if (!step(B, S1, pB, pgB, h + 1, ocB, A, S0, pA, pgA, ocA)) b
         tr[6] = tr_pages;
         tr[7] = tr_steals;
     }
+    group_next<WV>(a.nx, tab);
 }""")
 rep("""__device__ __forceinline__ uint32_t page_hash(""", """__device__ uint64_t g_log_trace[8 * 8192];
 __device__ __forceinline__ uint32_t page_hash(""")
