@@ -188,10 +188,6 @@ struct DevCtx : std::enable_shared_from_this<DevCtx> {
     };
     std::mutex log_mu;
     std::vector<LogTable> log_tabs;
-    // write-log page launches so far: each takes the next as its work-stealing
-    // epoch (kernels.h LogLaunch::steal_epoch), so words a launch finds from an
-    // earlier one never match
-    std::atomic<uint32_t> log_epoch{0};
     // the range kernel's scratch, one per stream (range_work): tile words, the
     // tail block and the split-range accumulators; range_mu is held over a
     // call's enqueue so the epoch order is the stream order
@@ -1457,11 +1453,6 @@ bool log_work(uint64_t n_updates, uint32_t max_len, uint32_t page_bytes, LogWork
 // when the log needs more than kLogTableCacheEntries slots (such a call takes a
 // table of its own, freed with it: one huge log must not pin device memory for
 // the rest of the process).  cc_engine_trim frees every cached table.
-uint32_t next_log_epoch(DevCtx* c) {
-    uint32_t e = c->log_epoch.fetch_add(1) + 1;
-    if (e == 0) e = c->log_epoch.fetch_add(1) + 1;  // 0 is what a cleared word holds
-    return e;
-}
 constexpr uint64_t kLogTableCacheEntries = 1ull << 23;  // 64 MiB a stream: logs of up to 1M pieces (512K two-page writes)
 DevCtx::LogTable* log_table(DevCtx* c, hipStream_t s, uint64_t entries, hipError_t* err) {
     *err = hipSuccess;
@@ -1483,14 +1474,13 @@ DevCtx::LogTable* log_table(DevCtx* c, hipStream_t s, uint64_t entries, hipError
     }
     if (!t->p) {
         void* p = nullptr;
-        if ((*err = hipMallocAsync(&p, kLogTableHeader + entries * 8 + kLogStealBytes, s)) != hipSuccess) return nullptr;
+        if ((*err = hipMallocAsync(&p, kLogTableHeader + entries * 8, s)) != hipSuccess) return nullptr;
         t->p = static_cast<unsigned char*>(p);
         t->entries = entries;
         t->dirty = true;
     }
     if (t->dirty) {
-        if ((*err = hipMemsetAsync(t->p, 0, kLogTableHeader + t->entries * 8 + kLogStealBytes, s)) != hipSuccess)
-            return nullptr;
+        if ((*err = hipMemsetAsync(t->p, 0, kLogTableHeader + t->entries * 8, s)) != hipSuccess) return nullptr;
         t->dirty = false;
     }
     return t;
@@ -1554,9 +1544,8 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
         a.clear_table = 1;
         a.table = reinterpret_cast<uint64_t*>(t->p + kLogTableHeader);
         a.table_mask = (uint32_t)(t->entries - 1);
-        a.steal = reinterpret_cast<unsigned long long*>(t->p + kLogTableHeader + t->entries * 8);
     } else {
-        const uint64_t bytes = kLogTableHeader + lw.table_entries * 8 + kLogStealBytes;
+        const uint64_t bytes = kLogTableHeader + lw.table_entries * 8;
         if ((e = hipMallocAsync(reinterpret_cast<void**>(&tmp), bytes, s)) != hipSuccess) return map_err(e);
         if ((e = hipMemsetAsync(tmp, 0, bytes, s)) != hipSuccess) {
             (void)hipFreeAsync(tmp, s);
@@ -1564,9 +1553,7 @@ int apply_log(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, const void
         }
         a.table = reinterpret_cast<uint64_t*>(tmp + kLogTableHeader);
         a.table_mask = (uint32_t)(lw.table_entries - 1);
-        a.steal = reinterpret_cast<unsigned long long*>(tmp + kLogTableHeader + lw.table_entries * 8);
     }
-    a.steal_epoch = next_log_epoch(c.get());
     e = launch_log_insert(a, s);
     if (e == hipSuccess) e = launch_log_pages(a, s);
     if (t && e != hipSuccess) t->dirty = true;  // the insert may have run: clear before the next use
@@ -1701,7 +1688,6 @@ int cc_apply_logs_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, co
     }
     unsigned char* w = static_cast<unsigned char*>(d_work);
     uint64_t* const t0 = reinterpret_cast<uint64_t*>(t->p + kLogTableHeader);
-    unsigned long long* const steal = reinterpret_cast<unsigned long long*>(t->p + kLogTableHeader + t->entries * 8);
     uint64_t* tabs[2] = {t0, t0 + W.table_entries};
     const uint32_t masks[2] = {(uint32_t)(W.table_entries - 1), (uint32_t)(W.table_entries - 1)};
     // the three chunk counters of the tail groupings: grouping kernel q takes
@@ -1784,8 +1770,6 @@ int cc_apply_logs_dev(void* d_pool, uint64_t pool_bytes, uint32_t page_bytes, co
                 grouped = true;
             }
         }
-        a.steal = steal;  // the page kernels of a stream run one at a time: one area serves them all
-        a.steal_epoch = next_log_epoch(c.get());
         e = launch_log_pages(a, s);
         r ^= 1;
     }

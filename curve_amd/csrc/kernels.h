@@ -174,13 +174,7 @@ struct LogLaunch {
     int delta;                  // 1: update the stored CRCs through linearity (reads touched rows only)
     LogInsert nx;               // the next batch's grouping, in this batch's page kernel (launch_log_pages)
     unsigned long long* zero_ctrs;  // log_insert_kernel zeroes these 3 words (the queue's chunk counters) or null
-    // work stealing in the full-mode page pass: {cut, progress} per wave of the
-    // grid (epoch << 32 | head index), zero when made; null = no stealing
-    unsigned long long* steal;
-    uint32_t steal_epoch;           // this launch's, unique per device (never 0)
 };
-constexpr uint64_t kLogStealWaves = 1024ull * 16;  // waves with steal words (a larger grid does not steal)
-constexpr uint64_t kLogStealBytes = kLogStealWaves * 128;  // {cut, progress}: up to a 128-byte line a wave
 hipError_t launch_log_insert(const LogLaunch& a, hipStream_t s);
 hipError_t launch_log_pages(const LogLaunch& a, hipStream_t s);
 // <= 64 writes of <= 2 pieces each in one launch (no table, no insert)

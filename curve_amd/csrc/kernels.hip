@@ -1489,9 +1489,6 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
     // (profiles/write_log_skew_ab_r03.txt): 33/27/22/18 = 32/28/22/18 =
     // 34/26/22/18 < 30/26/23/21 < 28/26/24/22 < 36/28/21/15 < equal.
     constexpr uint32_t kSkew[4] = {33, 27, 22, 18};
-    constexpr uint32_t kStealMargin = 3;  // pages past a victim's progress it may still do itself (its pipeline's reach)
-    constexpr uint32_t kStealMin = 4;     // fewer pages left are not worth a thief's metadata round trips
-    constexpr uint32_t kStealTries = 8;   // looks for a victim per wave at most
     auto wprefix = [&](uint32_t t) {  // sum of the weights of waves 0 .. t-1
         uint32_t p = 0;
         for (uint32_t u = 0; u < t; u++) p += kSkew[(u / 4) & 3];
@@ -1501,46 +1498,13 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
     const uint32_t H = hb0 + (uint32_t)((uint64_t)Hb * wprefix(wave + 1) / wsum);  // this wave: [first, H)
     const uint32_t first = hb0 + (uint32_t)((uint64_t)Hb * wprefix(wave) / wsum);
     constexpr uint32_t W = 1;  // lane k <- head base + k
-    // static shares, then work stealing (full mode).  A dynamic tail (the last
-    // 1/8 or 1/16 of the heads in chunks of 4-16 through one atomic counter, as
-    // the page kernel does) measured 7-19 % slower here (round 3), and round 4's
-    // stealing made every owner claim its tail pages with returning atomics.  Here
-    // an owner never waits on anything: it publishes its progress (a store a
-    // page) and reads its cut word with each page's loads; a wave done with its
-    // share takes the upper half of the remaining pages of the wave (of its
-    // workgroup and three others on its XCD) with the most left, lowering that
-    // wave's cut with one atomicMin, and the owner stops at the cut.  A page
-    // done twice (an owner past a cut it had not yet seen) is harmless: a full
-    // rehash applies source bytes and rehashes, so both write the same rows and
-    // CRC.  A thief skips pages whose table entry an owner already cleared.
-    // Delta mode does not steal (its CRC update reads the stored CRC: not
-    // idempotent).  Per-wave {cut, progress} words carry the launch's epoch.
-    constexpr bool kSteal = !Delta;
-    const uint64_t stag = (uint64_t)a.steal_epoch << 32;
-    unsigned long long* const my_steal =
-        (kSteal && a.steal && (uint64_t)gridDim.x * WV <= kLogStealWaves) ? a.steal + 2 * ((uint64_t)blockIdx.x * WV + wave)
-                                                                           : nullptr;
-    uint32_t vz0 = 0;
-    asm volatile("" : "+v"(vz0));  // opaque zero: uniform-address loads stay on the vector path
-    // where each step's cut load reads from (a dummy word without stealing: every step issues the same loads)
-    const unsigned long long* const cut_src =
-        my_steal ? my_steal : reinterpret_cast<const unsigned long long*>(a.seg_count);
-    if (my_steal && lane == 0) {
-        __hip_atomic_store(my_steal, stag | H, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the cut is visible before the progress word says "started"
-        __hip_atomic_store(my_steal + 1, stag | first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    uint32_t r0 = first, r1 = H;  // the range being worked: the wave's own share, then stolen ones
-    bool thief = false;
-    uint32_t cut_cur = H;  // the owner's cut as last read
-    uint32_t tries = 0;
-#pragma unroll 1
-    for (;;) {
-    bool stopped = false;
-    for (uint32_t base = r0; base < r1 && !stopped; base += 64u * W) {
+    // static shares only: a dynamic tail (the last 1/8 or 1/16 of the heads in
+    // chunks of 4-16 through one atomic counter, as the page kernel does) measured
+    // 7-19 % slower here (0.177-0.197 vs 0.165 ms a batch)
+    for (uint32_t base = first; base < H; base += 64u * W) {
         // lane k <- head base + k*W (clamped loads: no branches around them)
         const uint64_t ih = (uint64_t)base + (uint64_t)lane * W;
-        const bool hv = ih < r1;
+        const bool hv = ih < H;
         // the lane's head in its segment: the segment holding head `base` (lane
         // tl's segments, then the first of them past it), then a walk over the
         // (few) segments the batch spans
@@ -1564,7 +1528,7 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
             }
             seg = s;
             sbefore = st;
-            const uint32_t last = base + 63u < r1 - 1u ? base + 63u : r1 - 1u;
+            const uint32_t last = base + 63u < H - 1u ? base + 63u : H - 1u;
             for (;;) {
                 uint32_t v = sc[0];
 #pragma unroll
@@ -1583,23 +1547,9 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         // needed by pages with several pieces only, far behind)
         const uint2 hrec = reinterpret_cast<const uint2*>(a.heads)[(uint64_t)seg * a.seg_cap + (hi - sbefore)];
         const uint32_t hslot = hrec.x, claimer = hrec.y;
-        const unsigned long long ent0 = reinterpret_cast<const unsigned long long*>(a.table)[hslot];
+        const unsigned long long ent = reinterpret_cast<const unsigned long long*>(a.table)[hslot];
         const UpdateDesc d = a.upd[claimer / a.slots];
-        // full mode clears a page's slot after rehashing it (a thief reads it to
-        // know the page is done); delta mode here (the slot is this lane's alone:
-        // one head per page)
-        if (!kSteal && a.clear_table && hv) a.table[hslot] = 0ull;
-        // a thief's page whose slot an owner already cleared: done, skipped (nothing
-        // stored).  Its entry is rebuilt from the head record's claiming piece --
-        // the page that piece lies in (insert_piece: update claimer / slots, page
-        // dst / page_bytes + claimer % slots) and that piece as the list -- so every
-        // load the step issues for it stays inside the pool and the piece's source
-        // bytes, as for any page
-        const bool gone = ent0 == 0ull;
-        const uint64_t skips = __ballot(hv && gone);
-        const uint32_t gpage = (uint32_t)(d.dst / pb) + claimer % a.slots;
-        const unsigned long long ent =
-            gone ? ((uint64_t)(gpage + 1u) << 32 | (uint64_t)(claimer + 1u)) : ent0;
+        if (a.clear_table && hv) a.table[hslot] = 0ull;  // the slot is this lane's alone (one head per page)
         const uint32_t key = (uint32_t)(ent >> 32) - 1u;  // the page
         const uint32_t pfirst = (uint32_t)ent - 1u;       // the list head (the latest piece)
         const uint32_t nxt = a.next[pfirst];              // consumed by the several-piece path only
@@ -1637,7 +1587,6 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
         // delta mode: rows of page h to read (the head piece's if it is the
         // page's only piece) and the page's stored CRC (a vector load: a scalar
         // one would share lgkmcnt with the chain's LDS lookups)
-        unsigned long long cutw = stag | 0xFFFFFFFFull;  // the cut word a step checks (the first: nothing read yet)
         auto load_next = [&](uint32_t (&Y)[M], const Piece& py, uint32_t pgy, uint32_t h, uint32_t& ocy) {
             if constexpr (Delta) {
                 const PieceRows r = piece_rows(py);
@@ -1664,21 +1613,6 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
             py = head_piece(h1);
             load_next(Y, py, pgy, h1, ocy);
             fetch(SY, py);
-            if constexpr (kSteal) {
-                // the cut word for the next step's check, in flight with the next page's
-                // loads; this step checks the one that came with this page's
-                const unsigned long long cn = __hip_atomic_load(cut_src + vz0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t cv = readlane64(cutw, 0);
-                cutw = cn;
-                if (!thief && (cv >> 32) == (stag >> 32) && (uint32_t)cv < cut_cur) cut_cur = (uint32_t)cv;
-                if (!thief && base + hh >= cut_cur) {  // a thief has this page and the rest
-                    stopped = true;
-                    return false;
-                }
-                if (my_steal && !thief && lane == 0)
-                    __hip_atomic_store(my_steal + 1, stag | (base + hh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            const bool skip = (skips >> hh) & 1ull;
             const uint64_t pbase = (uint64_t)pg * pb;
             uint32_t dirty = 0;
             uint32_t O[Delta ? M : 1];
@@ -1686,9 +1620,7 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
 #pragma unroll
                 for (int j = 0; j < M; j++) O[j] = X[j];
             }
-            if (skip) {
-                // done by its owner: nothing merged, nothing stored
-            } else if ((singles >> hh) & 1ull) {
+            if ((singles >> hh) & 1ull) {
                 if constexpr (kRowSel) {
                     merge_edges<M>(X, dirty, SX, px, lane);
                 } else {
@@ -1780,9 +1712,7 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
             } else {
                 crc = wave_xor(apply_fin(tab, chain<M>(tab, X, c0, c1), cf)) ^ a.kconst;
             }
-            if (lane == 0 && !skip) a.page_crcs[pg] = crc;
-            if (kSteal && lane == 0 && !skip && a.clear_table)  // the page is done: its slot back to empty
-                a.table[__builtin_amdgcn_readlane(hslot, hh)] = 0ull;
+            if (lane == 0) a.page_crcs[pg] = crc;
             return more;
         };
         // the two register sets alternate (no copies): page k in one while page
@@ -1796,49 +1726,6 @@ __device__ __forceinline__ void log_pages_body(const LogLaunch& a, uint32_t* tab
             if (!step(A, S0, pA, pgA, h, ocA, B, S1, pB, pgB, ocB)) break;
             if (!step(B, S1, pB, pgB, h + 1, ocB, A, S0, pA, pgA, ocA)) break;
         }
-    }
-    // the next range: the upper half of what a victim has left
-    bool got = false;
-    while (my_steal && tries < kStealTries) {
-        tries++;
-        // lane l looks at wave l % WV of workgroup (this + 8 (l / WV)) % grid (this
-        // workgroup and three more on its XCD): its {cut, progress} words
-        const uint32_t G = gridDim.x;
-        const uint32_t vb = (blockIdx.x + 8u * (lane / WV)) % G, vw = lane % WV;
-        const unsigned long long* vs = a.steal + 2 * ((uint64_t)vb * WV + vw);
-        const unsigned long long cw = __hip_atomic_load(vs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long pw = __hip_atomic_load(vs + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t vb0 = (uint32_t)((uint64_t)Hall * vb / G);
-        const uint32_t vHb = (uint32_t)((uint64_t)Hall * (vb + 1) / G) - vb0;
-        const uint32_t vH = vb0 + (uint32_t)((uint64_t)vHb * wprefix(vw + 1) / wsum);  // its share's end
-        const bool ok = (cw >> 32) == (stag >> 32) && (pw >> 32) == (stag >> 32) && !(vb == blockIdx.x && vw == wave);
-        const uint32_t vcut = (uint32_t)cw < vH ? (uint32_t)cw : vH;
-        const uint32_t from = (uint32_t)pw + kStealMargin;
-        const uint32_t rem = ok && vcut > from ? vcut - from : 0u;
-        // the most pages left (ties: the lowest lane)
-        uint32_t k2 = rem << 6 | (63u - lane);
-#pragma unroll
-        for (int d = 32; d; d >>= 1) {
-            const uint32_t o = __shfl_xor(k2, d, 64);
-            k2 = o > k2 ? o : k2;
-        }
-        const uint32_t best = __builtin_amdgcn_readfirstlane(k2);
-        const uint32_t brem = best >> 6, bl = 63u - (best & 63u);
-        if (brem < kStealMin) break;
-        const uint32_t bcut = __builtin_amdgcn_readlane(vcut, bl), bH = __builtin_amdgcn_readlane(vH, bl);
-        const uint32_t c = bcut - brem / 2u;
-        unsigned long long old = 0;
-        if (lane == 0)
-            old = atomicMin(a.steal + 2 * ((uint64_t)((blockIdx.x + 8u * (bl / WV)) % G) * WV + bl % WV), stag | c);
-        old = readlane64(old, 0);
-        if ((old >> 32) != (stag >> 32) || (uint32_t)old <= c) continue;  // raced with another thief: look again
-        r0 = c;
-        r1 = (uint32_t)old < bH ? (uint32_t)old : bH;
-        thief = true;
-        got = true;
-        break;
-    }
-    if (!got) break;
     }
     group_next<WV>(a.nx, tab);
 }
