@@ -139,3 +139,24 @@ def test_lane_call_errors_leave_lanes_usable(oracle):
     rc, _, crcs, _, _ = bench.run_scan_ops(files, [0], [1 << 20], 3, "gpu")
     assert rc == 0
     _check(crcs, _want(oracle, files, [0], [1 << 20]), 3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("page_bytes", [256, 768, 4096, 8192, 1 << 20])
+def test_lane_and_slot_paths_by_page_size(oracle, page_bytes):
+    """cc_page_crc_host at every page geometry the ABI accepts, on both sides of
+    the lane limit (16 MiB: a lane of its own; above: the two shared staging
+    slots), pinned and pageable, the pageable buffer at an odd address (the
+    lane's staging copies it a 1 MiB piece at a time, the last piece partial):
+    every page CRC equal to the oracle's."""
+    import torch
+    from curve_amd import crc as C
+    rng = np.random.default_rng(page_bytes)
+    lane_pages = (16 << 20) // page_bytes
+    for n in sorted({1, 3, max(1, lane_pages // 3 + 1), lane_pages, lane_pages + 1}):
+        raw = rng.integers(0, 256, n * page_bytes + 3, dtype=np.uint8)
+        pages = raw[3:]  # pageable, not 4-byte aligned
+        want = oracle.page_crcs(pages, page_bytes, threads=8)
+        assert (C.page_crc_host(pages, page_bytes) == want).all(), (page_bytes, n, "pageable")
+        pinned = torch.from_numpy(np.ascontiguousarray(pages)).pin_memory()
+        assert (C.page_crc_host(pinned.numpy(), page_bytes) == want).all(), (page_bytes, n, "pinned")
