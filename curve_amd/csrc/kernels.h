@@ -231,7 +231,7 @@ struct ReadVerifyLaunch {
     const uint32_t* page_crcs;  // stored CRC per pool page
     uint32_t* bad_per_read;     // [n_reads] += mismatching pages; UINT32_MAX for a read beyond the pool
     unsigned long long* bad_total;
-    uint64_t* tiles;            // [kRangeTiles] epoch << 40 | pages of the tile
+    uint64_t* tiles;            // [kReadTiles] epoch << 40 | pages of the tile
     unsigned long long* tail;   // dynamic-tail counter slots (epoch % 2: this call's; the other zeroed for the next)
     uint32_t epoch;
     const void* image;
@@ -251,6 +251,10 @@ hipError_t launch_read_verify_small(const ReadVerifyLaunch& a, hipStream_t s);
 // call's words), the accumulators self-reset and each call zeroes the tail
 // counter slot the next call uses.
 constexpr uint32_t kRangeTiles = 1024;
+// verify on read counts its reads in fewer tiles (half the words every wave
+// polls; A/B round 6, profiles/range_tiles_ab_r06.txt); the scratch holds kRangeTiles
+constexpr uint32_t kReadTiles = 512;
+static_assert(kReadTiles <= kRangeTiles && kReadTiles % 64 == 0, "read tiles share the range scratch");
 struct RangeLaunch {
     const unsigned char* buf;
     const RangeDesc* ranges;

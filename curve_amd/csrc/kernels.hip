@@ -1954,7 +1954,7 @@ __device__ __forceinline__ uint64_t read_pages(const ReadVerifyLaunch& a, const 
 // Pages of tile t (reads [n t / T, n (t+1) / T)), uniform; mark: reads past the
 // pool get bad_per_read = UINT32_MAX (the tile's counting wave marks them).
 __device__ __forceinline__ uint64_t read_tile_count(const ReadVerifyLaunch& a, uint32_t t, uint32_t lane, bool mark) {
-    const uint64_t lo = a.n_reads * t / kRangeTiles, hi = a.n_reads * (t + 1) / kRangeTiles;
+    const uint64_t lo = a.n_reads * t / kReadTiles, hi = a.n_reads * (t + 1) / kReadTiles;
     uint64_t sum = 0;
     for (uint64_t i = lo + lane; i < hi; i += 64) {
         const RangeDesc r = a.reads[i];
@@ -1968,7 +1968,7 @@ __device__ __forceinline__ uint64_t read_tile_count(const ReadVerifyLaunch& a, u
 
 // Every page a read touches is one slot; the batch's slots are read 0's pages,
 // then read 1's, ...  ONE launch, scheduled as the range kernel is (§7): the
-// waves count kRangeTiles tiles of reads themselves (epoch-tagged words, a
+// waves count kReadTiles tiles of reads themselves (epoch-tagged words, a
 // bounded wait) and hold the counts in registers; wave w owns the slots
 // [Ts w / W, Ts (w+1) / W) at PAGE granularity (a read may be split over
 // waves; its mismatches are counted by atomics), the last T / kRvDynDiv slots
@@ -2000,7 +2000,7 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
     const uint64_t w = (uint64_t)blockIdx.x * kRvWaves + wave;
     const uint64_t tag = (uint64_t)a.epoch << kEpochShift;
     // this wave's tile counts, published before the LDS fill
-    for (uint64_t t = w; t < kRangeTiles; t += Wg) {
+    for (uint64_t t = w; t < kReadTiles; t += Wg) {
         const uint64_t cnt = read_tile_count(a, (uint32_t)t, lane, true);
         if (lane == 0) __hip_atomic_store(a.tiles + t, tag | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -2016,7 +2016,7 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
     uint32_t vz = 0;
     asm volatile("" : "+v"(vz));  // opaque zero: keeps uniform-address loads on the vector path
 
-    constexpr int kTpl = kRangeTiles / 64;
+    constexpr int kTpl = kReadTiles / 64;
     uint64_t tb[kTpl];
     wait_tiles<kTpl>(tb, a.tiles, tag, lane, [&](uint32_t t) { return read_tile_count(a, t, lane, false); });
     uint64_t lsum = 0;
@@ -2044,7 +2044,7 @@ __global__ __launch_bounds__(64 * kRvWaves) void read_verify_kernel(ReadVerifyLa
         bool have_rs = false;
         if (lo_slot < hi_slot) {
             const TileHit th = tile_of(cum, tb, lo_slot, lane);
-            base = n * th.tile / kRangeTiles;
+            base = n * th.tile / kReadTiles;
             S = th.before;
             // the tile's reads 64 at a time, to the group whose pages pass lo_slot
             for (;;) {

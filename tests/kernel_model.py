@@ -248,7 +248,7 @@ def range_accumulate(segs, nbs, contrib, rng):
     return out, left, stores
 
 
-def verify_flat_pages(counts, waves: int, tiles: int = 1024, dyn_div: int = 16, dyn_slots: int = 32,
+def verify_flat_pages(counts, waves: int, tiles: int = 512, dyn_div: int = 16, dyn_slots: int = 32,
                       min_slots: int = 8):
     """The page slots read_verify_kernel hashes, as (read, page-of-read) pairs in
     the order each share visits them: its static shares [Ts w / W, Ts (w+1) / W)
