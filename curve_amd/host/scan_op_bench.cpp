@@ -51,8 +51,7 @@ extern "C" int sob_run(uint32_t threads, const void* const* bufs, const uint64_t
         const unsigned char* base = static_cast<const unsigned char*>(bufs[t]);
         std::vector<uint32_t> pages;
         ready.fetch_add(1);
-        while (!go.load(std::memory_order_acquire)) {
-        }
+        while (!go.load(std::memory_order_acquire)) std::this_thread::yield();  // before the timed window
         const double c0 = now_s(CLOCK_THREAD_CPUTIME_ID);
         for (uint32_t i = 0; i < calls; i++) {
             const unsigned char* p = base + op_off[i % n_ops];
@@ -82,8 +81,7 @@ extern "C" int sob_run(uint32_t threads, const void* const* bufs, const uint64_t
     };
     std::vector<std::thread> ts;
     for (uint32_t t = 0; t < threads; t++) ts.emplace_back(body, t);
-    while (ready.load() < threads) {
-    }
+    while (ready.load() < threads) std::this_thread::yield();
     const double p0 = now_s(CLOCK_PROCESS_CPUTIME_ID);
     start = now_s(CLOCK_MONOTONIC);
     go.store(true, std::memory_order_release);
