@@ -147,7 +147,8 @@ def cpu_baseline(pool, args, rank):
     DRAM-resident sample of the same workload: `--cpu-sample-chunks` 16 MiB
     chunks (default 256 = 4 GiB, far above the L3) copied from HBM.  Timed at
     1 thread and at every core this process may use (page-partitioned), plus a
-    cache-resident microbench of libcurvecrc's own CPU primitive (3-way crc32q)
+    cache-resident microbench of libcurvecrc's own CPU primitive (VPCLMULQDQ
+    fold where the CPU has it, else 3-way crc32q; `libcurvecrc_path` says which)
     against the single-stream oracle at 4 KiB and 64 KiB per call."""
     import ctypes
     import sys
@@ -179,10 +180,11 @@ def cpu_baseline(pool, args, rank):
     buf = host[0, : 1 << 16]
     micro = {}
     for n in (4096, 65536):
-        for name, fn in (("oracle_single_stream", L.oc_crc32c_sse42), ("libcurvecrc_3way", P.crc32c_extend)):
+        for name, fn in (("oracle_single_stream", L.oc_crc32c_sse42), ("libcurvecrc", P.crc32c_extend)):
             it = max(1, (2 << 30) // n)  # 2 GiB per measurement
             t = L.oc_time_calls(ctypes.cast(fn, ctypes.c_void_p).value, buf.ctypes.data, n, it, None)
             micro[f"{name}_{n // 1024}KiB_GiBps"] = round(it * n / GiB / t, 2)
+    micro["libcurvecrc_path"] = cpu_primitive_path()
     v1, nb1, el1 = res[1]
     vN, nbN, elN = res[threads_all]
     return {
@@ -197,6 +199,23 @@ def cpu_baseline(pool, args, rank):
         "cpu_model": cpu_model(),
         "per_call_cache_resident": micro,
     }
+
+
+def cpu_primitive_path():
+    """Which loop crc32c_cpu.cpp's raw_update runs here: its run-time check
+    (avx512f + vpclmulqdq, CURVE_CRC_NO_FOLD unset) restated from /proc/cpuinfo."""
+    flags = set()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("flags"):
+                    flags = set(line.split(":", 1)[1].split())
+                    break
+    except OSError:
+        pass
+    off = os.environ.get("CURVE_CRC_NO_FOLD", "")
+    fold = {"avx512f", "vpclmulqdq", "pclmulqdq"} <= flags and not (off and off != "0")
+    return "vpclmulqdq fold (>= 256 B)" if fold else "3-way crc32q"
 
 
 def cpu_model():

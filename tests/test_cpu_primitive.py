@@ -26,7 +26,7 @@ def test_reference_chains(golden):
     assert crc == 599727352
 
 
-@pytest.mark.parametrize("n", [0, 1, 7, 8, 15, 16, 63, 503, 504, 768, 1008, 1536, 2040, 3072, 4080, 4095, 4096, 4104,
+@pytest.mark.parametrize("n", [0, 1, 7, 8, 15, 16, 63, 255, 256, 257, 319, 503, 504, 511, 512, 513, 767, 768, 1023, 1024, 1279, 1008, 1536, 2040, 3072, 4080, 4095, 4096, 4104,
                                6144, 8191, 12287, 12288, 12289, 3 * 4096 * 5 + 13, 1 << 20])
 def test_lengths_and_alignments(oracle, n):
     rng = np.random.default_rng(n)
@@ -124,3 +124,41 @@ def test_slice_fold_batched(oracle):
         assert got.tolist() == want
     with pytest.raises(CR.CurveCrcError):
         CR.slice_fold(pc[:10], 4, 4096)
+
+
+_BOTH_PATHS = """
+import sys, numpy as np, curve_amd as C
+rng = np.random.default_rng(5)
+out = []
+for n in [0, 1, 200, 255, 256, 257, 300, 511, 512, 513, 767, 768, 769, 1024, 1279, 1280, 1536, 4096, 65535, 65536, 65537]:
+    buf = rng.integers(0, 256, n + 64, dtype=np.uint8)
+    for off in (0, 1, 5, 13, 63):
+        out.append(C.CRC32(int(rng.integers(0, 2**32)), buf[off:off + n].tobytes()))
+print(" ".join(map(str, out)))
+"""
+
+
+def test_fold_and_crc32q_paths_agree(oracle):
+    """crc32c_cpu.cpp's VPCLMULQDQ fold (used when the CPU has it) and the
+    3-way crc32q loop (CURVE_CRC_NO_FOLD=1) give the same values, and both
+    equal the oracle's on the same seeded inputs."""
+    import os
+    import subprocess
+    import sys
+    runs = []
+    for off in ("0", "1"):
+        env = dict(os.environ, CURVE_CRC_NO_FOLD=off)
+        r = subprocess.run([sys.executable, "-c", _BOTH_PATHS], env=env, capture_output=True, text=True, timeout=120,
+                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert r.returncode == 0, r.stderr
+        runs.append(r.stdout.split())
+    assert runs[0] == runs[1]
+    rng = np.random.default_rng(5)
+    want = []
+    for n in [0, 1, 200, 255, 256, 257, 300, 511, 512, 513, 767, 768, 769, 1024, 1279, 1280, 1536, 4096, 65535, 65536,
+              65537]:
+        buf = rng.integers(0, 256, n + 64, dtype=np.uint8)
+        for off in (0, 1, 5, 13, 63):
+            seed = int(rng.integers(0, 2**32))
+            want.append(str(oracle.crc32c(buf[off:off + n].tobytes(), seed)))
+    assert runs[0] == want
