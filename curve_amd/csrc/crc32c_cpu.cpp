@@ -106,13 +106,29 @@ inline uint64_t three_way(uint64_t l, const unsigned char* p, const ShiftTables&
 // pinned by tests/test_cpu_primitive.py -- and XORed onto the lane D bits later.
 // Eight accumulators fold 512 bytes a step; at the end the accumulators fold
 // into one 16-byte lane, whose CRC (register 0) is the register of the whole.
+// The fold issues two 512-bit carry-less multiplies per 64 bytes, and on the
+// hosts measured that port, not the loads, sets the rate (4, 8 and 16
+// accumulators all ran at ~74 GiB/s, scripts/fold_accs_sweep.cpp).  The crc32
+// instruction runs on another port, so a split runs both: of M steps of
+// kStep bytes, the fold takes the first 512*M bytes and three crc32q streams
+// take kStreamQ qwords a step each from the three stretches after them; the
+// four registers are joined by x^(8*stretch) multiplies.  kStreamQ = 10 was the
+// best of 6..16 on the MI355X host (EPYC 9575F): 98 vs 60-74 GiB/s at 64 KiB.
+// Splits of kSplitMinSteps..kSplitMaxSteps steps take precomputed constants.
+constexpr int kStreamQ = 10;
+constexpr size_t kStep = 512 + 3 * 8 * kStreamQ;
+constexpr size_t kSplitMinSteps = 8, kSplitMaxSteps = 64;
+
 struct FoldKeys {
     uint64_t k[5][2];  // distances 4096, 2048, 512, 384, 256 bits; 128 below
     uint64_t k128[2];
+    uint32_t split[kSplitMaxSteps + 1][3];  // x^(8*s), x^(16*s), x^(24*s) for the stretch s of M steps
     FoldKeys() {
         const uint64_t d[5] = {4096, 2048, 512, 384, 256};
         for (int i = 0; i < 5; i++) k[i][0] = cc::xpow(d[i] + 31), k[i][1] = cc::xpow(d[i] - 33);
         k128[0] = cc::xpow(128 + 31), k128[1] = cc::xpow(128 - 33);
+        for (size_t m = 0; m <= kSplitMaxSteps; m++)
+            for (int j = 0; j < 3; j++) split[m][j] = cc::xpow(64ull * kStreamQ * m * (j + 1));
     }
 };
 const FoldKeys& fold_keys() {
@@ -140,8 +156,84 @@ CC_FOLD_TARGET inline __m512i keys512(const uint64_t (&k)[2]) {
                             (long long)k[0], (long long)k[1], (long long)k[0]);
 }
 
+CC_FOLD_TARGET inline uint32_t reduce8(__m512i (&x)[8], const FoldKeys& fk) {
+    // eight accumulators (x[7] the last 64 bytes) to one register: fold each onto
+    // the next, then the last zmm's four lanes onto its top lane
+    const __m512i k512 = keys512(fk.k[2]);
+    for (int i = 1; i < 8; i++) x[i] = fold512(x[i - 1], k512, x[i]);
+    __m128i v = _mm512_extracti32x4_epi32(x[7], 3);
+    v = fold128(_mm512_extracti32x4_epi32(x[7], 0), fk.k[3], v);
+    v = fold128(_mm512_extracti32x4_epi32(x[7], 1), fk.k[4], v);
+    v = fold128(_mm512_extracti32x4_epi32(x[7], 2), fk.k128, v);
+    const uint64_t l = _mm_crc32_u64(0, (uint64_t)_mm_cvtsi128_si64(v));
+    return static_cast<uint32_t>(_mm_crc32_u64(l, (uint64_t)_mm_extract_epi64(v, 1)));
+}
+
+// raw register update over [p, p + M*kStep), M >= kSplitMinSteps
+CC_FOLD_TARGET uint32_t fold_split(uint32_t reg, const unsigned char* p, size_t M) {
+    const FoldKeys& fk = fold_keys();
+    const size_t C = 8 * kStreamQ * M;  // one stream's stretch
+    const unsigned char* s = p + 512 * M;
+    __m512i x[8];
+    for (int i = 0; i < 8; i++) x[i] = _mm512_loadu_si512(p + 64 * i);
+    x[0] = _mm512_xor_si512(x[0], _mm512_castsi128_si512(_mm_cvtsi32_si128((int)reg)));
+    uint64_t a = 0, b = 0, c = 0;
+    const __m512i k4096 = keys512(fk.k[0]);
+    for (size_t m = 0;;) {
+        for (int q = 0; q < kStreamQ; q++) {
+            a = _mm_crc32_u64(a, load64(s + 8 * q));
+            b = _mm_crc32_u64(b, load64(s + C + 8 * q));
+            c = _mm_crc32_u64(c, load64(s + 2 * C + 8 * q));
+        }
+        s += 8 * kStreamQ;
+        if (++m == M) break;
+        p += 512;
+        for (int i = 0; i < 8; i++) x[i] = fold512(x[i], k4096, _mm512_loadu_si512(p + 64 * i));
+    }
+    uint32_t k[3];
+    if (M <= kSplitMaxSteps) {
+        k[0] = fk.split[M][0], k[1] = fk.split[M][1], k[2] = fk.split[M][2];
+    } else {  // ~20 multiplies, against >= 48 KiB of data
+        k[0] = xpow_clmul(8 * C), k[1] = mulmod_clmul(k[0], k[0]), k[2] = mulmod_clmul(k[1], k[0]);
+    }
+    return mulmod_clmul(k[2], reduce8(x, fk)) ^ mulmod_clmul(k[1], static_cast<uint32_t>(a)) ^
+           mulmod_clmul(k[0], static_cast<uint32_t>(b)) ^ static_cast<uint32_t>(c);
+}
+
+// The split pays where crc32 and the carry-less multiply issue on different
+// pipes (AMD Zen: +30 % at 64 KiB on the EPYC 9575F); on the Intel Xeon of the
+// build container the split ran slower than the fold alone, so it stays off there.
+// CURVE_CRC_FOLD_SPLIT=1 / =0 forces it on / off (tests run every path on any host).
+bool split_pays() {
+    static const bool on = [] {
+        const char* f = getenv("CURVE_CRC_FOLD_SPLIT");
+        if (f && f[0]) return f[0] != '0';
+        __builtin_cpu_init();
+        return __builtin_cpu_is("amd") != 0;
+    }();
+    return on;
+}
+
 // raw register update over [p, p+n), n >= kFoldMin; leaves n % 256 bytes to crc32q
 CC_FOLD_TARGET uint32_t fold_update(uint32_t reg, const unsigned char* p, size_t n) {
+    if (n / kStep >= kSplitMinSteps && split_pays()) {
+        // one split for the whole buffer: four long streams, which the hardware
+        // prefetchers follow (48 KiB splits chained ran 73 vs 97 GiB/s at 4 MiB)
+        const size_t M = n / kStep;
+        reg = fold_split(reg, p, M);
+        p += M * kStep;
+        n -= M * kStep;
+        if (n < kFoldMin) {
+            uint64_t l = reg;
+            while (n >= 8) {
+                l = _mm_crc32_u64(l, load64(p));
+                p += 8;
+                n -= 8;
+            }
+            while (n--) l = _mm_crc32_u8(static_cast<uint32_t>(l), *p++);
+            return static_cast<uint32_t>(l);
+        }
+    }
     const FoldKeys& fk = fold_keys();
     __m512i x0 = _mm512_loadu_si512(p), x1 = _mm512_loadu_si512(p + 64), x2 = _mm512_loadu_si512(p + 128),
             x3 = _mm512_loadu_si512(p + 192);

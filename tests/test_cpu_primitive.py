@@ -126,37 +126,41 @@ def test_slice_fold_batched(oracle):
         CR.slice_fold(pc[:10], 4, 4096)
 
 
+# around each path's edges: fold from 256 B; the fold + crc32q split from 8 steps of 752 B, at most 64 a split
+_PATH_LENGTHS = [0, 1, 200, 255, 256, 257, 300, 511, 512, 513, 767, 768, 769, 1024, 1279, 1280, 1536, 3007, 3008, 3009,
+                 3263, 3264, 3760, 4096, 6015, 6016, 6017, 6271, 6272, 9999, 48127, 48128, 48129, 48384,
+                 65535, 65536, 65537, 96256, 96256 + 6016, (1 << 20) + 4101]
 _BOTH_PATHS = """
 import sys, numpy as np, curve_amd as C
 rng = np.random.default_rng(5)
 out = []
-for n in [0, 1, 200, 255, 256, 257, 300, 511, 512, 513, 767, 768, 769, 1024, 1279, 1280, 1536, 4096, 65535, 65536, 65537]:
+for n in %s:
     buf = rng.integers(0, 256, n + 64, dtype=np.uint8)
     for off in (0, 1, 5, 13, 63):
         out.append(C.CRC32(int(rng.integers(0, 2**32)), buf[off:off + n].tobytes()))
 print(" ".join(map(str, out)))
-"""
+""" % _PATH_LENGTHS
 
 
 def test_fold_and_crc32q_paths_agree(oracle):
-    """crc32c_cpu.cpp's VPCLMULQDQ fold (used when the CPU has it) and the
-    3-way crc32q loop (CURVE_CRC_NO_FOLD=1) give the same values, and both
-    equal the oracle's on the same seeded inputs."""
+    """crc32c_cpu.cpp's VPCLMULQDQ fold (used when the CPU has it), the fold +
+    crc32q split (AMD hosts; CURVE_CRC_FOLD_SPLIT=1 forces it) and the 3-way
+    crc32q loop (CURVE_CRC_NO_FOLD=1) give the same values, and all equal the
+    oracle's on the same seeded inputs."""
     import os
     import subprocess
     import sys
     runs = []
-    for off in ("0", "1"):
-        env = dict(os.environ, CURVE_CRC_NO_FOLD=off)
+    for no_fold, split in (("0", "0"), ("0", "1"), ("1", "0")):
+        env = dict(os.environ, CURVE_CRC_NO_FOLD=no_fold, CURVE_CRC_FOLD_SPLIT=split)
         r = subprocess.run([sys.executable, "-c", _BOTH_PATHS], env=env, capture_output=True, text=True, timeout=120,
                            cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         assert r.returncode == 0, r.stderr
         runs.append(r.stdout.split())
-    assert runs[0] == runs[1]
+    assert runs[0] == runs[1] == runs[2]
     rng = np.random.default_rng(5)
     want = []
-    for n in [0, 1, 200, 255, 256, 257, 300, 511, 512, 513, 767, 768, 769, 1024, 1279, 1280, 1536, 4096, 65535, 65536,
-              65537]:
+    for n in _PATH_LENGTHS:
         buf = rng.integers(0, 256, n + 64, dtype=np.uint8)
         for off in (0, 1, 5, 13, 63):
             seed = int(rng.integers(0, 2**32))
