@@ -328,7 +328,7 @@ def scan_op_leg(args):
         res["threads"][str(nt)] = per
     # one thread's per-call latency by size (the cutoff): median of `n` calls
     sweep = {}
-    for size in (4096, 16384, 65536, 262144, 512 << 10, 1 << 20, 4 << 20, 16 << 20):
+    for size in (4096, 16384, 65536, 262144, 512 << 10, 1 << 20, 2 << 20, 4 << 20, 16 << 20):
         row = {}
         for mode in ("cpu", "gpu"):
             n = 64 if size >= (4 << 20) else 200

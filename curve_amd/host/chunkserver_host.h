@@ -48,13 +48,13 @@ enum CHUNK_OP_STATUS {
 constexpr uint8_t FORMAT_VERSION = 1;     // datastore/define.h:39
 constexpr uint8_t FORMAT_VERSION_V2 = 2;  // datastore/define.h:40
 // Hash ranges below this stay on the CPU primitive.  Measured per call on the
-// MI355X box (bench.py scan_op.latency_by_size_1thread): below
-// ~512 KiB the CPU primitive (36 GiB/s a core) costs less host CPU AND less
-// latency than a GPU call (~10-12 us of host CPU, >= 22 us of latency); from
-// 1 MiB the GPU call costs less host CPU (16 vs 27 us at 1 MiB, 16 vs 110 us
-// for a 4 MiB scan slice) at about equal latency (4 MiB: 112 vs 108 us), and
-// from 16 MiB it is faster too (337 vs 431 us).
-constexpr size_t kCpuHashMax = 512 << 10;
+// MI355X box (bench.py scan_op.latency_by_size_1thread), with the
+// primitive's fold + crc32q split (~100 GiB/s a core on the EPYC host): the CPU
+// call is faster at every size (4 MiB: 39 vs 113 us; 16 MiB: 162 vs 336 us), and
+// a GPU call (~12-18 us of host CPU whatever its size) costs less host CPU from
+// ~2 MiB (2 MiB: 18 vs 19 us; a 4 MiB scan slice: 15 vs 39 us).  The cutoff
+// routes for host CPU, since the reference paces its scan anyway.
+constexpr size_t kCpuHashMax = 2 << 20;
 
 struct ChunkFileMetaPage {
     uint8_t version = FORMAT_VERSION_V2;
