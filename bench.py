@@ -202,20 +202,27 @@ def cpu_baseline(pool, args, rank):
 
 
 def cpu_primitive_path():
-    """Which loop crc32c_cpu.cpp's raw_update runs here: its run-time check
-    (avx512f + vpclmulqdq, CURVE_CRC_NO_FOLD unset) restated from /proc/cpuinfo."""
-    flags = set()
+    """Which loop crc32c_cpu.cpp's raw_update runs here: its run-time checks
+    (avx512f + vpclmulqdq, CURVE_CRC_NO_FOLD unset; the split on AMD unless
+    CURVE_CRC_FOLD_SPLIT says otherwise) restated from /proc/cpuinfo."""
+    flags, vendor = set(), ""
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
+                if line.startswith("vendor_id") and not vendor:
+                    vendor = line.split(":", 1)[1].strip()
                 if line.startswith("flags"):
                     flags = set(line.split(":", 1)[1].split())
                     break
     except OSError:
         pass
     off = os.environ.get("CURVE_CRC_NO_FOLD", "")
-    fold = {"avx512f", "vpclmulqdq", "pclmulqdq"} <= flags and not (off and off != "0")
-    return "vpclmulqdq fold (>= 256 B)" if fold else "3-way crc32q"
+    if not ({"avx512f", "vpclmulqdq", "pclmulqdq"} <= flags) or (off and off != "0"):
+        return "3-way crc32q"
+    sp = os.environ.get("CURVE_CRC_FOLD_SPLIT", "")
+    split = sp != "0" if sp else vendor == "AuthenticAMD"
+    return ("vpclmulqdq fold (>= 256 B) + crc32q split (>= 6016 B)" if split
+            else "vpclmulqdq fold (>= 256 B)")
 
 
 def cpu_model():
