@@ -47,3 +47,27 @@ def test_reader_pool_under_thread_sanitizer(tmp_path):
                        env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "reader_pool_stress: ok" in r.stdout and "ThreadSanitizer" not in r.stderr
+
+
+@pytest.mark.parametrize("mode", [{}, {"CURVE_CRC_FOLD_SPLIT": "1"}, {"CURVE_CRC_FOLD_SPLIT": "0"},
+                                  {"CURVE_CRC_NO_FOLD": "1"}])
+def test_cpu_primitive_loops_under_address_sanitizer(tmp_path, mode):
+    """Every loop of the CPU primitive (csrc/crc32c_cpu.cpp, built from source
+    with ASan/UBSan) over buffers of their exact size, at each loop's edges and
+    three alignments (tests/native/crc_cpu_bounds.cpp): no load past a buffer's
+    end, values equal to a bitwise CRC32C.  Host only."""
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("no g++")
+    exe = str(tmp_path / "crc_cpu_bounds")
+    b = subprocess.run([cxx, "-O1", "-g", "-std=c++17", "-msse4.2", "-mpclmul", "-fsanitize=address,undefined",
+                        "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "include"),
+                        "-o", exe, os.path.join(ROOT, "curve_amd", "csrc", "crc32c_cpu.cpp"),
+                        os.path.join(ROOT, "tests", "native", "crc_cpu_bounds.cpp")], capture_output=True, text=True)
+    if b.returncode != 0 and "asan" in (b.stderr or "").lower():
+        pytest.skip("no AddressSanitizer runtime")
+    assert b.returncode == 0, b.stderr
+    env = {k: v for k, v in os.environ.items() if not k.startswith("CURVE_CRC_")}
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=dict(env, **mode))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "crc_cpu_bounds: ok" in r.stdout
